@@ -1,0 +1,337 @@
+/*
+ * C ABI of the MI355X-native FlashAttention-2 library (libflash_attn_mi355x.so).
+ *
+ * This is the drop-in boundary for the hot path.  Each entry point replaces the
+ * entry of the same name in the reference's Paddle C ABI (reference
+ * csrc/capi/flash_attn.h) with an identical argument list, except that the
+ * stream is a hipStream_t instead of a cudaStream_t:
+ *
+ *   flash_attn_fwd         <- reference csrc/capi/flash_attn.h:11-55
+ *   flash_attn_varlen_fwd  <- reference csrc/capi/flash_attn.h:57-98
+ *   flash_attn_bwd         <- reference csrc/capi/flash_attn.h:100-161
+ *   flash_attn_varlen_bwd  <- reference csrc/capi/flash_attn.h:163-221
+ *   flash_attn_error       <- reference csrc/capi/flash_attn.h:315
+ *
+ * Conventions (reference csrc/capi/flash_attn.cu:29-96, 576-1105):
+ *   - every buffer is a caller-owned device pointer; strides are in ELEMENTS;
+ *   - calls are stream-ordered and never synchronise;
+ *   - a call returns false on error and leaves a thread-local message readable
+ *     through flash_attn_error();
+ *   - head_size % 8 == 0, head_size <= 256, num_heads % num_heads_k == 0;
+ *   - the Paddle dense-mask / FlashMask arguments are accepted for ABI
+ *     compatibility but must be NULL (out of scope for this build: the call
+ *     fails with a message otherwise);
+ *   - backward: softmax_d (b, h, seqlen_q_rounded) fp32 and dq_accum
+ *     (b, h, seqlen_q_rounded, head_size_rounded) fp32 are caller-owned
+ *     workspaces; for MQA/GQA the caller passes dk/dv with num_heads heads
+ *     ("expanded", reference flash_api.cpp:628-635) and sums the groups itself;
+ *   - num_splits is accepted; the MI355X backward is deterministic in dK/dV for
+ *     every value (each workgroup owns its key block), dQ is accumulated with
+ *     fp32 atomics as in the reference.
+ *
+ * MI355X extensions (no reference counterpart):
+ *   flash_attn_bwd_gqa / flash_attn_varlen_bwd_gqa take the same arguments as
+ *   the reference entries but write dk/dv with num_heads_k heads, summing each
+ *   query-head group inside the kernel (no expanded buffers, no extra HBM pass:
+ *   replaces the at::sum_out of reference flash_api.cpp:682-686, 900-904).
+ *   flash_attn_block_size reports the tile sizes the launchers use.
+ */
+#ifndef FLASH_ATTN_MI355X_H_
+#define FLASH_ATTN_MI355X_H_
+
+#include <hip/hip_runtime.h>
+#include <stdbool.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+bool flash_attn_fwd(const void * const q,
+                    const void * const k,
+                    const void * const v,
+                    void * const rng_state,
+                    void * const out,
+                    void * const softmax_ptr,
+                    void * const softmax_lse_ptr,
+                    const int batch_size,
+                    const int seqlen_q,
+                    const int seqlen_k,
+                    const int seqlen_q_rounded,
+                    const int seqlen_k_rounded,
+                    const int num_heads,
+                    const int num_heads_k,
+                    const int head_size,
+                    const int head_size_rounded,
+                    const float p_dropout,
+                    const float softmax_scale,
+                    const float softmax_unscale,
+                    const bool is_causal,
+                    const bool return_softmax,
+                    const bool is_bf16,
+                    hipStream_t stream,
+                    uint64_t seed,
+                    uint64_t offset,
+                    const void * const attn_mask,
+                    const int64_t * const mask_dims,
+                    const void * const flashmask_downstart_ptr,
+                    const int64_t * const flashmask_dims,
+                    const void * const flashmask_upend_ptr,
+                    const void * const flashmask_downend_ptr,
+                    const void * const flashmask_upstart_ptr,
+                    const void * const flashmask_maxmin_ptr,
+                    const int q_row_stride,
+                    const int k_row_stride,
+                    const int v_row_stride,
+                    const int q_head_stride,
+                    const int k_head_stride,
+                    const int v_head_stride,
+                    const int o_row_stride,
+                    const int o_head_stride,
+                    const int q_batch_stride,
+                    const int k_batch_stride,
+                    const int v_batch_stride,
+                    const int o_batch_stride);
+
+bool flash_attn_varlen_fwd(const void * const q,
+                           const void * const k,
+                           const void * const v,
+                           const int32_t * const cu_seqlens_q,
+                           const int32_t * const cu_seqlens_k,
+                           void * const rng_state,
+                           void * const out,
+                           void * const softmax_ptr,
+                           void * const softmax_lse_ptr,
+                           const int batch_size,
+                           const int max_seqlen_q,
+                           const int max_seqlen_k,
+                           const int seqlen_q_rounded,
+                           const int seqlen_k_rounded,
+                           const int num_heads,
+                           const int num_heads_k,
+                           const int head_size,
+                           const int head_size_rounded,
+                           const float p_dropout,
+                           const float softmax_scale,
+                           const float softmax_unscale,
+                           const bool is_causal,
+                           const bool return_softmax,
+                           const bool is_bf16,
+                           hipStream_t stream,
+                           uint64_t seed,
+                           uint64_t offset,
+                           const void * const attn_mask,
+                           const void * const mask_dims,
+                           const int q_row_stride,
+                           const int k_row_stride,
+                           const int v_row_stride,
+                           const int q_head_stride,
+                           const int k_head_stride,
+                           const int v_head_stride,
+                           const int o_row_stride,
+                           const int o_head_stride,
+                           const int q_batch_stride,
+                           const int k_batch_stride,
+                           const int v_batch_stride,
+                           const int o_batch_stride,
+                           bool varlen_padded_input);
+
+bool flash_attn_bwd(const void * const dout,
+                    const void * const q,
+                    const void * const k,
+                    const void * const v,
+                    const void * const out,
+                    const void * const softmax_d,
+                    const void * const softmax_lse,
+                    void * const rng_state,
+                    void * const dq,
+                    void * const dk,
+                    void * const dv,
+                    void * const dq_accum,
+                    const int batch_size,
+                    const int seqlen_q,
+                    const int seqlen_k,
+                    const int seqlen_q_rounded,
+                    const int seqlen_k_rounded,
+                    const int num_heads,
+                    const int num_heads_k,
+                    const int head_size,
+                    const int head_size_rounded,
+                    const float p_dropout,
+                    const float softmax_scale,
+                    const float softmax_unscale,
+                    const bool is_causal,
+                    const bool is_bf16,
+                    const int num_splits,
+                    hipStream_t stream,
+                    uint64_t seed,
+                    uint64_t offset,
+                    const void * const attn_mask,
+                    const int64_t * const mask_dims,
+                    const void * const flashmask_downstart_ptr,
+                    const int64_t * const flashmask_dims,
+                    const void * const flashmask_upend_ptr,
+                    const void * const flashmask_downend_ptr,
+                    const void * const flashmask_upstart_ptr,
+                    const void * const flashmask_maxmin_ptr,
+                    const int q_row_stride,
+                    const int k_row_stride,
+                    const int v_row_stride,
+                    const int q_head_stride,
+                    const int k_head_stride,
+                    const int v_head_stride,
+                    const int o_row_stride,
+                    const int o_head_stride,
+                    const int q_batch_stride,
+                    const int k_batch_stride,
+                    const int v_batch_stride,
+                    const int o_batch_stride,
+                    const int dq_row_stride,
+                    const int dk_row_stride,
+                    const int dv_row_stride,
+                    const int dq_head_stride,
+                    const int dk_head_stride,
+                    const int dv_head_stride,
+                    const int do_row_stride,
+                    const int do_head_stride,
+                    const int dq_batch_stride,
+                    const int dk_batch_stride,
+                    const int dv_batch_stride,
+                    const int do_batch_stride);
+
+bool flash_attn_varlen_bwd(const void * const dout,
+                           const void * const q,
+                           const void * const k,
+                           const void * const v,
+                           const void * const out,
+                           const void * const softmax_d,
+                           const void * const softmax_lse,
+                           const int32_t * const cu_seqlens_q,
+                           const int32_t * const cu_seqlens_k,
+                           void * const rng_state,
+                           void * const dq,
+                           void * const dk,
+                           void * const dv,
+                           void * const dq_accum,
+                           const int batch_size,
+                           const int max_seqlen_q,
+                           const int max_seqlen_k,
+                           const int seqlen_q_rounded,
+                           const int seqlen_k_rounded,
+                           const int num_heads,
+                           const int num_heads_k,
+                           const int head_size,
+                           const int head_size_rounded,
+                           const float p_dropout,
+                           const float softmax_scale,
+                           const float softmax_unscale,
+                           const bool is_causal,
+                           const bool is_bf16,
+                           const int num_splits,
+                           hipStream_t stream,
+                           uint64_t seed,
+                           uint64_t offset,
+                           const void * attn_mask,
+                           const int64_t * const mask_dims,
+                           const int q_row_stride,
+                           const int k_row_stride,
+                           const int v_row_stride,
+                           const int q_head_stride,
+                           const int k_head_stride,
+                           const int v_head_stride,
+                           const int o_row_stride,
+                           const int o_head_stride,
+                           const int q_batch_stride,
+                           const int k_batch_stride,
+                           const int v_batch_stride,
+                           const int o_batch_stride,
+                           const int dq_row_stride,
+                           const int dk_row_stride,
+                           const int dv_row_stride,
+                           const int dq_head_stride,
+                           const int dk_head_stride,
+                           const int dv_head_stride,
+                           const int do_row_stride,
+                           const int do_head_stride,
+                           const int dq_batch_stride,
+                           const int dk_batch_stride,
+                           const int dv_batch_stride,
+                           const int do_batch_stride,
+                           const bool varlen_padded_input);
+
+const char *flash_attn_error();
+
+/* ---- MI355X extensions ---- */
+
+/* Same arguments as flash_attn_bwd; dk/dv have num_heads_k heads (group-summed in kernel). */
+bool flash_attn_bwd_gqa(const void * const dout, const void * const q, const void * const k,
+                        const void * const v, const void * const out,
+                        const void * const softmax_d, const void * const softmax_lse,
+                        void * const rng_state, void * const dq, void * const dk,
+                        void * const dv, void * const dq_accum,
+                        const int batch_size, const int seqlen_q, const int seqlen_k,
+                        const int seqlen_q_rounded, const int seqlen_k_rounded,
+                        const int num_heads, const int num_heads_k,
+                        const int head_size, const int head_size_rounded,
+                        const float p_dropout, const float softmax_scale,
+                        const float softmax_unscale, const bool is_causal, const bool is_bf16,
+                        const int num_splits, hipStream_t stream, uint64_t seed, uint64_t offset,
+                        const void * const attn_mask, const int64_t * const mask_dims,
+                        const void * const flashmask_downstart_ptr,
+                        const int64_t * const flashmask_dims,
+                        const void * const flashmask_upend_ptr,
+                        const void * const flashmask_downend_ptr,
+                        const void * const flashmask_upstart_ptr,
+                        const void * const flashmask_maxmin_ptr,
+                        const int q_row_stride, const int k_row_stride, const int v_row_stride,
+                        const int q_head_stride, const int k_head_stride, const int v_head_stride,
+                        const int o_row_stride, const int o_head_stride,
+                        const int q_batch_stride, const int k_batch_stride,
+                        const int v_batch_stride, const int o_batch_stride,
+                        const int dq_row_stride, const int dk_row_stride, const int dv_row_stride,
+                        const int dq_head_stride, const int dk_head_stride,
+                        const int dv_head_stride, const int do_row_stride,
+                        const int do_head_stride, const int dq_batch_stride,
+                        const int dk_batch_stride, const int dv_batch_stride,
+                        const int do_batch_stride);
+
+/* Same arguments as flash_attn_varlen_bwd; dk/dv have num_heads_k heads. */
+bool flash_attn_varlen_bwd_gqa(const void * const dout, const void * const q,
+                               const void * const k, const void * const v,
+                               const void * const out, const void * const softmax_d,
+                               const void * const softmax_lse,
+                               const int32_t * const cu_seqlens_q,
+                               const int32_t * const cu_seqlens_k, void * const rng_state,
+                               void * const dq, void * const dk, void * const dv,
+                               void * const dq_accum, const int batch_size,
+                               const int max_seqlen_q, const int max_seqlen_k,
+                               const int seqlen_q_rounded, const int seqlen_k_rounded,
+                               const int num_heads, const int num_heads_k,
+                               const int head_size, const int head_size_rounded,
+                               const float p_dropout, const float softmax_scale,
+                               const float softmax_unscale, const bool is_causal,
+                               const bool is_bf16, const int num_splits, hipStream_t stream,
+                               uint64_t seed, uint64_t offset, const void * attn_mask,
+                               const int64_t * const mask_dims,
+                               const int q_row_stride, const int k_row_stride,
+                               const int v_row_stride, const int q_head_stride,
+                               const int k_head_stride, const int v_head_stride,
+                               const int o_row_stride, const int o_head_stride,
+                               const int q_batch_stride, const int k_batch_stride,
+                               const int v_batch_stride, const int o_batch_stride,
+                               const int dq_row_stride, const int dk_row_stride,
+                               const int dv_row_stride, const int dq_head_stride,
+                               const int dk_head_stride, const int dv_head_stride,
+                               const int do_row_stride, const int do_head_stride,
+                               const int dq_batch_stride, const int dk_batch_stride,
+                               const int dv_batch_stride, const int do_batch_stride,
+                               const bool varlen_padded_input);
+
+/* Tile sizes (block_m x block_n) of the forward / backward launchers for head_size. */
+void flash_attn_block_size(int head_size, int is_backward, int * block_m, int * block_n);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif  /* FLASH_ATTN_MI355X_H_ */

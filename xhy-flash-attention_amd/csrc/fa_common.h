@@ -1,0 +1,144 @@
+// Shared device-side building blocks for the MI355X (gfx950 / CDNA4) FlashAttention-2 kernels.
+//
+// Everything here is written for wave64 + the gfx950 32x32x16 bf16/f16 MFMA:
+//   * mfma_f32_32x32x16_{bf16,f16}: lane l (r = l&31, h = l>>5) holds A[r][8h+j] and B[8h+j][r]
+//     (j = 0..7) and accumulator element g at (row = (g&3) + 8(g>>2) + 4h, col = r).
+//   * An accumulator tile X used as the next MFMA's B operand ("X as operand", no lane movement):
+//     registers 8s..8s+7 packed to 16-bit form the fragment of k-step s, whose element j of lane
+//     half h is row 16s + 8(j>>2) + 4h + (j&3) of X.  The other operand must supply the same
+//     permuted k order, which ds_read_b64_tr_b16 (4 rows x 16 cols per 16-lane group, column-major
+//     delivery) gives directly from a row-major LDS tile.
+//
+// LDS tile layout ("panel" layout), used for every K/V/Q/dO/dS image in this library:
+//   a [rows][D] 16-bit tile is stored as D/32 panels of [rows][32 elements] (64-byte rows).  The
+//   16-byte chunk c (0..3) of row `row` inside a panel lives at chunk c ^ ((row >> 2) & 3).
+//   With 64-byte rows four consecutive rows fill one 256-byte LDS bank line, so
+//     - ds_read_b128 row reads (16 distinct rows, same logical chunk) hit 16 distinct 16-byte slots,
+//     - ds_read_b64_tr_b16 reads (4 consecutive rows x 64 bytes per half-wave) fill one bank line,
+//   i.e. both access kinds are conflict-free on the same image, for any D that is a multiple of 32.
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace fa {
+
+typedef __attribute__((ext_vector_type(8))) __bf16 bf16x8_t;
+typedef __attribute__((ext_vector_type(2))) __bf16 bf16x2_t;
+typedef __attribute__((ext_vector_type(8))) _Float16 f16x8_t;
+typedef __attribute__((ext_vector_type(2))) _Float16 f16x2_t;
+typedef __attribute__((ext_vector_type(16))) float f32x16_t;
+typedef __attribute__((ext_vector_type(4))) float f32x4_t;
+typedef __attribute__((ext_vector_type(4))) short i16x4_t;
+typedef __attribute__((ext_vector_type(8))) short i16x8_t;
+typedef __attribute__((ext_vector_type(4))) unsigned u32x4_t;
+typedef __attribute__((ext_vector_type(2))) unsigned u32x2_t;
+typedef __attribute__((address_space(3))) i16x4_t lds_i16x4_t;
+
+constexpr float kNegInf = -__builtin_huge_valf();
+constexpr float kLog2e = 1.4426950408889634f;
+constexpr float kLn2 = 0.6931471805599453f;
+
+// ------------------------------------------------------------------------------------------------
+// Element traits: 16-bit storage type, MFMA, f32 <-> 16-bit conversions.
+// ------------------------------------------------------------------------------------------------
+template <bool BF16> struct Elt;
+
+template <> struct Elt<true> {
+  __device__ static inline f32x16_t mfma(i16x8_t a, i16x8_t b, f32x16_t c) {
+    return __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf16x8_t, a),
+                                                   __builtin_bit_cast(bf16x8_t, b), c, 0, 0, 0);
+  }
+  __device__ static inline unsigned pack2(float lo, float hi) {
+    bf16x2_t v = {(__bf16)lo, (__bf16)hi};  // v_cvt_pk_bf16_f32 (RNE, NaN-preserving)
+    return __builtin_bit_cast(unsigned, v);
+  }
+  __device__ static inline float to_f32(unsigned short x) {
+    return __builtin_bit_cast(float, (unsigned)x << 16);
+  }
+};
+
+template <> struct Elt<false> {
+  __device__ static inline f32x16_t mfma(i16x8_t a, i16x8_t b, f32x16_t c) {
+    return __builtin_amdgcn_mfma_f32_32x32x16_f16(__builtin_bit_cast(f16x8_t, a),
+                                                  __builtin_bit_cast(f16x8_t, b), c, 0, 0, 0);
+  }
+  __device__ static inline unsigned pack2(float lo, float hi) {
+    f16x2_t v = {(_Float16)lo, (_Float16)hi};
+    return __builtin_bit_cast(unsigned, v);
+  }
+  __device__ static inline float to_f32(unsigned short x) {
+    return (float)__builtin_bit_cast(_Float16, x);
+  }
+};
+
+// Pack accumulator registers 8s..8s+7 of a 32x32 f32 tile into a 16-bit MFMA operand fragment.
+template <bool BF16>
+__device__ inline i16x8_t pack_frag(const f32x16_t& x, int s) {
+  u32x4_t u;
+  u[0] = Elt<BF16>::pack2(x[8 * s + 0], x[8 * s + 1]);
+  u[1] = Elt<BF16>::pack2(x[8 * s + 2], x[8 * s + 3]);
+  u[2] = Elt<BF16>::pack2(x[8 * s + 4], x[8 * s + 5]);
+  u[3] = Elt<BF16>::pack2(x[8 * s + 6], x[8 * s + 7]);
+  return __builtin_bit_cast(i16x8_t, u);
+}
+
+// ------------------------------------------------------------------------------------------------
+// Panel-layout LDS addressing (see header comment).  `chunk` counts 16-byte chunks along D
+// (0 .. D/8-1), `nrows` is the row count of the tile.
+// ------------------------------------------------------------------------------------------------
+__device__ __host__ inline int panel_off(int row, int chunk, int nrows) {
+  return (chunk >> 2) * nrows * 64 + row * 64 + (((chunk & 3) ^ ((row >> 2) & 3)) << 4);
+}
+
+// ds_read_b64_tr_b16 of the 4x16 block whose rows start at `row0` (multiple of 4) and whose
+// columns start at element `col0` (multiple of 16) of a panel-layout tile with `nrows` rows.
+// `i` = lane & 15 (lane 4q+p addresses row q, columns 4p..4p+3).  Element q of the result holds
+// row row0+q, column col0 + i.
+__device__ inline i16x4_t tr_read(const char* tile, int row0, int col0, int nrows, int i) {
+  const int q = i >> 2, p = i & 3;
+  const int row = row0 + q;
+  const int col = col0 + 4 * p;                       // element column
+  const int off = panel_off(row, col >> 3, nrows) + ((col & 4) << 1);
+  return __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_i16x4_t*)(tile + off));
+}
+
+// Two tr reads -> one 8-element operand fragment (rows row0..row0+3 and row0+8..row0+11).
+__device__ inline i16x8_t tr_frag(const char* tile, int row0, int col0, int nrows, int i) {
+  i16x4_t lo = tr_read(tile, row0, col0, nrows, i);
+  i16x4_t hi = tr_read(tile, row0 + 8, col0, nrows, i);
+  i16x8_t r;
+  r[0] = lo[0]; r[1] = lo[1]; r[2] = lo[2]; r[3] = lo[3];
+  r[4] = hi[0]; r[5] = hi[1]; r[6] = hi[2]; r[7] = hi[3];
+  return r;
+}
+
+// Row read of 8 consecutive elements (one 16-byte chunk) of a panel-layout tile.
+__device__ inline i16x8_t row_read(const char* tile, int row, int chunk, int nrows) {
+  return *(const i16x8_t*)(tile + panel_off(row, chunk, nrows));
+}
+
+// max / sum across the two 32-lane halves (lanes l and l^32 hold the same query / key column).
+__device__ inline float half_swap_max(float x) {
+  auto r = __builtin_amdgcn_permlane32_swap(__builtin_bit_cast(unsigned, x),
+                                            __builtin_bit_cast(unsigned, x), false, false);
+  return fmaxf(__builtin_bit_cast(float, (unsigned)r[0]), __builtin_bit_cast(float, (unsigned)r[1]));
+}
+__device__ inline float half_swap_sum(float x) {
+  auto r = __builtin_amdgcn_permlane32_swap(__builtin_bit_cast(unsigned, x),
+                                            __builtin_bit_cast(unsigned, x), false, false);
+  return __builtin_bit_cast(float, (unsigned)r[0]) + __builtin_bit_cast(float, (unsigned)r[1]);
+}
+
+__device__ inline float fast_exp2(float x) { return __builtin_amdgcn_exp2f(x); }
+
+// 16-byte global load with zero fill when !valid.
+__device__ inline u32x4_t ld16(const void* p, bool valid) {
+  u32x4_t z = {0u, 0u, 0u, 0u};
+  return valid ? *(const u32x4_t*)p : z;
+}
+
+// Accumulator element g -> row offset inside a 32x32 tile for lane half h.
+__device__ __host__ constexpr inline int acc_row(int g, int h) { return (g & 3) + 8 * (g >> 2) + 4 * h; }
+
+}  // namespace fa

@@ -1,0 +1,75 @@
+// Kernel parameter blocks (passed by value to the kernels) and launcher declarations.
+//
+// Semantics follow the reference's Qkv_params / Flash_fwd_params / Flash_bwd_params
+// (reference csrc/flash_attn/src/flash.h:30-168): element strides, h % h_k == 0 grouping, the
+// varlen cu_seqlens convention of BlockInfo (reference block_info.h:11-38) and the padded LSE /
+// softmax_d row pitch.  Unlike the reference, every stride and offset is 64-bit (the reference's
+// uint32 element offsets are flagged "won't work for arrays > 2GB", flash.h:150-151) so a 288 GB
+// HBM3E device can take arbitrarily large shards.
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace fa {
+
+struct AttnShape {
+  int b;            // batch (number of sequences for varlen)
+  int h;            // query heads
+  int hk;           // key/value heads (h % hk == 0)
+  int seqlen_q;     // fixed-length seqlen, or max_seqlen_q for varlen
+  int seqlen_k;
+  int d;            // head dim actually stored (multiple of 8, <= 256)
+  int lse_pitch;    // row pitch of softmax_lse / softmax_d per (b, h): seqlen_q (fwd) / rounded (bwd)
+  const int* cu_seqlens_q;  // nullptr for fixed-length
+  const int* cu_seqlens_k;
+  bool varlen_padded_input;  // cu_seqlens give lengths only; rows addressed with batch strides
+  bool causal;
+  float scale;      // softmax scale
+  float scale_log2; // scale * log2(e)
+};
+
+struct FwdParams {
+  AttnShape s;
+  const void* q; const void* k; const void* v; void* o;
+  float* lse;
+  uint64_t* rng_state;      // if non-null, {seed, offset} is recorded here (reference
+  uint64_t seed, offset;    // flash_fwd_kernel.h:321-324 writes it unconditionally)
+  int64_t q_batch, q_row, q_head;
+  int64_t k_batch, k_row, k_head;
+  int64_t v_batch, v_row, v_head;
+  int64_t o_batch, o_row, o_head;
+  int num_m_blocks;
+};
+
+struct BwdParams {
+  AttnShape s;
+  const void* q; const void* k; const void* v; const void* o; const void* dout;
+  void* dq; void* dk; void* dv;
+  const float* lse;
+  float* dsum;      // softmax_d: (b, h, seqlen_q_rounded) fp32, D = rowsum(dO * O)
+  float* dq_accum;  // (b, h, seqlen_q_rounded, d_rounded) fp32
+  int64_t q_batch, q_row, q_head;
+  int64_t k_batch, k_row, k_head;
+  int64_t v_batch, v_row, v_head;
+  int64_t o_batch, o_row, o_head;
+  int64_t do_batch, do_row, do_head;
+  int64_t dq_batch, dq_row, dq_head;
+  int64_t dk_batch, dk_row, dk_head;
+  int64_t dv_batch, dv_row, dv_head;
+  int seqlen_q_rounded;   // pitch of dsum / dq_accum rows
+  int d_rounded;          // pitch of dq_accum columns (multiple of 32)
+  bool gqa_reduce;        // true: dk/dv have hk heads and the kernel sums the group in-register;
+                          // false: dk/dv have h heads (reference "expanded" contract)
+  int num_n_blocks;
+};
+
+// Host launchers (fa_fwd.hip / fa_bwd.hip).  Throw std::runtime_error on invalid configuration.
+void launch_fwd(const FwdParams& p, bool is_bf16, hipStream_t stream);
+void launch_bwd(const BwdParams& p, bool is_bf16, hipStream_t stream);
+
+// Tile sizes the launchers use for a given head dim (reported by _get_block_size in Python).
+void fwd_block_size(int d, int* block_m, int* block_n);
+void bwd_block_size(int d, int* block_m, int* block_n);
+
+}  // namespace fa
