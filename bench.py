@@ -1,0 +1,234 @@
+#!/usr/bin/env python3
+"""Headline benchmark: attention TFLOPS (fwd, fwd+bwd) at seqlen 8k, hdim 128, causal.
+
+One "step" = one forward + backward of ``flash_attn_func`` on the C3 workload
+(batch 4 x seqlen 8192 x 16 heads x hdim 128, bf16, causal; BASELINE.json configs[2]) with the
+inputs already resident in HBM.  FLOPs follow the reference's convention
+(benchmarks/benchmark_flash_attention.py:27-30): F_fwd = 4 b s^2 h d / 2 (causal),
+F_bwd = 2.5 F_fwd, F_fwd+bwd = 3.5 F_fwd.
+
+Multi-GPU (``torch.distributed.run``, one process per GPU): every rank runs the same per-GPU batch
+(weak scaling, batch-sharded, no collective on the data path); a barrier + synchronize bracket the
+timed region on every rank and the MAX elapsed time over ranks is reduced with one RCCL all-reduce
+after the region.  ``value`` = total FLOPs of all ranks / that max time.
+
+Also reported: live per-kernel device time from HIP events recorded on the launch stream by the
+library (``flash_attn_timing_*``), the roofline of the dominant kernel against the 2516.6 TF dense
+bf16 MFMA peak, and the reference's CPU path (torch SDPA) timed on this host on a bounded sample.
+"""
+import argparse
+import ctypes
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+PKG = os.path.join(ROOT, "xhy-flash-attention_amd")
+for _p in (ROOT, PKG):
+    if _p not in sys.path:
+        sys.path.insert(0, _p)
+
+METRIC = "attention TFLOPS/GPU (fwd, fwd+bwd) at seqlen 8k hdim 128 causal"
+PEAK_TFLOPS = 2516.6          # 256 CU x 4096 bf16/f16 MFMA FLOP/clk x 2.4 GHz (dense)
+H100_FWD_BWD_TFLOPS = 308.0   # FA2 fwd+bwd, causal, hdim128, s=8k, H100 SXM5
+KERNELS = {0: "fwd_kernel", 1: "bwd_pre_kernel", 2: "bwd_main_kernel", 3: "bwd_dq_kernel"}
+
+WORKLOADS = {
+    # name: (batch per GPU, seqlen, nheads, nheads_k, headdim, dtype, causal)
+    "c3": (4, 8192, 16, 16, 128, "bf16", True),
+    "c2": (4, 2048, 16, 16, 64, "bf16", True),
+    "c5": (8, 32768, 32, 8, 128, "fp16", True),
+}
+
+
+def flops_fwd(b, s, h, d, causal):
+    return 4.0 * b * s * s * h * d / (2.0 if causal else 1.0)
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--workload", default="c3", choices=sorted(WORKLOADS))
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-threads", type=int, default=16)
+    ap.add_argument("--traffic", default=os.path.join(ROOT, "profiles", "traffic.json"),
+                    help="JSON with PMC-measured HBM bytes per launch (see profiles/)")
+    return ap.parse_args()
+
+
+def dist_init():
+    import torch
+    import torch.distributed as dist
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        torch.cuda.set_device(local)
+        dist.init_process_group(backend="nccl", device_id=torch.device("cuda", local))
+    else:
+        torch.cuda.set_device(0)
+    return rank, local, world
+
+
+def barrier(world):
+    if world > 1:
+        import torch.distributed as dist
+        dist.barrier()
+
+
+def max_over_ranks(x, world):
+    if world == 1:
+        return x
+    import torch
+    import torch.distributed as dist
+    t = torch.tensor([x], dtype=torch.float64, device="cuda")
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    return float(t.item())
+
+
+def timed(step, steps, warmup, world):
+    """W untimed steps, then EXACTLY `steps` steps bracketed by barrier + synchronize."""
+    import torch
+    for _ in range(warmup):
+        step()
+    barrier(world)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        step()
+    torch.cuda.synchronize()
+    t1 = time.perf_counter()
+    barrier(world)
+    return max_over_ranks(t1 - t0, world)
+
+
+class KernelTimer:
+    """Reads the library's HIP-event per-kernel timings (recorded on the launch stream)."""
+
+    def __init__(self):
+        import flash_attn_2_cuda as m
+        self.lib = m._lib
+        self.lib.flash_attn_timing_enable.argtypes = [ctypes.c_int]
+        self.lib.flash_attn_timing_read.argtypes = [ctypes.c_int, ctypes.POINTER(ctypes.c_double),
+                                                    ctypes.POINTER(ctypes.c_long)]
+
+    def start(self):
+        self.lib.flash_attn_timing_enable(1)
+
+    def stop(self):
+        out = {}
+        for kid, name in KERNELS.items():
+            ms, n = ctypes.c_double(), ctypes.c_long()
+            self.lib.flash_attn_timing_read(kid, ctypes.byref(ms), ctypes.byref(n))
+            if n.value:
+                out[name] = {"total_ms": ms.value, "launches": n.value, "avg_ms": ms.value / n.value}
+        self.lib.flash_attn_timing_enable(0)
+        return out
+
+
+def main():
+    args = parse()
+    import torch
+
+    from flash_attn import flash_attn_func
+
+    rank, local, world = dist_init()
+    b, s, h, hk, d, dt_name, causal = WORKLOADS[args.workload]
+    dtype = torch.bfloat16 if dt_name == "bf16" else torch.float16
+    dev = torch.device("cuda", local)
+    g = torch.Generator(device=dev).manual_seed(1234 + rank)
+    q = torch.randn(b, s, h, d, device=dev, dtype=dtype, generator=g).requires_grad_()
+    k = torch.randn(b, s, hk, d, device=dev, dtype=dtype, generator=g).requires_grad_()
+    v = torch.randn(b, s, hk, d, device=dev, dtype=dtype, generator=g).requires_grad_()
+    dout = torch.randn(b, s, h, d, device=dev, dtype=dtype, generator=g)
+
+    f_fwd = flops_fwd(b, s, h, d, causal)
+    f_step = 3.5 * f_fwd
+
+    def fwd_only():
+        with torch.no_grad():
+            flash_attn_func(q, k, v, causal=causal)
+
+    def fwd_bwd():
+        out = flash_attn_func(q, k, v, causal=causal)
+        torch.autograd.grad(out, (q, k, v), dout)
+
+    timer = KernelTimer()
+    # forward-only leg (the north_star's >= 50%-of-peak target is quoted on the forward)
+    t_fwd = timed(fwd_only, args.steps, args.warmup, world)
+    # headline leg: fwd + bwd, with live per-kernel event timing
+    timer.start()
+    t_step = timed(fwd_bwd, args.steps, args.warmup, world)
+    kt = timer.stop()
+    # the timer also saw the warm-up launches; averages are per launch, so that is harmless
+
+    value = world * f_step * args.steps / t_step / 1e12
+    fwd_tflops = world * f_fwd * args.steps / t_fwd / 1e12
+
+    # roofline of the dominant kernel (largest total device time in the fwd+bwd leg)
+    alg = {"fwd_kernel": f_fwd, "bwd_main_kernel": 2.5 * f_fwd}
+    dom = max(kt, key=lambda n: kt[n]["total_ms"]) if kt else None
+    roofline = None
+    if dom in alg:
+        achieved = alg[dom] / (kt[dom]["avg_ms"] / 1e3) / 1e12
+        traffic = None
+        try:
+            with open(args.traffic) as f:
+                traffic = json.load(f).get(args.workload, {}).get(dom)
+        except (OSError, ValueError):
+            traffic = None
+        roofline = {"bound": "mfma", "kernel": dom, "achieved": round(achieved, 2), "peak": PEAK_TFLOPS,
+                    "unit": "TFLOP/s", "frac": round(achieved / PEAK_TFLOPS, 4), "traffic": traffic,
+                    "alg_flops_per_launch": alg[dom], "avg_launch_ms": round(kt[dom]["avg_ms"], 4)}
+
+    cpu = None
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        from oracle.cpu_baseline import cpu_model_name, sdpa_fwd_bwd_tflops
+        threads = max(1, min(args.cpu_threads, os.cpu_count() or 1))
+        sample_b = 1
+        tf, sec = sdpa_fwd_bwd_tflops(sample_b, s, h, d, causal, dtype, threads, repeats=2,
+                                      flops_fn=lambda bb: 3.5 * flops_fwd(bb, s, h, d, causal))
+        cpu = {"value": round(tf, 4), "unit": "TFLOPS", "cores": threads, "kind": "port",
+               "sample": f"torch SDPA fwd+bwd on CPU ({cpu_model_name()}), batch {sample_b} of the "
+                         f"{args.workload} workload (s={s}, h={h}, d={d}, {dt_name}, causal), "
+                         f"{sec:.2f} s per rep, 1 warm-up + 2 reps"}
+
+    if rank == 0:
+        line = {
+            "metric": METRIC,
+            "value": round(value, 2),
+            "unit": "TFLOPS",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(t_step / args.steps * 1e3, 4),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": round(value / world / H100_FWD_BWD_TFLOPS, 4),
+            "dtype": dt_name,
+            "data": "synthetic N(0,1) Q/K/V/dO, resident in HBM",
+            "config": {"workload": f"flash_attn_func fwd+bwd ({args.workload})", "batch_per_gpu": b,
+                       "global_batch": b * world, "seq_len": s, "nheads": h, "nheads_k": hk,
+                       "headdim": d, "causal": causal,
+                       "parallelism": f"batch-sharded x{world}, no collectives on the hot path"},
+            "fwd_tflops": round(fwd_tflops, 2),
+            "fwd_ms": round(t_fwd / args.steps * 1e3, 4),
+            "fwd_bwd_tflops_per_gpu": round(value / world, 2),
+            "baseline_note": "vs_baseline = per-GPU fwd+bwd TFLOPS / 308 (FA2 on H100 SXM5, causal hdim128 s8k, BASELINE.md)",
+            "kernels": {n: {"avg_ms": round(x["avg_ms"], 4), "launches": x["launches"]} for n, x in kt.items()},
+            "roofline": roofline,
+            "cpu_baseline": cpu,
+        }
+        print(json.dumps(line), flush=True)
+
+    if world > 1:
+        import torch.distributed as dist
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

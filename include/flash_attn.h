@@ -330,6 +330,12 @@ bool flash_attn_varlen_bwd_gqa(const void * const dout, const void * const q,
 /* Tile sizes (block_m x block_n) of the forward / backward launchers for head_size. */
 void flash_attn_block_size(int head_size, int is_backward, int * block_m, int * block_n);
 
+/* Per-kernel device timing with HIP events on the launch stream (benchmarking only; not under
+ * graph capture).  enable != 0 clears the totals and starts recording.  Kernel ids: 0 forward,
+ * 1 backward preprocess (D = rowsum(dO*O)), 2 backward main (dK/dV/dQ), 3 dQ conversion. */
+void flash_attn_timing_enable(int enable);
+void flash_attn_timing_read(int kernel_id, double * total_ms, long * count);
+
 #ifdef __cplusplus
 }
 #endif

@@ -376,7 +376,9 @@ template <bool BF16, int D, bool CAUSAL>
 static void run_bwd(const BwdParams& p, hipStream_t stream) {
   const int nheads_grid = p.gqa_reduce ? p.s.hk : p.s.h;
   dim3 grid(p.s.b * nheads_grid, p.num_n_blocks);
+  prof_begin(kTimeBwdMain, stream);
   hipLaunchKernelGGL((bwd_main_kernel<BF16, D, CAUSAL>), grid, dim3(256), 0, stream, p);
+  prof_end(kTimeBwdMain, stream);
 }
 
 template <bool BF16, bool CAUSAL>
@@ -400,13 +402,17 @@ static void launch_bwd_t(const BwdParams& p, hipStream_t stream) {
   const int sq = p.s.seqlen_q;
   {
     dim3 grid(p.s.b * p.s.h, (sq + 15) / 16);
+    prof_begin(kTimeBwdPre, stream);
     if (grid.y > 0) hipLaunchKernelGGL((bwd_pre_kernel<BF16>), grid, dim3(256), 0, stream, p);
+    prof_end(kTimeBwdPre, stream);
   }
   if (p.s.causal) dispatch_bwd_d<BF16, true>(p, stream); else dispatch_bwd_d<BF16, false>(p, stream);
   {
     const int64_t chunks = (int64_t)sq * (p.s.d / 8);
     dim3 grid(p.s.b * p.s.h, (unsigned)((chunks + 255) / 256));
+    prof_begin(kTimeBwdDq, stream);
     if (grid.y > 0) hipLaunchKernelGGL((bwd_dq_kernel<BF16>), grid, dim3(256), 0, stream, p);
+    prof_end(kTimeBwdDq, stream);
   }
 }
 

@@ -248,7 +248,9 @@ __global__ void __launch_bounds__(256, 2) fwd_kernel(const FwdParams p) {
 template <bool BF16, int D, bool CAUSAL>
 static void run_fwd(const FwdParams& p, hipStream_t stream) {
   dim3 grid(p.s.b * p.s.h, p.num_m_blocks);
+  prof_begin(kTimeFwd, stream);
   hipLaunchKernelGGL((fwd_kernel<BF16, D, CAUSAL>), grid, dim3(256), 0, stream, p);
+  prof_end(kTimeFwd, stream);
 }
 
 template <bool BF16, bool CAUSAL>

@@ -72,4 +72,9 @@ void launch_bwd(const BwdParams& p, bool is_bf16, hipStream_t stream);
 void fwd_block_size(int d, int* block_m, int* block_n);
 void bwd_block_size(int d, int* block_m, int* block_n);
 
+// Optional HIP-event timing around each kernel launch (fa_timing.cpp).
+enum TimedKernel { kTimeFwd = 0, kTimeBwdPre = 1, kTimeBwdMain = 2, kTimeBwdDq = 3, kNumTimedKernels = 4 };
+void prof_begin(int id, hipStream_t s);
+void prof_end(int id, hipStream_t s);
+
 }  // namespace fa

@@ -1,0 +1,88 @@
+// Optional per-kernel timing with HIP events recorded on the launch stream.
+//
+// Off by default (one branch per launch).  bench.py enables it around its timed region and reads
+// the average device duration of each kernel, so the roofline numbers it reports come from the
+// kernels themselves rather than from host wall time.  Not for use under graph capture.
+#include <hip/hip_runtime.h>
+
+#include <mutex>
+#include <vector>
+
+#include "fa_params.h"
+
+namespace fa {
+namespace {
+
+struct Pending { hipEvent_t a, b; int id; };
+
+std::mutex g_mu;
+bool g_on = false;
+std::vector<Pending> g_pending;
+std::vector<hipEvent_t> g_pool;
+double g_ms[kNumTimedKernels] = {};
+long g_count[kNumTimedKernels] = {};
+thread_local hipEvent_t t_start = nullptr;
+
+hipEvent_t take() {
+  if (!g_pool.empty()) { hipEvent_t e = g_pool.back(); g_pool.pop_back(); return e; }
+  hipEvent_t e = nullptr;
+  (void)hipEventCreate(&e);
+  return e;
+}
+
+void drain_locked() {
+  for (auto& p : g_pending) {
+    float ms = 0.f;
+    (void)hipEventSynchronize(p.b);
+    if (hipEventElapsedTime(&ms, p.a, p.b) == hipSuccess) { g_ms[p.id] += ms; g_count[p.id] += 1; }
+    g_pool.push_back(p.a);
+    g_pool.push_back(p.b);
+  }
+  g_pending.clear();
+}
+
+}  // namespace
+
+void prof_begin(int id, hipStream_t s) {
+  (void)id;
+  if (!g_on) return;
+  std::lock_guard<std::mutex> lk(g_mu);
+  t_start = take();
+  (void)hipEventRecord(t_start, s);
+}
+
+void prof_end(int id, hipStream_t s) {
+  if (!g_on || t_start == nullptr) return;
+  std::lock_guard<std::mutex> lk(g_mu);
+  hipEvent_t e = take();
+  (void)hipEventRecord(e, s);
+  g_pending.push_back({t_start, e, id});
+  t_start = nullptr;
+  if (g_pending.size() > 4096) drain_locked();
+}
+
+}  // namespace fa
+
+extern "C" {
+
+// enable != 0 starts recording (and clears accumulated totals); 0 stops.
+void flash_attn_timing_enable(int enable) {
+  std::lock_guard<std::mutex> lk(fa::g_mu);
+  fa::drain_locked();
+  if (enable) {
+    for (int i = 0; i < fa::kNumTimedKernels; ++i) { fa::g_ms[i] = 0.0; fa::g_count[i] = 0; }
+  }
+  fa::g_on = enable != 0;
+}
+
+// Total device milliseconds and launch count of kernel `id` since the last enable
+// (0 fwd, 1 bwd_pre, 2 bwd_main, 3 bwd_dq).  Synchronises on the recorded events.
+void flash_attn_timing_read(int id, double* total_ms, long* count) {
+  std::lock_guard<std::mutex> lk(fa::g_mu);
+  fa::drain_locked();
+  if (id < 0 || id >= fa::kNumTimedKernels) { *total_ms = 0.0; *count = 0; return; }
+  *total_ms = fa::g_ms[id];
+  *count = fa::g_count[id];
+}
+
+}  // extern "C"
