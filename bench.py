@@ -32,7 +32,7 @@ for _p in (ROOT, PKG):
 METRIC = "attention TFLOPS/GPU (fwd, fwd+bwd) at seqlen 8k hdim 128 causal"
 PEAK_TFLOPS = 2516.6          # 256 CU x 4096 bf16/f16 MFMA FLOP/clk x 2.4 GHz (dense)
 H100_FWD_BWD_TFLOPS = 308.0   # FA2 fwd+bwd, causal, hdim128, s=8k, H100 SXM5
-KERNELS = {0: "fwd_kernel", 1: "bwd_pre_kernel", 2: "bwd_main_kernel", 3: "bwd_dq_kernel"}
+KERNELS = {0: "fwd_kernel", 1: "bwd_pre_kernel", 2: "bwd_dkdv_kernel", 3: "bwd_dq_kernel"}
 
 WORKLOADS = {
     # name: (batch per GPU, seqlen, nheads, nheads_k, headdim, dtype, causal)
@@ -170,7 +170,7 @@ def main():
     fwd_tflops = world * f_fwd * args.steps / t_fwd / 1e12
 
     # roofline of the dominant kernel (largest total device time in the fwd+bwd leg)
-    alg = {"fwd_kernel": f_fwd, "bwd_main_kernel": 2.5 * f_fwd}
+    alg = {"fwd_kernel": f_fwd, "bwd_dkdv_kernel": 2.0 * f_fwd, "bwd_dq_kernel": 1.5 * f_fwd}
     dom = max(kt, key=lambda n: kt[n]["total_ms"]) if kt else None
     roofline = None
     if dom in alg:

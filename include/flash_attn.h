@@ -21,13 +21,14 @@
  *   - the Paddle dense-mask / FlashMask arguments are accepted for ABI
  *     compatibility but must be NULL (out of scope for this build: the call
  *     fails with a message otherwise);
- *   - backward: softmax_d (b, h, seqlen_q_rounded) fp32 and dq_accum
- *     (b, h, seqlen_q_rounded, head_size_rounded) fp32 are caller-owned
- *     workspaces; for MQA/GQA the caller passes dk/dv with num_heads heads
- *     ("expanded", reference flash_api.cpp:628-635) and sums the groups itself;
- *   - num_splits is accepted; the MI355X backward is deterministic in dK/dV for
- *     every value (each workgroup owns its key block), dQ is accumulated with
- *     fp32 atomics as in the reference.
+ *   - backward: softmax_d (b, h, seqlen_q_rounded) fp32 is a caller-owned
+ *     output (D = rowsum(dO * O)); dq_accum is accepted but unused and may be
+ *     NULL (the MI355X backward computes dQ in its own kernel, without the
+ *     reference's fp32 atomic accumulator); for MQA/GQA the caller passes dk/dv
+ *     with num_heads heads ("expanded", reference flash_api.cpp:628-635) and
+ *     sums the groups itself;
+ *   - num_splits is accepted and ignored: the MI355X backward uses no atomics,
+ *     so dQ, dK and dV are bitwise deterministic for every value.
  *
  * MI355X extensions (no reference counterpart):
  *   flash_attn_bwd_gqa / flash_attn_varlen_bwd_gqa take the same arguments as
@@ -332,7 +333,7 @@ void flash_attn_block_size(int head_size, int is_backward, int * block_m, int * 
 
 /* Per-kernel device timing with HIP events on the launch stream (benchmarking only; not under
  * graph capture).  enable != 0 clears the totals and starts recording.  Kernel ids: 0 forward,
- * 1 backward preprocess (D = rowsum(dO*O)), 2 backward main (dK/dV/dQ), 3 dQ conversion. */
+ * 1 backward preprocess (D = rowsum(dO*O)), 2 backward dK/dV, 3 backward dQ. */
 void flash_attn_timing_enable(int enable);
 void flash_attn_timing_read(int kernel_id, double * total_ms, long * count);
 

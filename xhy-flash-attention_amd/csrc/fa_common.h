@@ -21,6 +21,8 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <type_traits>
+
 namespace fa {
 
 typedef __attribute__((ext_vector_type(8))) __bf16 bf16x8_t;
@@ -118,6 +120,76 @@ __device__ inline i16x8_t row_read(const char* tile, int row, int chunk, int nro
   return *(const i16x8_t*)(tile + panel_off(row, chunk, nrows));
 }
 
+// ------------------------------------------------------------------------------------------------
+// Per-lane LDS bases for the two access kinds on a panel-layout tile, valid whenever the tile row
+// offset R0 of the access is a multiple of 16.  Every address then is   base + compile-time
+// constant, so the reads use the ds_* immediate offset and keep no per-read address VGPRs.
+//   row read  (ds_read_b128, A/B operand rows r, chunk C):   tile + (C>>2)*NR*64 + R0*64 + rb[(C>>1)&1]
+//   tr read   (ds_read_b64_tr_b16, rows R0+4h+q, 16 cols at DT*32 + 16(r>>4)):
+//                                   lo = tile + DT*NR*64 + R0*64 + tb[0],  hi = ... + 8*64 + tb[1]
+// ------------------------------------------------------------------------------------------------
+struct LdsBases {
+  int rb[2];  // row-read bases for chunk&3 = hh (even k-step) and 2+hh (odd k-step)
+  int tb[2];  // tr-read bases for rows R0+4h+q and R0+8+4h+q
+  __device__ inline LdsBases(int lane) {
+    const int r = lane & 31, hh = lane >> 5, i = lane & 15;
+    const int xr = (r >> 2) & 3;
+    rb[0] = r * 64 + (((0 + hh) ^ xr) << 4);
+    rb[1] = r * 64 + (((2 + hh) ^ xr) << 4);
+    const int q = i >> 2, pp = i & 3;
+    const int trc = 2 * (r >> 4) + (pp >> 1);
+    tb[0] = (4 * hh + q) * 64 + ((trc ^ hh) << 4) + (pp & 1) * 8;
+    tb[1] = (4 * hh + q) * 64 + ((trc ^ (2 + hh)) << 4) + (pp & 1) * 8;
+  }
+};
+
+// Opaque 32-bit value: stops LICM / reassociation from turning "base + constant" LDS addresses into
+// one hoisted VGPR per constant (the ring-buffer offset changes every tile).
+__device__ inline int opaque(int x) {
+  asm volatile("" : "+v"(x));
+  return x;
+}
+
+// Per-tile LDS addresses: the four lane bases of LdsBases shifted to one tile (byte offset
+// `tile_off` from `smem`), made opaque so each read is   base VGPR + immediate offset.
+struct TileAddr {
+  int r[2], t[2];
+  __device__ inline TileAddr(const LdsBases& b, int tile_off) {
+    r[0] = opaque(tile_off + b.rb[0]); r[1] = opaque(tile_off + b.rb[1]);
+    t[0] = opaque(tile_off + b.tb[0]); t[1] = opaque(tile_off + b.tb[1]);
+  }
+};
+
+// 16-byte row read of chunk C (compile-time) for rows R0 + (lane & 31), R0 % 16 == 0.
+template <int NR, int R0, int C>
+__device__ inline i16x8_t row_read_c(const char* smem, const TileAddr& a) {
+  static_assert(R0 % 16 == 0, "row offset must be a multiple of 16");
+  return *(const i16x8_t*)(smem + a.r[(C >> 1) & 1] + ((C >> 2) * NR * 64 + R0 * 64));
+}
+
+// Operand fragment of the 16-row k-step at rows R0..R0+15 (R0 % 16 == 0), columns DT*32 + [0, 32),
+// in the "accumulator as operand" k order (two ds_read_b64_tr_b16).
+template <int NR, int R0, int DT>
+__device__ inline i16x8_t tr_frag_c(const char* smem, const TileAddr& a) {
+  static_assert(R0 % 16 == 0, "row offset must be a multiple of 16");
+  constexpr int off = DT * NR * 64 + R0 * 64;
+  const i16x4_t lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_i16x4_t*)(smem + a.t[0] + off));
+  const i16x4_t hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_i16x4_t*)(smem + a.t[1] + off + 8 * 64));
+  i16x8_t r;
+  r[0] = lo[0]; r[1] = lo[1]; r[2] = lo[2]; r[3] = lo[3];
+  r[4] = hi[0]; r[5] = hi[1]; r[6] = hi[2]; r[7] = hi[3];
+  return r;
+}
+
+// Compile-time loop helper: f(std::integral_constant<int, I>) for I in [0, N).
+template <int I, int N, typename F>
+__device__ inline void static_for(F&& f) {
+  if constexpr (I < N) {
+    f(std::integral_constant<int, I>{});
+    static_for<I + 1, N>(f);
+  }
+}
+
 // max / sum across the two 32-lane halves (lanes l and l^32 hold the same query / key column).
 __device__ inline float half_swap_max(float x) {
   auto r = __builtin_amdgcn_permlane32_swap(__builtin_bit_cast(unsigned, x),
@@ -131,6 +203,23 @@ __device__ inline float half_swap_sum(float x) {
 }
 
 __device__ inline float fast_exp2(float x) { return __builtin_amdgcn_exp2f(x); }
+__device__ inline float fast_rcp(float x) { return __builtin_amdgcn_rcpf(x); }
+__device__ inline int wave_uniform(int x) { return __builtin_amdgcn_readfirstlane(x); }
+
+// LDS-DMA: 16 bytes per lane from a range-checked buffer (offsets past `bytes` read as zero) into
+// the wave-uniform LDS address `lds_dst` + 16 * lane.
+typedef __amdgpu_buffer_rsrc_t buf_rsrc_t;
+__device__ inline buf_rsrc_t make_rsrc(const void* base, int bytes) {
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), (short)0, bytes, 0x00020000);
+}
+__device__ inline void dma16(buf_rsrc_t rsrc, char* lds_dst, int voffset) {
+  __builtin_amdgcn_raw_ptr_buffer_load_lds(rsrc, (__attribute__((address_space(3))) void*)lds_dst, 16,
+                                           voffset, 0, 0, 0);
+}
+__device__ inline void wait_dma_and_barrier() {
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+}
 
 // 16-byte global load with zero fill when !valid.
 __device__ inline u32x4_t ld16(const void* p, bool valid) {

@@ -6,17 +6,22 @@
 // flash_fwd_kernel.h:509-518); causal mask is top-left aligned (key <= query, softmax.h:143-178).
 //
 // MI355X mapping (not a translation of the CUDA tiling):
-//   * 4 waves x 32 query rows = 128-row query block; BN = 64 keys per K/V tile.
+//   * 8 waves x 32 query rows = 256-row query block per workgroup; BN = 64 keys per K/V tile.
+//   * K/V tiles arrive by LDS-DMA (buffer_load ... lds, one 1-KiB piece per wave instruction) two
+//     tiles ahead into a 3-deep LDS ring; the buffer descriptor's range check zero-fills rows past
+//     seqlen_k and padded head-dim columns, so the kernel never branches on the load side.  One
+//     s_waitcnt vmcnt(0) + barrier per tile (the DMA had a whole tile of compute to land).
 //   * "Swapped" QK^T: each wave computes S^T = K . Q^T with v_mfma_f32_32x32x16, so the query sits on
 //     the MFMA column (= lane) and every lane holds 32 scores of ONE query row: the row max / sum are
-//     in-lane reductions plus one v_permlane32_swap, with no LDS and no shuffles.
+//     in-lane reductions plus one v_permlane32_swap.
 //   * O^T = V^T . P^T: the S^T accumulator, converted to bf16/f16 in registers, is directly the B
 //     operand of the PV MFMA (no LDS round trip for P); V^T fragments come from the row-major V tile
 //     through ds_read_b64_tr_b16.  O^T keeps the query on the lane, so the online-softmax rescale is
-//     a per-lane scalar multiply.
-//   * Q lives in registers for the whole K/V sweep.  K and V are register-staged: the global loads of
-//     tile n+1 are issued before the MFMAs of tile n and written (XOR-swizzled panel layout, see
-//     fa_common.h) into the other LDS buffer afterwards: one barrier per tile.
+//     a per-lane scalar multiply, skipped (wave-uniformly, exactly) when no row max of the wave moved.
+//   * Software pipeline over the tiles that need no mask (all but the causal diagonal / the ragged
+//     last tile): one basic block per tile holds QK^T(n+1) (MFMA), the exp / sum / pack of tile n
+//     (VALU) and PV(n) (MFMA), so the matrix pipe has independent work while the softmax runs.
+//   * Every LDS address is one of four per-lane bases + an immediate (fa_common.h LdsBases).
 //   * Heaviest causal query blocks are dispatched first (blockIdx.y reversed) to shorten the tail.
 #include <stdexcept>
 #include <string>
@@ -26,26 +31,31 @@
 
 namespace fa {
 
-constexpr int kFwdWaves = 4;
+constexpr int kFwdWaves = 8;
 constexpr int kFwdBM = 32 * kFwdWaves;
-
-template <int D> struct FwdTile { static constexpr int BN = 64; };
+constexpr int kFwdBN = 64;
+constexpr int kFwdBufs = 3;
 
 template <bool BF16, int D, bool CAUSAL>
-__global__ void __launch_bounds__(256, 2) fwd_kernel(const FwdParams p) {
+__global__ void __launch_bounds__(kFwdWaves * 64, 2) fwd_kernel(const FwdParams p) {
   using E = Elt<BF16>;
-  constexpr int BN = FwdTile<D>::BN;
+  constexpr int NW = kFwdWaves;
+  constexpr int BN = kFwdBN;
+  constexpr int BM = kFwdBM;
   constexpr int KS = D / 16;            // QK^T k-steps (16 along d)
   constexpr int NT = BN / 32;           // 32-key subtiles per K/V tile
   constexpr int NP = D / 32;            // 32-wide d panels == PV output tiles
   constexpr int TILE = BN * D * 2;      // bytes of one K or V tile
-  constexpr int NPAIR = BN * NP / 2;    // (2 rows x 64 B) staging units per tile
-  constexpr int LOADS = (NPAIR + 31) / 32;
-  __shared__ __attribute__((aligned(16))) char smem[4 * TILE];  // [buffer][K | V]
+  constexpr int PIECES = TILE / 1024;   // 1-KiB LDS-DMA pieces per K (or V) tile
+  constexpr int PPW = (PIECES + NW - 1) / NW;
+  static_assert(TILE % 1024 == 0, "tile must be whole DMA pieces");
+  __shared__ __attribute__((aligned(16))) char smem[kFwdBufs * 2 * TILE];  // [buffer][K | V]
 
   const AttnShape s = p.s;
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int r = lane & 31, hh = lane >> 5, i16 = lane & 15;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = wave_uniform(tid >> 6);
+  const int r = lane & 31, hh = lane >> 5;
+  const LdsBases lb(lane);
 
   const int bh = blockIdx.x;
   const int bidb = bh / s.h;
@@ -71,7 +81,7 @@ __global__ void __launch_bounds__(256, 2) fwd_kernel(const FwdParams p) {
     p.rng_state[0] = p.seed;
     p.rng_state[1] = p.offset;
   }
-  const int m0 = m_block * kFwdBM;
+  const int m0 = m_block * BM;
   if (m0 >= sq) return;
 
   typedef unsigned short u16;
@@ -97,39 +107,72 @@ __global__ void __launch_bounds__(256, 2) fwd_kernel(const FwdParams p) {
     }
   }
 
-  const int n_end = CAUSAL ? min(sk, m0 + kFwdBM) : sk;
+  const int n_end = CAUSAL ? min(sk, m0 + BM) : sk;
   const int nblk = n_end > 0 ? (n_end + BN - 1) / BN : 0;
+  // tiles [0, nfast) need no mask for any row of the workgroup
+  const int nfast = min(nblk, (CAUSAL ? min(sk, m0 + 1) : sk) / BN);
 
-  // ---- register staging of K/V tiles ----
-  u32x4_t stk[LOADS], stv[LOADS];
-  auto issue = [&](int n0) {
+  // ---- LDS-DMA of K/V tiles: per-lane byte offsets of this wave's 1-KiB pieces ----
+  // piece pc covers rows 16*(pc % (BN/16)) .. +15 of panel pc / (BN/16); lane l writes
+  // (row = l/4, slot = l%4), i.e. logical chunk slot ^ ((row >> 2) & 3) (panel XOR swizzle).
+  int voff_k[PPW], voff_v[PPW];
 #pragma unroll
-    for (int i = 0; i < LOADS; ++i) {
-      const int pid = i * 32 + (tid >> 3);
-      const int panel = pid % NP;
-      const int row = 2 * (pid / NP) + ((tid >> 2) & 1);
-      const int d0 = panel * 32 + (tid & 3) * 8;
-      const int key = n0 + row;
-      const bool ok = (pid < NPAIR) && key < sk && d0 < dlim;
-      const int64_t kr = ok ? key : 0;
-      stk[i] = ld16(K + kr * p.k_row + d0, ok);
-      stv[i] = ld16(V + kr * p.v_row + d0, ok);
-    }
-  };
-  auto commit = [&](int buf) {
-    char* kt = smem + buf * 2 * TILE;
-    char* vt = kt + TILE;
+  for (int j = 0; j < PPW; ++j) {
+    const int pc = wave + j * NW;
+    const int panel = pc / (BN / 16);
+    const int row = (pc % (BN / 16)) * 16 + (lane >> 2);
+    const int col = panel * 32 + (((lane & 3) ^ ((row >> 2) & 3)) << 3);
+    const bool ok = col < dlim;
+    voff_k[j] = ok ? (int)(((int64_t)row * p.k_row + col) * 2) : 0x7ffffff0;
+    voff_v[j] = ok ? (int)(((int64_t)row * p.v_row + col) * 2) : 0x7ffffff0;
+  }
+  auto issue = [&](int nb) {
+    const int n0 = nb * BN;
+    char* dst = smem + (nb % kFwdBufs) * 2 * TILE;
+    const int64_t kb = (int64_t)(sk - n0) * p.k_row * 2, vb = (int64_t)(sk - n0) * p.v_row * 2;
+    const int krec = (int)(kb > 0x7fffffff ? 0x7fffffff : kb);
+    const int vrec = (int)(vb > 0x7fffffff ? 0x7fffffff : vb);
+    const buf_rsrc_t rk = make_rsrc(K + (int64_t)n0 * p.k_row, krec);
+    const buf_rsrc_t rv = make_rsrc(V + (int64_t)n0 * p.v_row, vrec);
 #pragma unroll
-    for (int i = 0; i < LOADS; ++i) {
-      const int pid = i * 32 + (tid >> 3);
-      if (NPAIR % 32 == 0 || pid < NPAIR) {
-        const int panel = pid % NP;
-        const int row = 2 * (pid / NP) + ((tid >> 2) & 1);
-        const int off = panel_off(row, panel * 4 + (tid & 3), BN);
-        *(u32x4_t*)(kt + off) = stk[i];
-        *(u32x4_t*)(vt + off) = stv[i];
+    for (int j = 0; j < PPW; ++j) {
+      const int pc = wave + j * NW;
+      if (PIECES % NW == 0 || pc < PIECES) {
+        dma16(rk, dst + pc * 1024, voff_k[j]);
+        dma16(rv, dst + TILE + pc * 1024, voff_v[j]);
       }
     }
+  };
+  auto tile_sync = [&]() { wait_dma_and_barrier(); };
+
+  // S^T = K Q^T for the tile in buffer kt (K fragments issued in groups of KG ahead of their MFMAs)
+  constexpr int KG = (KS % 4 == 0) ? 4 : ((KS % 3 == 0) ? 3 : 2);
+  static_assert(KS % KG == 0, "K fragment group must divide the k-steps");
+  auto qk = [&](int kt_off, f32x16_t (&st)[NT]) {
+    const TileAddr ta(lb, kt_off);
+    static_for<0, NT>([&](auto T) {
+      constexpr int t = decltype(T)::value;
+#pragma unroll
+      for (int g = 0; g < 16; ++g) st[t][g] = 0.f;
+      static_for<0, KS / KG>([&](auto GG) {
+        constexpr int g0 = decltype(GG)::value * KG;
+        i16x8_t ka[KG];
+        static_for<0, KG>([&](auto KK) {
+          constexpr int ks = g0 + decltype(KK)::value;
+          ka[ks - g0] = row_read_c<BN, t * 32, 2 * ks>(smem, ta);
+        });
+#pragma unroll
+        for (int k = 0; k < KG; ++k) st[t] = E::mfma(ka[k], qf[g0 + k], st[t]);
+      });
+    });
+  };
+  auto rowmax = [&](const f32x16_t (&st)[NT]) {
+    float mx[4] = {kNegInf, kNegInf, kNegInf, kNegInf};
+#pragma unroll
+    for (int t = 0; t < NT; ++t)
+#pragma unroll
+      for (int g = 0; g < 16; ++g) mx[g & 3] = fmaxf(mx[g & 3], st[t][g]);
+    return half_swap_max(fmaxf(fmaxf(mx[0], mx[1]), fmaxf(mx[2], mx[3])));
   };
 
   float m_run = kNegInf, l_run = 0.f;
@@ -140,92 +183,111 @@ __global__ void __launch_bounds__(256, 2) fwd_kernel(const FwdParams p) {
     for (int g = 0; g < 16; ++g) o[t][g] = 0.f;
   const float c = s.scale_log2;
 
-  if (nblk > 0) {
-    issue(0);
-    commit(0);
-    __syncthreads();
-  }
-
-  for (int nb = 0; nb < nblk; ++nb) {
-    const int n0 = nb * BN;
-    const int cur = nb & 1;
-    const bool has_next = nb + 1 < nblk;
-    if (has_next) issue(n0 + BN);
-    const char* kt = smem + cur * 2 * TILE;
-    const char* vt = kt + TILE;
-
-    const bool active = (wq0 < sq) && (!CAUSAL || n0 <= wq0 + 31);
-    if (active) {
-      // S^T[key][query] for NT subtiles of 32 keys
-      f32x16_t st[NT];
-#pragma unroll
-      for (int t = 0; t < NT; ++t) {
-#pragma unroll
-        for (int g = 0; g < 16; ++g) st[t][g] = 0.f;
-#pragma unroll
-        for (int ks = 0; ks < KS; ++ks)
-          st[t] = E::mfma(row_read(kt, t * 32 + r, 2 * ks + hh, BN), qf[ks], st[t]);
-      }
-      const bool need_mask = (n0 + BN > sk) || (CAUSAL && n0 + BN - 1 > wq0);
-      if (need_mask) {
-#pragma unroll
-        for (int t = 0; t < NT; ++t)
-#pragma unroll
-          for (int g = 0; g < 16; ++g) {
-            const int key = n0 + t * 32 + acc_row(g, hh);
-            if (key >= sk || (CAUSAL && key > qi)) st[t][g] = kNegInf;
-          }
-      }
-      float mt = kNegInf;
-#pragma unroll
-      for (int t = 0; t < NT; ++t)
-#pragma unroll
-        for (int g = 0; g < 16; ++g) mt = fmaxf(mt, st[t][g]);
-      mt = half_swap_max(mt);
-      const float m_new = fmaxf(m_run, mt);
-      const float ms = (m_new == kNegInf) ? 0.f : m_new * c;
-      const float alpha = fast_exp2(m_run * c - ms);
-      float ls = 0.f;
-#pragma unroll
-      for (int t = 0; t < NT; ++t)
-#pragma unroll
-        for (int g = 0; g < 16; ++g) {
-          const float pv = fast_exp2(fmaf(st[t][g], c, -ms));
-          st[t][g] = pv;
-          ls += pv;
-        }
-      l_run = l_run * alpha + ls;
-      m_run = m_new;
+  // online-softmax update for a tile whose row max (incl. the other lane half) is mt
+  auto rescale = [&](float mt) {
+    const float m_new = fmaxf(m_run, mt);
+    if (__any(m_new != m_run)) {
+      const float alpha = fast_exp2(m_run * c - ((m_new == kNegInf) ? 0.f : m_new * c));
+      l_run *= alpha;
 #pragma unroll
       for (int t = 0; t < NP; ++t)
 #pragma unroll
         for (int g = 0; g < 16; ++g) o[t][g] *= alpha;
-
-      i16x8_t pf[2 * NT];
-#pragma unroll
-      for (int t = 0; t < NT; ++t) {
-        pf[2 * t] = pack_frag<BF16>(st[t], 0);
-        pf[2 * t + 1] = pack_frag<BF16>(st[t], 1);
-      }
-      // O^T[d][q] += V^T[d][key] P^T[key][q]
-#pragma unroll
-      for (int dt = 0; dt < NP; ++dt)
-#pragma unroll
-        for (int t = 0; t < NT; ++t)
-#pragma unroll
-          for (int s2 = 0; s2 < 2; ++s2) {
-            const i16x8_t a = tr_frag(vt, t * 32 + 16 * s2 + 4 * hh, dt * 32 + 16 * (r >> 4), BN, i16);
-            o[dt] = E::mfma(a, pf[2 * t + s2], o[dt]);
-          }
+      m_run = m_new;
     }
-    if (has_next) commit(cur ^ 1);
-    __syncthreads();
+  };
+  // P = exp2(S c - m c) -> packed B operands; returns the partial row sum of this lane
+  auto softmax_pack = [&](f32x16_t (&st)[NT], i16x8_t (&pf)[2 * NT]) {
+    const float ms = (m_run == kNegInf) ? 0.f : m_run * c;
+    float ls[4] = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int t = 0; t < NT; ++t) {
+#pragma unroll
+      for (int g = 0; g < 16; ++g) {
+        const float pv = fast_exp2(fmaf(st[t][g], c, -ms));
+        st[t][g] = pv;
+        ls[g & 3] += pv;
+      }
+      pf[2 * t] = pack_frag<BF16>(st[t], 0);
+      pf[2 * t + 1] = pack_frag<BF16>(st[t], 1);
+    }
+    l_run += (ls[0] + ls[1]) + (ls[2] + ls[3]);
+  };
+  // O^T[d][q] += V^T[d][key] P^T[key][q], one 32-wide d tile at a time
+  auto pv = [&](int vt_off, const i16x8_t (&pf)[2 * NT]) {
+    const TileAddr ta(lb, vt_off);
+    static_for<0, NP>([&](auto DTC) {
+      constexpr int dt = decltype(DTC)::value;
+      i16x8_t a[2 * NT];
+      static_for<0, 2 * NT>([&](auto KC) {
+        constexpr int kk = decltype(KC)::value;
+        a[kk] = tr_frag_c<BN, kk * 16, dt>(smem, ta);
+      });
+#pragma unroll
+      for (int kk = 0; kk < 2 * NT; ++kk) o[dt] = E::mfma(a[kk], pf[kk], o[dt]);
+    });
+  };
+
+  if (nblk > 0) issue(0);
+  if (nblk > 1) issue(1);
+  tile_sync();
+
+  // ---- fast path: unmasked tiles, QK^T of the next tile overlapped with this tile's softmax ----
+  if (nfast > 0) {
+    f32x16_t sa[NT], sb[NT];
+    qk(0, sa);
+    float mt = rowmax(sa);
+    auto body = [&](int nb, f32x16_t (&scur)[NT], f32x16_t (&snxt)[NT]) {
+      if (nb + 2 < nblk) issue(nb + 2);
+      rescale(mt);
+      const int cur = (nb % kFwdBufs) * 2 * TILE;
+      const int nxt = ((nb + 1) % kFwdBufs) * 2 * TILE;
+      i16x8_t pf[2 * NT];
+      softmax_pack(scur, pf);
+      // tile nb+1 is resident (possibly past nblk: then its scores are simply discarded); its
+      // MFMAs are independent of the softmax above, so the two interleave in this basic block
+      qk(nxt, snxt);
+      __builtin_amdgcn_sched_barrier(0);   // bound the V-read hoisting (register pressure)
+      pv(cur + TILE, pf);
+      mt = rowmax(snxt);
+      tile_sync();
+    };
+    int nb = 0;
+    for (; nb + 1 < nfast; nb += 2) {
+      body(nb, sa, sb);
+      body(nb + 1, sb, sa);
+    }
+    if (nb < nfast) body(nb, sa, sb);
+  }
+
+  // ---- general path: causal diagonal / ragged tiles, per-element masks ----
+  for (int nb = nfast; nb < nblk; ++nb) {
+    const int n0 = nb * BN;
+    if (nb + 2 < nblk) issue(nb + 2);
+    const int cur = (nb % kFwdBufs) * 2 * TILE;
+    const bool active = (wq0 < sq) && (!CAUSAL || n0 <= wq0 + 31);
+    if (active) {
+      f32x16_t st[NT];
+      qk(cur, st);
+#pragma unroll
+      for (int t = 0; t < NT; ++t)
+#pragma unroll
+        for (int g = 0; g < 16; ++g) {
+          const int key = n0 + t * 32 + acc_row(g, hh);
+          if (key >= sk || (CAUSAL && key > qi)) st[t][g] = kNegInf;
+        }
+      rescale(rowmax(st));
+      i16x8_t pf[2 * NT];
+      softmax_pack(st, pf);
+      pv(cur + TILE, pf);
+    }
+    tile_sync();
   }
 
   // ---- epilogue ----
   const float l_tot = half_swap_sum(l_run);
   const bool bad = (l_tot == 0.f) || (l_tot != l_tot);
-  const float inv = bad ? 1.f : 1.f / l_tot;
+  const float inv = bad ? 1.f : fast_rcp(l_tot);
   const float lse = bad ? __builtin_huge_valf() : m_run * s.scale + __logf(l_tot);
   if (qi < sq) {
     u16* orow = O + (int64_t)qi * p.o_row;
@@ -249,7 +311,7 @@ template <bool BF16, int D, bool CAUSAL>
 static void run_fwd(const FwdParams& p, hipStream_t stream) {
   dim3 grid(p.s.b * p.s.h, p.num_m_blocks);
   prof_begin(kTimeFwd, stream);
-  hipLaunchKernelGGL((fwd_kernel<BF16, D, CAUSAL>), grid, dim3(256), 0, stream, p);
+  hipLaunchKernelGGL((fwd_kernel<BF16, D, CAUSAL>), grid, dim3(kFwdWaves * 64), 0, stream, p);
   prof_end(kTimeFwd, stream);
 }
 
@@ -265,7 +327,7 @@ static void dispatch_d(const FwdParams& p, hipStream_t stream) {
 
 void fwd_block_size(int d, int* block_m, int* block_n) {
   *block_m = kFwdBM;
-  *block_n = 64;
+  *block_n = kFwdBN;
   (void)d;
 }
 

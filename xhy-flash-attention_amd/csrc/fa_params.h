@@ -73,7 +73,7 @@ void fwd_block_size(int d, int* block_m, int* block_n);
 void bwd_block_size(int d, int* block_m, int* block_n);
 
 // Optional HIP-event timing around each kernel launch (fa_timing.cpp).
-enum TimedKernel { kTimeFwd = 0, kTimeBwdPre = 1, kTimeBwdMain = 2, kTimeBwdDq = 3, kNumTimedKernels = 4 };
+enum TimedKernel { kTimeFwd = 0, kTimeBwdPre = 1, kTimeBwdMain = 2 /* dK/dV */, kTimeBwdDq = 3, kNumTimedKernels = 4 };
 void prof_begin(int id, hipStream_t s);
 void prof_end(int id, hipStream_t s);
 

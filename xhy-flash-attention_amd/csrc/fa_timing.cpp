@@ -76,7 +76,7 @@ void flash_attn_timing_enable(int enable) {
 }
 
 // Total device milliseconds and launch count of kernel `id` since the last enable
-// (0 fwd, 1 bwd_pre, 2 bwd_main, 3 bwd_dq).  Synchronises on the recorded events.
+// (0 fwd, 1 bwd_pre, 2 bwd_dkdv, 3 bwd_dq).  Synchronises on the recorded events.
 void flash_attn_timing_read(int id, double* total_ms, long* count) {
   std::lock_guard<std::mutex> lk(fa::g_mu);
   fa::drain_locked();
