@@ -9,21 +9,25 @@
 // MI355X design (not the reference's seqk-parallel kernel with fp32 dQ atomics, which on this chip
 // is bound by the ~1.3 TB/s global-atomic rate: 8.7 GB of dQ adds at the C3 headline shape):
 //   1. bwd_pre_kernel   D = rowsum(dO o O)  (one 16-lane group per query row)
-//   2. bwd_dkdv_kernel  one workgroup per 128-key block of a (batch, kv-head); K and V fragments
-//                       live in registers, 64-row (Q, dO) slices stream through LDS; dK^T / dV^T
-//                       accumulate in registers over every query slice (and, for GQA, every query
-//                       head of the group) and are written once: 4 MFMA GEMMs per tile, no atomics.
-//   3. bwd_dq_kernel    one workgroup per 128-row query block, structured like the forward: Q and
-//                       dO fragments in registers, K/V tiles streamed through LDS, S^T and dP^T with
-//                       the query on the MFMA lane (LSE and D become per-lane scalars), dQ^T += K^T dS^T
-//                       with dS^T used in-register as the MFMA B operand; dQ written directly in
-//                       bf16/f16 (no fp32 accumulator buffer, no conversion pass).
+//   2. bwd_dkdv_kernel  one workgroup (4 waves, one per SIMD, full 512-entry register file) per
+//                       128-key block of a (batch, kv-head); each wave's 32 keys of K and V stay in
+//                       registers, (Q, dO, LSE, D) slices of 64 query rows arrive by LDS-DMA two
+//                       slices ahead into a 3-deep ring; dK^T / dV^T accumulate in registers over
+//                       every slice (and, for GQA, every query head of the group) and are written
+//                       once: 4 MFMA GEMMs per tile, no atomics.
+//   3. bwd_dq_kernel    one workgroup (8 waves) per 256-row query block, structured like the
+//                       forward: Q and dO fragments in registers, K/V tiles by LDS-DMA ring,
+//                       S^T and dP^T with the query on the MFMA lane (LSE and D are per-lane
+//                       scalars), dQ^T += K^T dS^T with dS^T used in-register as the B operand;
+//                       dQ written directly in bf16/f16 (no fp32 accumulator, no conversion pass).
 // Both main kernels are deterministic (no atomics), so dQ is bitwise reproducible too.
 //
 //   * "Key on the lane" in dkdv: S = Q K^T and dP = dO V^T have the key on the MFMA column, so
 //     their accumulators are directly the B operands of dV^T = dO^T P and dK^T = Q^T dS; dO^T and
 //     Q^T come from the row-major LDS slice through ds_read_b64_tr_b16.
 //   * Row constants as the initial accumulator in dkdv: S starts at -LSE/scale and dP at -D.
+//   * Slices / tiles that need no mask run a branch-free body (the two 32-row q-tiles of a slice,
+//     resp. the S / dP chains of a tile, interleave in one basic block).
 #include <stdexcept>
 #include <string>
 
@@ -37,8 +41,10 @@ typedef unsigned short u16;
 constexpr int kDkdvWaves = 4;
 constexpr int kDkdvBN = 32 * kDkdvWaves;  // keys per dK/dV workgroup
 constexpr int kDkdvBQ = 64;               // query rows per sweep step
-constexpr int kDqBM = 128;                // query rows per dQ workgroup (4 waves x 32)
+constexpr int kDqWaves = 8;
+constexpr int kDqBM = 32 * kDqWaves;      // query rows per dQ workgroup
 constexpr int kDqBN = 64;                 // keys per streamed K/V tile
+constexpr int kBwdBufs = 3;
 
 // ------------------------------------------------------------------------------------------------
 // geometry shared by the kernels (reference BlockInfo, block_info.h:14-31)
@@ -75,6 +81,21 @@ __device__ inline SeqGeom seq_geom(const BwdParams& p, int bidb) {
   return g;
 }
 
+// bytes of rows [0, rows) of a strided operand, clamped to the buffer descriptor's range
+__device__ inline int rec_bytes(int rows, int64_t row_stride, int elem_bytes) {
+  const int64_t b = (int64_t)(rows > 0 ? rows : 0) * row_stride * elem_bytes;
+  return (int)(b > 0x7fffffff ? 0x7fffffff : b);
+}
+
+// per-lane byte offset of piece `pc` of a panel-layout tile of NR rows (see fa_fwd.hip)
+template <int NR>
+__device__ inline int dma_voff(int pc, int lane, int64_t row_stride, int dlim) {
+  const int panel = pc / (NR / 16);
+  const int row = (pc % (NR / 16)) * 16 + (lane >> 2);
+  const int col = panel * 32 + (((lane & 3) ^ ((row >> 2) & 3)) << 3);
+  return col < dlim ? (int)(((int64_t)row * row_stride + col) * 2) : 0x7ffffff0;
+}
+
 // ------------------------------------------------------------------------------------------------
 // 1. D = rowsum(dO * O)
 // ------------------------------------------------------------------------------------------------
@@ -109,20 +130,24 @@ __global__ void __launch_bounds__(256) bwd_pre_kernel(const BwdParams p) {
 // 2. dK / dV
 // ------------------------------------------------------------------------------------------------
 template <bool BF16, int D, bool CAUSAL>
-__global__ void __launch_bounds__(256, 1) bwd_dkdv_kernel(const BwdParams p) {
+__global__ void __launch_bounds__(kDkdvWaves * 64, 1) bwd_dkdv_kernel(const BwdParams p) {
   using E = Elt<BF16>;
+  constexpr int NW = kDkdvWaves;
   constexpr int BQ = kDkdvBQ;
   constexpr int KS = D / 16;
   constexpr int NP = D / 32;
   constexpr int QTILE = BQ * D * 2;                 // bytes of a Q or dO slice
-  constexpr int SLICE = 2 * QTILE + 2 * BQ * 4;     // Q | dO | lse[BQ] | dsum[BQ]
-  constexpr int QPAIR = BQ * NP / 2;                // (2 rows x 64 B) staging units per slice
-  constexpr int QLOADS = (QPAIR + 31) / 32;
-  __shared__ __attribute__((aligned(16))) char smem[2 * SLICE];
+  constexpr int SLICE = 2 * QTILE + 2 * BQ * 4;     // Q | dO | lse[BQ] | D[BQ]
+  constexpr int PIECES = QTILE / 1024;
+  constexpr int PPW = (PIECES + NW - 1) / NW;
+  static_assert(QTILE % 1024 == 0, "slice must be whole DMA pieces");
+  __shared__ __attribute__((aligned(16))) char smem[kBwdBufs * SLICE];
 
   const AttnShape s = p.s;
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int r = lane & 31, hh = lane >> 5, i16 = lane & 15;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = wave_uniform(tid >> 6);
+  const int r = lane & 31, hh = lane >> 5;
+  const LdsBases lb(lane);
   const int group = s.h / s.hk;
 
   const int nheads_grid = p.gqa_reduce ? s.hk : s.h;
@@ -159,49 +184,33 @@ __global__ void __launch_bounds__(256, 1) bwd_dkdv_kernel(const BwdParams p) {
   const int ns = m_count > m_first ? m_count - m_first : 0;
   const int total = ns * nh;
 
-  u32x4_t stq[QLOADS], sto[QLOADS];
-  float st_ld = 0.f;
+  int voff_q[PPW], voff_o[PPW];
+#pragma unroll
+  for (int j = 0; j < PPW; ++j) {
+    voff_q[j] = dma_voff<BQ>(wave + j * NW, lane, p.q_row, dlim);
+    voff_o[j] = dma_voff<BQ>(wave + j * NW, lane, p.do_row, dlim);
+  }
   auto issue = [&](int it) {
     const int hq = h_begin + it / ns;
     const int q0 = (m_first + it % ns) * BQ;
-    const u16* Qp = (const u16*)p.q + geo.q_off + (int64_t)hq * p.q_head;
-    const u16* Dp = (const u16*)p.dout + geo.do_off + (int64_t)hq * p.do_head;
+    char* dst = smem + (it % kBwdBufs) * SLICE;
+    const u16* Qp = (const u16*)p.q + geo.q_off + (int64_t)hq * p.q_head + (int64_t)q0 * p.q_row;
+    const u16* Dp = (const u16*)p.dout + geo.do_off + (int64_t)hq * p.do_head + (int64_t)q0 * p.do_row;
+    const buf_rsrc_t rq = make_rsrc(Qp, rec_bytes(sq - q0, p.q_row, 2));
+    const buf_rsrc_t ro = make_rsrc(Dp, rec_bytes(sq - q0, p.do_row, 2));
 #pragma unroll
-    for (int i = 0; i < QLOADS; ++i) {
-      const int pid = i * 32 + (tid >> 3);
-      const int panel = pid % NP;
-      const int row = 2 * (pid / NP) + ((tid >> 2) & 1);
-      const int d0 = panel * 32 + (tid & 3) * 8;
-      const int qrow = q0 + row;
-      const bool ok = (pid < QPAIR) && qrow < sq && d0 < dlim;
-      const int64_t qr = ok ? qrow : 0;
-      stq[i] = ld16(Qp + qr * p.q_row + d0, ok);
-      sto[i] = ld16(Dp + qr * p.do_row + d0, ok);
-    }
-    if (tid < 2 * BQ) {   // [0, BQ): lse, [BQ, 2BQ): D
-      const int row = tid & (BQ - 1);
-      const int qrow = q0 + row;
-      const int64_t bhi = (int64_t)bidb * s.h + hq;
-      if (qrow < sq) st_ld = (tid < BQ) ? p.lse[bhi * s.lse_pitch + qrow] : p.dsum[bhi * p.seqlen_q_rounded + qrow];
-      else st_ld = (tid < BQ) ? __builtin_huge_valf() : 0.f;
-    }
-  };
-  auto commit = [&](int buf) {
-    char* qt = smem + buf * SLICE;
-    char* ot = qt + QTILE;
-    float* lt = (float*)(qt + 2 * QTILE);
-#pragma unroll
-    for (int i = 0; i < QLOADS; ++i) {
-      const int pid = i * 32 + (tid >> 3);
-      if (QPAIR % 32 == 0 || pid < QPAIR) {
-        const int panel = pid % NP;
-        const int row = 2 * (pid / NP) + ((tid >> 2) & 1);
-        const int off = panel_off(row, panel * 4 + (tid & 3), BQ);
-        *(u32x4_t*)(qt + off) = stq[i];
-        *(u32x4_t*)(ot + off) = sto[i];
+    for (int j = 0; j < PPW; ++j) {
+      const int pc = wave + j * NW;
+      if (PIECES % NW == 0 || pc < PIECES) {
+        dma16(rq, dst + pc * 1024, voff_q[j]);
+        dma16(ro, dst + QTILE + pc * 1024, voff_o[j]);
       }
     }
-    if (tid < 2 * BQ) lt[tid] = st_ld;
+    if (wave < 2) {   // wave 0: LSE rows, wave 1: D rows (64 x 4 bytes each)
+      const int64_t bhi = (int64_t)bidb * s.h + hq;
+      const float* src = (wave == 0) ? p.lse + bhi * s.lse_pitch + q0 : p.dsum + bhi * p.seqlen_q_rounded + q0;
+      dma4(make_rsrc(src, rec_bytes(sq - q0, 1, 4)), dst + 2 * QTILE + wave * BQ * 4, lane * 4);
+    }
   };
 
   f32x16_t dvt[NP], dkt[NP];
@@ -213,67 +222,78 @@ __global__ void __launch_bounds__(256, 1) bwd_dkdv_kernel(const BwdParams p) {
   const float inv_scale = 1.f / s.scale;
   const float c = s.scale_log2;
 
-  if (total > 0) {
-    issue(0);
-    commit(0);
-  }
-  __syncthreads();
+  // one 32-row q-tile QI of the slice at byte offset `so`; MASK adds the causal / bound masks
+  auto qtile = [&](auto QIC, auto MASKC, int so, int q0) {
+    constexpr int QI = decltype(QIC)::value;
+    constexpr bool MASK = decltype(MASKC)::value;
+    const int qa = q0 + 32 * QI;
+    const TileAddr tq(lb, so), to(lb, so + QTILE);
+    const float* lt = (const float*)(smem + so + 2 * QTILE);
+    // S' = Q K^T - LSE/scale ; dP' = dO V^T - D      (query on registers, key on lane)
+    f32x16_t sacc, pacc;
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const f32x4_t lv = *(const f32x4_t*)(lt + 32 * QI + 8 * u + 4 * hh);
+      const f32x4_t dv = *(const f32x4_t*)(lt + BQ + 32 * QI + 8 * u + 4 * hh);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) { sacc[4 * u + j] = -lv[j] * inv_scale; pacc[4 * u + j] = -dv[j]; }
+    }
+    i16x8_t qa_f[KS], oa_f[KS];
+    static_for<0, KS>([&](auto KK) {
+      constexpr int ks = decltype(KK)::value;
+      qa_f[ks] = row_read_c<BQ, 32 * QI, 2 * ks>(smem, tq);
+      oa_f[ks] = row_read_c<BQ, 32 * QI, 2 * ks>(smem, to);
+    });
+#pragma unroll
+    for (int ks = 0; ks < KS; ++ks) {
+      sacc = E::mfma(qa_f[ks], kf[ks], sacc);
+      pacc = E::mfma(oa_f[ks], vf[ks], pacc);
+    }
+#pragma unroll
+    for (int g = 0; g < 16; ++g) {
+      float pv = fast_exp2(sacc[g] * c);
+      if constexpr (MASK) {
+        const int q = qa + acc_row(g, hh);
+        if (key >= sk || q >= sq || (CAUSAL && key > q)) pv = 0.f;
+      }
+      sacc[g] = pv;
+      pacc[g] = pv * pacc[g];
+    }
+    const i16x8_t pf0 = pack_frag<BF16>(sacc, 0), pf1 = pack_frag<BF16>(sacc, 1);
+    const i16x8_t df0 = pack_frag<BF16>(pacc, 0), df1 = pack_frag<BF16>(pacc, 1);
+    // dV^T += dO^T P ; dK^T += Q^T dS
+    static_for<0, NP>([&](auto DTC) {
+      constexpr int dt = decltype(DTC)::value;
+      const i16x8_t o0 = tr_frag_c<BQ, 32 * QI, dt>(smem, to);
+      const i16x8_t o1 = tr_frag_c<BQ, 32 * QI + 16, dt>(smem, to);
+      const i16x8_t q0f = tr_frag_c<BQ, 32 * QI, dt>(smem, tq);
+      const i16x8_t q1f = tr_frag_c<BQ, 32 * QI + 16, dt>(smem, tq);
+      dvt[dt] = E::mfma(o0, pf0, dvt[dt]);
+      dvt[dt] = E::mfma(o1, pf1, dvt[dt]);
+      dkt[dt] = E::mfma(q0f, df0, dkt[dt]);
+      dkt[dt] = E::mfma(q1f, df1, dkt[dt]);
+    });
+  };
+
+  if (total > 0) issue(0);
+  if (total > 1) issue(1);
+  wait_dma_and_barrier();
 
   for (int it = 0; it < total; ++it) {
-    const int cur = it & 1;
     const int q0 = (m_first + it % ns) * BQ;
-    const bool has_next = it + 1 < total;
-    if (has_next) issue(it + 1);
-
-    const char* qt = smem + cur * SLICE;
-    const char* ot = qt + QTILE;
-    const float* lt = (const float*)(qt + 2 * QTILE);
-
-#pragma unroll
-    for (int qi = 0; qi < BQ / 32; ++qi) {
-      const int qa = q0 + 32 * qi;   // first query row of this 32-row tile
-      const bool skip = (qa >= sq) || (CAUSAL && kw0 > qa + 31);
-      if (!skip) {
-        // S' = Q K^T - LSE/scale ; dP' = dO V^T - D      (query on registers, key on lane)
-        f32x16_t sacc, pacc;
-#pragma unroll
-        for (int u = 0; u < 4; ++u) {
-          const f32x4_t lv = *(const f32x4_t*)(lt + 32 * qi + 8 * u + 4 * hh);
-          const f32x4_t dv = *(const f32x4_t*)(lt + BQ + 32 * qi + 8 * u + 4 * hh);
-#pragma unroll
-          for (int j = 0; j < 4; ++j) { sacc[4 * u + j] = -lv[j] * inv_scale; pacc[4 * u + j] = -dv[j]; }
-        }
-#pragma unroll
-        for (int ks = 0; ks < KS; ++ks) {
-          sacc = E::mfma(row_read(qt, 32 * qi + r, 2 * ks + hh, BQ), kf[ks], sacc);
-          pacc = E::mfma(row_read(ot, 32 * qi + r, 2 * ks + hh, BQ), vf[ks], pacc);
-        }
-        const bool need_mask = (key >= sk) || (qa + 32 > sq) || (CAUSAL && kw0 + 31 > qa);
-#pragma unroll
-        for (int g = 0; g < 16; ++g) {
-          float pv = fast_exp2(sacc[g] * c);
-          if (need_mask) {
-            const int q = qa + acc_row(g, hh);
-            if (key >= sk || q >= sq || (CAUSAL && key > q)) pv = 0.f;
-          }
-          sacc[g] = pv;
-          pacc[g] = pv * pacc[g];
-        }
-        const i16x8_t pf0 = pack_frag<BF16>(sacc, 0), pf1 = pack_frag<BF16>(sacc, 1);
-        const i16x8_t df0 = pack_frag<BF16>(pacc, 0), df1 = pack_frag<BF16>(pacc, 1);
-        // dV^T += dO^T P ; dK^T += Q^T dS
-#pragma unroll
-        for (int dt = 0; dt < NP; ++dt) {
-          const int col0 = dt * 32 + 16 * (r >> 4);
-          dvt[dt] = E::mfma(tr_frag(ot, 32 * qi + 4 * hh, col0, BQ, i16), pf0, dvt[dt]);
-          dvt[dt] = E::mfma(tr_frag(ot, 32 * qi + 16 + 4 * hh, col0, BQ, i16), pf1, dvt[dt]);
-          dkt[dt] = E::mfma(tr_frag(qt, 32 * qi + 4 * hh, col0, BQ, i16), df0, dkt[dt]);
-          dkt[dt] = E::mfma(tr_frag(qt, 32 * qi + 16 + 4 * hh, col0, BQ, i16), df1, dkt[dt]);
-        }
-      }
+    if (it + 2 < total) issue(it + 2);
+    const int so = (it % kBwdBufs) * SLICE;
+    const bool fast = (q0 + BQ <= sq) && (n0 + kDkdvBN <= sk) && (!CAUSAL || q0 >= n0 + kDkdvBN - 1);
+    if (fast) {
+      qtile(std::integral_constant<int, 0>{}, std::false_type{}, so, q0);
+      qtile(std::integral_constant<int, 1>{}, std::false_type{}, so, q0);
+    } else {
+      static_for<0, BQ / 32>([&](auto QIC) {
+        const int qa = q0 + 32 * decltype(QIC)::value;
+        if (qa < sq && !(CAUSAL && kw0 > qa + 31)) qtile(QIC, std::true_type{}, so, q0);
+      });
     }
-    if (has_next) commit(cur ^ 1);
-    __syncthreads();
+    wait_dma_and_barrier();
   }
 
   // ---- epilogue: dK = scale * (dK^T)^T, dV = (dV^T)^T ----
@@ -304,28 +324,34 @@ __global__ void __launch_bounds__(256, 1) bwd_dkdv_kernel(const BwdParams p) {
 // 3. dQ  (forward-shaped: query on the lane, K/V streamed)
 // ------------------------------------------------------------------------------------------------
 template <bool BF16, int D, bool CAUSAL>
-__global__ void __launch_bounds__(256, 1) bwd_dq_kernel(const BwdParams p) {
+__global__ void __launch_bounds__(kDqWaves * 64, 2) bwd_dq_kernel(const BwdParams p) {
   using E = Elt<BF16>;
+  constexpr int NW = kDqWaves;
   constexpr int BN = kDqBN;
+  constexpr int BM = kDqBM;
   constexpr int KS = D / 16;
   constexpr int NT = BN / 32;
   constexpr int NP = D / 32;
   constexpr int TILE = BN * D * 2;
-  constexpr int NPAIR = BN * NP / 2;
-  constexpr int LOADS = (NPAIR + 31) / 32;
-  __shared__ __attribute__((aligned(16))) char smem[4 * TILE];  // [buffer][K | V]
+  constexpr int PIECES = TILE / 1024;
+  constexpr int PPW = (PIECES + NW - 1) / NW;
+  constexpr int KG = (KS % 4 == 0) ? 4 : ((KS % 3 == 0) ? 3 : 2);
+  static_assert(TILE % 1024 == 0 && KS % KG == 0, "tile shape");
+  __shared__ __attribute__((aligned(16))) char smem[kBwdBufs * 2 * TILE];  // [buffer][K | V]
 
   const AttnShape s = p.s;
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int r = lane & 31, hh = lane >> 5, i16 = lane & 15;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = wave_uniform(tid >> 6);
+  const int r = lane & 31, hh = lane >> 5;
+  const LdsBases lb(lane);
   const int bidb = blockIdx.x / s.h;
   const int head = blockIdx.x - bidb * s.h;
   const int kvh = head / (s.h / s.hk);
-  const int num_m = (s.seqlen_q + kDqBM - 1) / kDqBM;
+  const int num_m = (s.seqlen_q + BM - 1) / BM;
   const int m_block = num_m - 1 - (int)blockIdx.y;   // heaviest causal blocks first
   const SeqGeom geo = seq_geom(p, bidb);
   const int sq = geo.sq, sk = geo.sk;
-  const int m0 = m_block * kDqBM;
+  const int m0 = m_block * BM;
   if (m0 >= sq) return;
   const int dlim = s.d;
 
@@ -356,36 +382,27 @@ __global__ void __launch_bounds__(256, 1) bwd_dq_kernel(const BwdParams p) {
     dsum_q = p.dsum[bhi * p.seqlen_q_rounded + qi];
   }
 
-  const int n_end = CAUSAL ? min(sk, m0 + kDqBM) : sk;
+  const int n_end = CAUSAL ? min(sk, m0 + BM) : sk;
   const int nblk = n_end > 0 ? (n_end + BN - 1) / BN : 0;
+  const int nfast = min(nblk, (CAUSAL ? min(sk, m0 + 1) : sk) / BN);
 
-  u32x4_t stk[LOADS], stv[LOADS];
-  auto issue = [&](int n0) {
+  int voff_k[PPW], voff_v[PPW];
 #pragma unroll
-    for (int i = 0; i < LOADS; ++i) {
-      const int pid = i * 32 + (tid >> 3);
-      const int panel = pid % NP;
-      const int row = 2 * (pid / NP) + ((tid >> 2) & 1);
-      const int d0 = panel * 32 + (tid & 3) * 8;
-      const int kr = n0 + row;
-      const bool ok = (pid < NPAIR) && kr < sk && d0 < dlim;
-      const int64_t rr = ok ? kr : 0;
-      stk[i] = ld16(K + rr * p.k_row + d0, ok);
-      stv[i] = ld16(V + rr * p.v_row + d0, ok);
-    }
-  };
-  auto commit = [&](int buf) {
-    char* kt = smem + buf * 2 * TILE;
-    char* vt = kt + TILE;
+  for (int j = 0; j < PPW; ++j) {
+    voff_k[j] = dma_voff<BN>(wave + j * NW, lane, p.k_row, dlim);
+    voff_v[j] = dma_voff<BN>(wave + j * NW, lane, p.v_row, dlim);
+  }
+  auto issue = [&](int nb) {
+    const int n0 = nb * BN;
+    char* dst = smem + (nb % kBwdBufs) * 2 * TILE;
+    const buf_rsrc_t rk = make_rsrc(K + (int64_t)n0 * p.k_row, rec_bytes(sk - n0, p.k_row, 2));
+    const buf_rsrc_t rv = make_rsrc(V + (int64_t)n0 * p.v_row, rec_bytes(sk - n0, p.v_row, 2));
 #pragma unroll
-    for (int i = 0; i < LOADS; ++i) {
-      const int pid = i * 32 + (tid >> 3);
-      if (NPAIR % 32 == 0 || pid < NPAIR) {
-        const int panel = pid % NP;
-        const int row = 2 * (pid / NP) + ((tid >> 2) & 1);
-        const int off = panel_off(row, panel * 4 + (tid & 3), BN);
-        *(u32x4_t*)(kt + off) = stk[i];
-        *(u32x4_t*)(vt + off) = stv[i];
+    for (int j = 0; j < PPW; ++j) {
+      const int pc = wave + j * NW;
+      if (PIECES % NW == 0 || pc < PIECES) {
+        dma16(rk, dst + pc * 1024, voff_k[j]);
+        dma16(rv, dst + TILE + pc * 1024, voff_v[j]);
       }
     }
   };
@@ -396,57 +413,73 @@ __global__ void __launch_bounds__(256, 1) bwd_dq_kernel(const BwdParams p) {
 #pragma unroll
     for (int g = 0; g < 16; ++g) dq[t][g] = 0.f;
 
-  if (nblk > 0) {
-    issue(0);
-    commit(0);
-    __syncthreads();
-  }
-  for (int nb = 0; nb < nblk; ++nb) {
+  auto tile = [&](auto MASKC, int nb) {
+    constexpr bool MASK = decltype(MASKC)::value;
     const int n0 = nb * BN;
-    const int cur = nb & 1;
-    const bool has_next = nb + 1 < nblk;
-    if (has_next) issue(n0 + BN);
-    const char* kt = smem + cur * 2 * TILE;
-    const char* vt = kt + TILE;
-    const bool active = (wq0 < sq) && (!CAUSAL || n0 <= wq0 + 31);
-    if (active) {
-      f32x16_t st[NT], pt[NT];
+    const int kt = (nb % kBwdBufs) * 2 * TILE;
+    const TileAddr tk(lb, kt), tv(lb, kt + TILE);
+    f32x16_t st[NT], pt[NT];
+    static_for<0, NT>([&](auto T) {
+      constexpr int t = decltype(T)::value;
 #pragma unroll
-      for (int t = 0; t < NT; ++t) {
+      for (int g = 0; g < 16; ++g) { st[t][g] = 0.f; pt[t][g] = -dsum_q; }
+      static_for<0, KS / KG>([&](auto GG) {
+        constexpr int g0 = decltype(GG)::value * KG;
+        i16x8_t ka[KG], va[KG];
+        static_for<0, KG>([&](auto KK) {
+          constexpr int ks = g0 + decltype(KK)::value;
+          ka[ks - g0] = row_read_c<BN, t * 32, 2 * ks>(smem, tk);
+          va[ks - g0] = row_read_c<BN, t * 32, 2 * ks>(smem, tv);
+        });
 #pragma unroll
-        for (int g = 0; g < 16; ++g) { st[t][g] = 0.f; pt[t][g] = -dsum_q; }
-#pragma unroll
-        for (int ks = 0; ks < KS; ++ks) {
-          st[t] = E::mfma(row_read(kt, t * 32 + r, 2 * ks + hh, BN), qf[ks], st[t]);
-          pt[t] = E::mfma(row_read(vt, t * 32 + r, 2 * ks + hh, BN), of[ks], pt[t]);
+        for (int k = 0; k < KG; ++k) {
+          st[t] = E::mfma(ka[k], qf[g0 + k], st[t]);
+          pt[t] = E::mfma(va[k], of[g0 + k], pt[t]);
         }
+      });
+    });
+#pragma unroll
+    for (int t = 0; t < NT; ++t)
+#pragma unroll
+      for (int g = 0; g < 16; ++g) {
+        float pv = fast_exp2(fmaf(st[t][g], c, -lse_l2));
+        if constexpr (MASK) {
+          const int kk = n0 + t * 32 + acc_row(g, hh);
+          if (kk >= sk || (CAUSAL && kk > qi)) pv = 0.f;
+        }
+        pt[t][g] = pv * pt[t][g];     // dS^T = P^T o (dP^T - D)
       }
-      const bool need_mask = (n0 + BN > sk) || (CAUSAL && n0 + BN - 1 > wq0);
+    // dQ^T[d][q] += K^T[d][key] dS^T[key][q]
+    i16x8_t df[2 * NT];
 #pragma unroll
-      for (int t = 0; t < NT; ++t)
-#pragma unroll
-        for (int g = 0; g < 16; ++g) {
-          float pv = fast_exp2(fmaf(st[t][g], c, -lse_l2));
-          if (need_mask) {
-            const int kk = n0 + t * 32 + acc_row(g, hh);
-            if (kk >= sk || (CAUSAL && kk > qi)) pv = 0.f;
-          }
-          pt[t][g] = pv * pt[t][g];     // dS^T = P^T o (dP^T - D)
-        }
-      // dQ^T[d][q] += K^T[d][key] dS^T[key][q]
-#pragma unroll
-      for (int t = 0; t < NT; ++t) {
-        const i16x8_t d0f = pack_frag<BF16>(pt[t], 0), d1f = pack_frag<BF16>(pt[t], 1);
-#pragma unroll
-        for (int dt = 0; dt < NP; ++dt) {
-          const int col0 = dt * 32 + 16 * (r >> 4);
-          dq[dt] = E::mfma(tr_frag(kt, t * 32 + 4 * hh, col0, BN, i16), d0f, dq[dt]);
-          dq[dt] = E::mfma(tr_frag(kt, t * 32 + 16 + 4 * hh, col0, BN, i16), d1f, dq[dt]);
-        }
-      }
+    for (int t = 0; t < NT; ++t) {
+      df[2 * t] = pack_frag<BF16>(pt[t], 0);
+      df[2 * t + 1] = pack_frag<BF16>(pt[t], 1);
     }
-    if (has_next) commit(cur ^ 1);
-    __syncthreads();
+    static_for<0, NP>([&](auto DTC) {
+      constexpr int dt = decltype(DTC)::value;
+      i16x8_t a[2 * NT];
+      static_for<0, 2 * NT>([&](auto KC) {
+        constexpr int kk = decltype(KC)::value;
+        a[kk] = tr_frag_c<BN, kk * 16, dt>(smem, tk);
+      });
+#pragma unroll
+      for (int kk = 0; kk < 2 * NT; ++kk) dq[dt] = E::mfma(a[kk], df[kk], dq[dt]);
+    });
+  };
+
+  if (nblk > 0) issue(0);
+  if (nblk > 1) issue(1);
+  wait_dma_and_barrier();
+  for (int nb = 0; nb < nfast; ++nb) {
+    if (nb + 2 < nblk) issue(nb + 2);
+    tile(std::false_type{}, nb);
+    wait_dma_and_barrier();
+  }
+  for (int nb = nfast; nb < nblk; ++nb) {
+    if (nb + 2 < nblk) issue(nb + 2);
+    if ((wq0 < sq) && (!CAUSAL || nb * BN <= wq0 + 31)) tile(std::true_type{}, nb);
+    wait_dma_and_barrier();
   }
 
   if (q_ok) {
@@ -474,13 +507,13 @@ static void run_bwd(const BwdParams& p, hipStream_t stream) {
   {
     dim3 grid(p.s.b * nheads_grid, p.num_n_blocks);
     prof_begin(kTimeBwdMain, stream);
-    hipLaunchKernelGGL((bwd_dkdv_kernel<BF16, D, CAUSAL>), grid, dim3(256), 0, stream, p);
+    hipLaunchKernelGGL((bwd_dkdv_kernel<BF16, D, CAUSAL>), grid, dim3(kDkdvWaves * 64), 0, stream, p);
     prof_end(kTimeBwdMain, stream);
   }
   {
     dim3 grid(p.s.b * p.s.h, (p.s.seqlen_q + kDqBM - 1) / kDqBM);
     prof_begin(kTimeBwdDq, stream);
-    hipLaunchKernelGGL((bwd_dq_kernel<BF16, D, CAUSAL>), grid, dim3(256), 0, stream, p);
+    hipLaunchKernelGGL((bwd_dq_kernel<BF16, D, CAUSAL>), grid, dim3(kDqWaves * 64), 0, stream, p);
     prof_end(kTimeBwdDq, stream);
   }
 }

@@ -216,6 +216,10 @@ __device__ inline void dma16(buf_rsrc_t rsrc, char* lds_dst, int voffset) {
   __builtin_amdgcn_raw_ptr_buffer_load_lds(rsrc, (__attribute__((address_space(3))) void*)lds_dst, 16,
                                            voffset, 0, 0, 0);
 }
+__device__ inline void dma4(buf_rsrc_t rsrc, char* lds_dst, int voffset) {
+  __builtin_amdgcn_raw_ptr_buffer_load_lds(rsrc, (__attribute__((address_space(3))) void*)lds_dst, 4,
+                                           voffset, 0, 0, 0);
+}
 __device__ inline void wait_dma_and_barrier() {
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
