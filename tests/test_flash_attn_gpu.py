@@ -416,9 +416,9 @@ def test_headline_sizes_sampled(cfg):
         rows = np.sort(rng.choice(s, 24, replace=False))
         keys = np.sort(rng.choice(s, 24, replace=False))
         ref = _rows_fp64(q.detach(), k.detach(), v.detach(), g, bi, hi, rows, keys, causal, scale)
-        o = out[bi, rows, hi].double().cpu().numpy()
+        o = out.detach()[bi, rows, hi].double().cpu().numpy()
         np.testing.assert_allclose(o, ref["O"], atol=tol * max(1.0, np.abs(ref["O"]).max()), rtol=0)
-        np.testing.assert_allclose(lse[bi, hi, rows].double().cpu().numpy(), ref["lse"], atol=2e-3, rtol=1e-4)
+        np.testing.assert_allclose(lse.detach()[bi, hi, rows].double().cpu().numpy(), ref["lse"], atol=2e-3, rtol=1e-4)
         gq = dq[bi, rows, hi].double().cpu().numpy()
         np.testing.assert_allclose(gq, ref["dQ"], atol=tol * max(1.0, np.abs(ref["dQ"]).max()), rtol=0)
         if hk == h:

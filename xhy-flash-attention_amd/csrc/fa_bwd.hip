@@ -275,25 +275,107 @@ __global__ void __launch_bounds__(kDkdvWaves * 64, 1) bwd_dkdv_kernel(const BwdP
     });
   };
 
+  // ---- pipelined pieces of the mask-free path ----
+  // S' / dP' accumulators of 32-row q-tile QI of the slice at byte offset so
+  // raw S = Q K^T and dP = dO V^T (chains start from a zero accumulator: no VALU init)
+  auto sdp = [&](auto QIC, int so, f32x16_t& sacc, f32x16_t& pacc) {
+    constexpr int QI = decltype(QIC)::value;
+    const TileAddr tq(lb, so), to(lb, so + QTILE);
+    i16x8_t qa_f[KS], oa_f[KS];
+    static_for<0, KS>([&](auto KK) {
+      constexpr int ks = decltype(KK)::value;
+      qa_f[ks] = row_read_c<BQ, 32 * QI, 2 * ks>(smem, tq);
+      oa_f[ks] = row_read_c<BQ, 32 * QI, 2 * ks>(smem, to);
+    });
+    const f32x16_t zero = {};
+    sacc = E::mfma(qa_f[0], kf[0], zero);
+    pacc = E::mfma(oa_f[0], vf[0], zero);
+#pragma unroll
+    for (int ks = 1; ks < KS; ++ks) {
+      sacc = E::mfma(qa_f[ks], kf[ks], sacc);
+      pacc = E::mfma(oa_f[ks], vf[ks], pacc);
+    }
+  };
+  // P = exp2(c S - LSE log2e), dS = P o (dP - D) -> packed B operands (no masks); the per-row
+  // LSE / D of the accumulator rows come from the slice's LDS copy (4 x 16-byte broadcast reads)
+  auto finish = [&](auto QIC, int so, f32x16_t& sacc, f32x16_t& pacc, i16x8_t (&fr)[4]) {
+    constexpr int QI = decltype(QIC)::value;
+    const float* lt = (const float*)(smem + so + 2 * QTILE);
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const f32x4_t lv = *(const f32x4_t*)(lt + 32 * QI + 8 * u + 4 * hh);
+      const f32x4_t dv = *(const f32x4_t*)(lt + BQ + 32 * QI + 8 * u + 4 * hh);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int g = 4 * u + j;
+        const float pv = fast_exp2(fmaf(sacc[g], c, -lv[j] * kLog2e));
+        sacc[g] = pv;
+        pacc[g] = pv * (pacc[g] - dv[j]);
+      }
+    }
+    fr[0] = pack_frag<BF16>(sacc, 0); fr[1] = pack_frag<BF16>(sacc, 1);
+    fr[2] = pack_frag<BF16>(pacc, 0); fr[3] = pack_frag<BF16>(pacc, 1);
+  };
+  // dV^T += dO^T P ; dK^T += Q^T dS for q-tile QI of the slice at so
+  auto update = [&](auto QIC, int so, const i16x8_t (&fr)[4]) {
+    constexpr int QI = decltype(QIC)::value;
+    const TileAddr tq(lb, so), to(lb, so + QTILE);
+    static_for<0, NP>([&](auto DTC) {
+      constexpr int dt = decltype(DTC)::value;
+      const i16x8_t o0 = tr_frag_c<BQ, 32 * QI, dt>(smem, to);
+      const i16x8_t o1 = tr_frag_c<BQ, 32 * QI + 16, dt>(smem, to);
+      const i16x8_t q0f = tr_frag_c<BQ, 32 * QI, dt>(smem, tq);
+      const i16x8_t q1f = tr_frag_c<BQ, 32 * QI + 16, dt>(smem, tq);
+      dvt[dt] = E::mfma(o0, fr[0], dvt[dt]);
+      dvt[dt] = E::mfma(o1, fr[1], dvt[dt]);
+      dkt[dt] = E::mfma(q0f, fr[2], dkt[dt]);
+      dkt[dt] = E::mfma(q1f, fr[3], dkt[dt]);
+    });
+  };
+  const std::integral_constant<int, 0> QT0{};
+  const std::integral_constant<int, 1> QT1{};
+  static_assert(BQ == 64, "the pipelined path assumes two 32-row q-tiles per slice");
+  auto is_fast = [&](int it) {
+    const int q0 = (m_first + it % ns) * BQ;
+    return (q0 + BQ <= sq) && (n0 + kDkdvBN <= sk) && (!CAUSAL || q0 >= n0 + kDkdvBN - 1);
+  };
+
   if (total > 0) issue(0);
   if (total > 1) issue(1);
   wait_dma_and_barrier();
 
-  for (int it = 0; it < total; ++it) {
-    const int q0 = (m_first + it % ns) * BQ;
-    if (it + 2 < total) issue(it + 2);
-    const int so = (it % kBwdBufs) * SLICE;
-    const bool fast = (q0 + BQ <= sq) && (n0 + kDkdvBN <= sk) && (!CAUSAL || q0 >= n0 + kDkdvBN - 1);
-    if (fast) {
-      qtile(std::integral_constant<int, 0>{}, std::false_type{}, so, q0);
-      qtile(std::integral_constant<int, 1>{}, std::false_type{}, so, q0);
+  int it = 0;
+  while (it < total) {
+    if (is_fast(it)) {
+      // run of mask-free slices: S/dP of the next q-tile (MFMA) overlaps this q-tile's exp/pack (VALU)
+      int it_end = it + 1;
+      while (it_end < total && is_fast(it_end)) ++it_end;
+      f32x16_t sa, pa, sb, pb;
+      sdp(QT0, (it % kBwdBufs) * SLICE, sa, pa);
+      for (; it < it_end; ++it) {
+        if (it + 2 < total) issue(it + 2);
+        const int so = (it % kBwdBufs) * SLICE;
+        const int so_next = ((it + 1) % kBwdBufs) * SLICE;   // resident (or unused garbage at the end)
+        i16x8_t fr[4];
+        sdp(QT1, so, sb, pb);
+        finish(QT0, so, sa, pa, fr);
+        update(QT0, so, fr);
+        sdp(QT0, so_next, sa, pa);
+        finish(QT1, so, sb, pb, fr);
+        update(QT1, so, fr);
+        wait_dma_and_barrier();
+      }
     } else {
+      const int q0 = (m_first + it % ns) * BQ;
+      if (it + 2 < total) issue(it + 2);
+      const int so = (it % kBwdBufs) * SLICE;
       static_for<0, BQ / 32>([&](auto QIC) {
         const int qa = q0 + 32 * decltype(QIC)::value;
         if (qa < sq && !(CAUSAL && kw0 > qa + 31)) qtile(QIC, std::true_type{}, so, q0);
       });
+      wait_dma_and_barrier();
+      ++it;
     }
-    wait_dma_and_barrier();
   }
 
   // ---- epilogue: dK = scale * (dK^T)^T, dV = (dV^T)^T ----
