@@ -9,12 +9,12 @@
 // MI355X design (not the reference's seqk-parallel kernel with fp32 dQ atomics, which on this chip
 // is bound by the ~1.3 TB/s global-atomic rate: 8.7 GB of dQ adds at the C3 headline shape):
 //   1. bwd_pre_kernel   D = rowsum(dO o O)  (one 16-lane group per query row)
-//   2. bwd_dkdv_kernel  one workgroup (4 waves, one per SIMD, full 512-entry register file) per
-//                       128-key block of a (batch, kv-head); each wave's 32 keys of K and V stay in
-//                       registers, (Q, dO, LSE, D) slices of 64 query rows arrive by LDS-DMA two
-//                       slices ahead into a 3-deep ring; dK^T / dV^T accumulate in registers over
-//                       every slice (and, for GQA, every query head of the group) and are written
-//                       once: 4 MFMA GEMMs per tile, no atomics.
+//   2. bwd_dkdv_kernel  one workgroup (8 waves) per 128-key block of a (batch, kv-head), the waves
+//                       specialised by role: 4 "P" waves hold K and accumulate dV^T, 4 "dS" waves
+//                       hold V and accumulate dK^T, P passing between them through LDS; (Q, dO,
+//                       LSE, D) slices of 64 query rows arrive by LDS-DMA two slices ahead into a
+//                       3-deep ring; dK^T / dV^T accumulate in registers over every slice (and, for
+//                       GQA, every query head of the group) and are written once: no atomics.
 //   3. bwd_dq_kernel    one workgroup (8 waves) per 256-row query block, structured like the
 //                       forward: Q and dO fragments in registers, K/V tiles by LDS-DMA ring,
 //                       S^T and dP^T with the query on the MFMA lane (LSE and D are per-lane
@@ -25,9 +25,7 @@
 //   * "Key on the lane" in dkdv: S = Q K^T and dP = dO V^T have the key on the MFMA column, so
 //     their accumulators are directly the B operands of dV^T = dO^T P and dK^T = Q^T dS; dO^T and
 //     Q^T come from the row-major LDS slice through ds_read_b64_tr_b16.
-//   * Row constants as the initial accumulator in dkdv: S starts at -LSE/scale and dP at -D.
-//   * Slices / tiles that need no mask run a branch-free body (the two 32-row q-tiles of a slice,
-//     resp. the S / dP chains of a tile, interleave in one basic block).
+//   * Slices that need no mask skip the mask arithmetic (one wave-uniform test per slice).
 #include <stdexcept>
 #include <string>
 
@@ -38,8 +36,8 @@ namespace fa {
 
 typedef unsigned short u16;
 
-constexpr int kDkdvWaves = 4;
-constexpr int kDkdvBN = 32 * kDkdvWaves;  // keys per dK/dV workgroup
+constexpr int kDkdvWaves = 8;             // 4 P waves + 4 dS waves
+constexpr int kDkdvBN = 128;              // keys per dK/dV workgroup (32 per key group)
 constexpr int kDkdvBQ = 64;               // query rows per sweep step
 constexpr int kDqWaves = 8;
 constexpr int kDqBM = 32 * kDqWaves;      // query rows per dQ workgroup
@@ -127,8 +125,18 @@ __global__ void __launch_bounds__(256) bwd_pre_kernel(const BwdParams p) {
 }
 
 // ------------------------------------------------------------------------------------------------
-// 2. dK / dV
+// 2. dK / dV  (wave-specialised: 4 "P" waves + 4 "dS" waves per 128-key block)
 // ------------------------------------------------------------------------------------------------
+// Waves 0-3 ("P" waves) hold K of their 32 keys and accumulate dV^T:
+//     S = Q K^T  ->  P = exp2(c S - LSE log2e) (masked)  ->  P to LDS  ->  dV^T += dO^T P
+// Waves 4-7 ("dS" waves) hold V of the same 32 keys and accumulate dK^T:
+//     dP = dO V^T  ->  (barrier, P from LDS)  dS = P o (dP - D)  ->  dK^T += Q^T dS
+// Both roles run the same instruction skeleton (row-read A operand x register B operand, then
+// transpose-read A operand x packed B operand); only the operand offsets and the elementwise step
+// differ.  Each wave needs one 32-key operand set and one D x 32 accumulator set (<= 256 registers),
+// so two waves share every SIMD and the hardware interleaves one wave's VALU / LDS work with the
+// other's MFMAs -- the single-wave-per-SIMD design that kept K, V, dK^T and dV^T in one wave could
+// not overlap them.  P crosses between the roles as an fp32 32x32 tile per (key group, q-tile).
 template <bool BF16, int D, bool CAUSAL>
 __global__ void __launch_bounds__(kDkdvWaves * 64, 1) bwd_dkdv_kernel(const BwdParams p) {
   using E = Elt<BF16>;
@@ -138,14 +146,19 @@ __global__ void __launch_bounds__(kDkdvWaves * 64, 1) bwd_dkdv_kernel(const BwdP
   constexpr int NP = D / 32;
   constexpr int QTILE = BQ * D * 2;                 // bytes of a Q or dO slice
   constexpr int SLICE = 2 * QTILE + 2 * BQ * 4;     // Q | dO | lse[BQ] | D[BQ]
+  constexpr int XTILE = 32 * 32 * 4;                // one fp32 32x32 P tile
+  constexpr int XBASE = kBwdBufs * SLICE;
   constexpr int PIECES = QTILE / 1024;
   constexpr int PPW = (PIECES + NW - 1) / NW;
   static_assert(QTILE % 1024 == 0, "slice must be whole DMA pieces");
-  __shared__ __attribute__((aligned(16))) char smem[kBwdBufs * SLICE];
+  static_assert(BQ == 64 && NW == 8, "two 32-row q-tiles per slice, 4 key groups x 2 roles");
+  __shared__ __attribute__((aligned(16))) char smem[XBASE + 4 * 2 * XTILE];
 
   const AttnShape s = p.s;
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = wave_uniform(tid >> 6);
+  const bool pwave = wave < 4;
+  const int kg = wave & 3;
   const int r = lane & 31, hh = lane >> 5;
   const LdsBases lb(lane);
   const int group = s.h / s.hk;
@@ -162,19 +175,18 @@ __global__ void __launch_bounds__(kDkdvWaves * 64, 1) bwd_dkdv_kernel(const BwdP
   if (n0 >= sk) return;
   const int dlim = s.d;
 
-  // ---- this wave's 32 keys: K / V fragments (B operands of S = Q K^T and dP = dO V^T) ----
-  const int kw0 = n0 + 32 * wave;
+  // ---- this wave's 32 keys: K (P waves) or V (dS waves) fragments, the B operand of phase 1 ----
+  const int kw0 = n0 + 32 * kg;
   const int key = kw0 + r;
-  i16x8_t kf[KS], vf[KS];
+  i16x8_t kv[KS];
   {
     const bool ok = key < sk;
-    const u16* krow = (const u16*)p.k + geo.k_off + (int64_t)kvh * p.k_head + (int64_t)(ok ? key : 0) * p.k_row;
-    const u16* vrow = (const u16*)p.v + geo.v_off + (int64_t)kvh * p.v_head + (int64_t)(ok ? key : 0) * p.v_row;
+    const u16* src = pwave ? (const u16*)p.k + geo.k_off + (int64_t)kvh * p.k_head + (int64_t)(ok ? key : 0) * p.k_row
+                           : (const u16*)p.v + geo.v_off + (int64_t)kvh * p.v_head + (int64_t)(ok ? key : 0) * p.v_row;
 #pragma unroll
     for (int ks = 0; ks < KS; ++ks) {
       const int d0 = 16 * ks + 8 * hh;
-      kf[ks] = __builtin_bit_cast(i16x8_t, ld16(krow + d0, ok && d0 < dlim));
-      vf[ks] = __builtin_bit_cast(i16x8_t, ld16(vrow + d0, ok && d0 < dlim));
+      kv[ks] = __builtin_bit_cast(i16x8_t, ld16(src + d0, ok && d0 < dlim));
     }
   }
 
@@ -213,190 +225,149 @@ __global__ void __launch_bounds__(kDkdvWaves * 64, 1) bwd_dkdv_kernel(const BwdP
     }
   };
 
-  f32x16_t dvt[NP], dkt[NP];
+  // dV^T (P waves) or dK^T (dS waves): D x 32 keys
+  f32x16_t acc[NP];
 #pragma unroll
   for (int t = 0; t < NP; ++t)
 #pragma unroll
-    for (int g = 0; g < 16; ++g) { dvt[t][g] = 0.f; dkt[t][g] = 0.f; }
+    for (int g = 0; g < 16; ++g) acc[t][g] = 0.f;
 
-  const float inv_scale = 1.f / s.scale;
   const float c = s.scale_log2;
+  // phase-1 A operand rows: Q (P waves) / dO (dS waves); phase-2 transposed A operand: the other
+  const int a1_off = pwave ? 0 : QTILE;
+  const int a2_off = pwave ? QTILE : 0;
+  char* const xw = smem + XBASE + kg * 2 * XTILE + lane * 16;   // this key group's P tiles
 
-  // one 32-row q-tile QI of the slice at byte offset `so`; MASK adds the causal / bound masks
-  auto qtile = [&](auto QIC, auto MASKC, int so, int q0) {
-    constexpr int QI = decltype(QIC)::value;
+  // DMA operations one issue() leaves outstanding in this wave (for the counted vmcnt wait)
+  int ndma = wave < 2 ? 1 : 0;
+#pragma unroll
+  for (int j = 0; j < PPW; ++j)
+    if (PIECES % NW == 0 || wave + j * NW < PIECES) ndma += 2;
+
+  // P = exp2(c S - LSE log2e) for both q-tiles, published for the dS waves of this key group
+  auto p_step = [&](auto MASKC, f32x16_t (&sp)[2], const float* lt, int q0, i16x8_t (&fr)[4]) {
     constexpr bool MASK = decltype(MASKC)::value;
-    const int qa = q0 + 32 * QI;
-    const TileAddr tq(lb, so), to(lb, so + QTILE);
-    const float* lt = (const float*)(smem + so + 2 * QTILE);
-    // S' = Q K^T - LSE/scale ; dP' = dO V^T - D      (query on registers, key on lane)
-    f32x16_t sacc, pacc;
 #pragma unroll
-    for (int u = 0; u < 4; ++u) {
-      const f32x4_t lv = *(const f32x4_t*)(lt + 32 * QI + 8 * u + 4 * hh);
-      const f32x4_t dv = *(const f32x4_t*)(lt + BQ + 32 * QI + 8 * u + 4 * hh);
+    for (int qi = 0; qi < 2; ++qi) {
 #pragma unroll
-      for (int j = 0; j < 4; ++j) { sacc[4 * u + j] = -lv[j] * inv_scale; pacc[4 * u + j] = -dv[j]; }
-    }
-    i16x8_t qa_f[KS], oa_f[KS];
-    static_for<0, KS>([&](auto KK) {
-      constexpr int ks = decltype(KK)::value;
-      qa_f[ks] = row_read_c<BQ, 32 * QI, 2 * ks>(smem, tq);
-      oa_f[ks] = row_read_c<BQ, 32 * QI, 2 * ks>(smem, to);
-    });
+      for (int u = 0; u < 4; ++u) {
+        const f32x4_t lv = *(const f32x4_t*)(lt + 32 * qi + 8 * u + 4 * hh);
+        f32x4_t pv;
 #pragma unroll
-    for (int ks = 0; ks < KS; ++ks) {
-      sacc = E::mfma(qa_f[ks], kf[ks], sacc);
-      pacc = E::mfma(oa_f[ks], vf[ks], pacc);
-    }
-#pragma unroll
-    for (int g = 0; g < 16; ++g) {
-      float pv = fast_exp2(sacc[g] * c);
-      if constexpr (MASK) {
-        const int q = qa + acc_row(g, hh);
-        if (key >= sk || q >= sq || (CAUSAL && key > q)) pv = 0.f;
+        for (int j = 0; j < 4; ++j) {
+          float x = fast_exp2(fmaf(sp[qi][4 * u + j], c, -lv[j] * kLog2e));
+          if constexpr (MASK) {
+            const int q = q0 + 32 * qi + 8 * u + 4 * hh + j;
+            x = (key >= sk || q >= sq || (CAUSAL && key > q)) ? 0.f : x;
+          }
+          pv[j] = x;
+          sp[qi][4 * u + j] = x;
+        }
+        *(f32x4_t*)(xw + qi * XTILE + u * 1024) = pv;
       }
-      sacc[g] = pv;
-      pacc[g] = pv * pacc[g];
+      fr[2 * qi] = pack_frag<BF16>(sp[qi], 0);
+      fr[2 * qi + 1] = pack_frag<BF16>(sp[qi], 1);
     }
-    const i16x8_t pf0 = pack_frag<BF16>(sacc, 0), pf1 = pack_frag<BF16>(sacc, 1);
-    const i16x8_t df0 = pack_frag<BF16>(pacc, 0), df1 = pack_frag<BF16>(pacc, 1);
-    // dV^T += dO^T P ; dK^T += Q^T dS
-    static_for<0, NP>([&](auto DTC) {
-      constexpr int dt = decltype(DTC)::value;
-      const i16x8_t o0 = tr_frag_c<BQ, 32 * QI, dt>(smem, to);
-      const i16x8_t o1 = tr_frag_c<BQ, 32 * QI + 16, dt>(smem, to);
-      const i16x8_t q0f = tr_frag_c<BQ, 32 * QI, dt>(smem, tq);
-      const i16x8_t q1f = tr_frag_c<BQ, 32 * QI + 16, dt>(smem, tq);
-      dvt[dt] = E::mfma(o0, pf0, dvt[dt]);
-      dvt[dt] = E::mfma(o1, pf1, dvt[dt]);
-      dkt[dt] = E::mfma(q0f, df0, dkt[dt]);
-      dkt[dt] = E::mfma(q1f, df1, dkt[dt]);
-    });
-  };
-
-  // ---- pipelined pieces of the mask-free path ----
-  // S' / dP' accumulators of 32-row q-tile QI of the slice at byte offset so
-  // raw S = Q K^T and dP = dO V^T (chains start from a zero accumulator: no VALU init)
-  auto sdp = [&](auto QIC, int so, f32x16_t& sacc, f32x16_t& pacc) {
-    constexpr int QI = decltype(QIC)::value;
-    const TileAddr tq(lb, so), to(lb, so + QTILE);
-    i16x8_t qa_f[KS], oa_f[KS];
-    static_for<0, KS>([&](auto KK) {
-      constexpr int ks = decltype(KK)::value;
-      qa_f[ks] = row_read_c<BQ, 32 * QI, 2 * ks>(smem, tq);
-      oa_f[ks] = row_read_c<BQ, 32 * QI, 2 * ks>(smem, to);
-    });
-    const f32x16_t zero = {};
-    sacc = E::mfma(qa_f[0], kf[0], zero);
-    pacc = E::mfma(oa_f[0], vf[0], zero);
-#pragma unroll
-    for (int ks = 1; ks < KS; ++ks) {
-      sacc = E::mfma(qa_f[ks], kf[ks], sacc);
-      pacc = E::mfma(oa_f[ks], vf[ks], pacc);
-    }
-  };
-  // P = exp2(c S - LSE log2e), dS = P o (dP - D) -> packed B operands (no masks); the per-row
-  // LSE / D of the accumulator rows come from the slice's LDS copy (4 x 16-byte broadcast reads)
-  auto finish = [&](auto QIC, int so, f32x16_t& sacc, f32x16_t& pacc, i16x8_t (&fr)[4]) {
-    constexpr int QI = decltype(QIC)::value;
-    const float* lt = (const float*)(smem + so + 2 * QTILE);
-#pragma unroll
-    for (int u = 0; u < 4; ++u) {
-      const f32x4_t lv = *(const f32x4_t*)(lt + 32 * QI + 8 * u + 4 * hh);
-      const f32x4_t dv = *(const f32x4_t*)(lt + BQ + 32 * QI + 8 * u + 4 * hh);
-#pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        const int g = 4 * u + j;
-        const float pv = fast_exp2(fmaf(sacc[g], c, -lv[j] * kLog2e));
-        sacc[g] = pv;
-        pacc[g] = pv * (pacc[g] - dv[j]);
-      }
-    }
-    fr[0] = pack_frag<BF16>(sacc, 0); fr[1] = pack_frag<BF16>(sacc, 1);
-    fr[2] = pack_frag<BF16>(pacc, 0); fr[3] = pack_frag<BF16>(pacc, 1);
-  };
-  // dV^T += dO^T P ; dK^T += Q^T dS for q-tile QI of the slice at so
-  auto update = [&](auto QIC, int so, const i16x8_t (&fr)[4]) {
-    constexpr int QI = decltype(QIC)::value;
-    const TileAddr tq(lb, so), to(lb, so + QTILE);
-    static_for<0, NP>([&](auto DTC) {
-      constexpr int dt = decltype(DTC)::value;
-      const i16x8_t o0 = tr_frag_c<BQ, 32 * QI, dt>(smem, to);
-      const i16x8_t o1 = tr_frag_c<BQ, 32 * QI + 16, dt>(smem, to);
-      const i16x8_t q0f = tr_frag_c<BQ, 32 * QI, dt>(smem, tq);
-      const i16x8_t q1f = tr_frag_c<BQ, 32 * QI + 16, dt>(smem, tq);
-      dvt[dt] = E::mfma(o0, fr[0], dvt[dt]);
-      dvt[dt] = E::mfma(o1, fr[1], dvt[dt]);
-      dkt[dt] = E::mfma(q0f, fr[2], dkt[dt]);
-      dkt[dt] = E::mfma(q1f, fr[3], dkt[dt]);
-    });
-  };
-  const std::integral_constant<int, 0> QT0{};
-  const std::integral_constant<int, 1> QT1{};
-  static_assert(BQ == 64, "the pipelined path assumes two 32-row q-tiles per slice");
-  auto is_fast = [&](int it) {
-    const int q0 = (m_first + it % ns) * BQ;
-    return (q0 + BQ <= sq) && (n0 + kDkdvBN <= sk) && (!CAUSAL || q0 >= n0 + kDkdvBN - 1);
   };
 
   if (total > 0) issue(0);
+  wait_vmem_all();   // K/V fragments and slice 0 (compiler-visible: no vmcnt waits inside the loop)
   if (total > 1) issue(1);
-  wait_dma_and_barrier();
+  lds_barrier();
 
-  int it = 0;
-  while (it < total) {
-    if (is_fast(it)) {
-      // run of mask-free slices: S/dP of the next q-tile (MFMA) overlaps this q-tile's exp/pack (VALU)
-      int it_end = it + 1;
-      while (it_end < total && is_fast(it_end)) ++it_end;
-      f32x16_t sa, pa, sb, pb;
-      sdp(QT0, (it % kBwdBufs) * SLICE, sa, pa);
-      for (; it < it_end; ++it) {
-        if (it + 2 < total) issue(it + 2);
-        const int so = (it % kBwdBufs) * SLICE;
-        const int so_next = ((it + 1) % kBwdBufs) * SLICE;   // resident (or unused garbage at the end)
-        i16x8_t fr[4];
-        sdp(QT1, so, sb, pb);
-        finish(QT0, so, sa, pa, fr);
-        update(QT0, so, fr);
-        sdp(QT0, so_next, sa, pa);
-        finish(QT1, so, sb, pb, fr);
-        update(QT1, so, fr);
-        wait_dma_and_barrier();
-      }
-    } else {
-      const int q0 = (m_first + it % ns) * BQ;
-      if (it + 2 < total) issue(it + 2);
-      const int so = (it % kBwdBufs) * SLICE;
-      static_for<0, BQ / 32>([&](auto QIC) {
-        const int qa = q0 + 32 * decltype(QIC)::value;
-        if (qa < sq && !(CAUSAL && kw0 > qa + 31)) qtile(QIC, std::true_type{}, so, q0);
+  for (int it = 0; it < total; ++it) {
+    const bool ahead = it + 2 < total;
+    if (ahead) issue(it + 2);
+    const int q0 = (m_first + it % ns) * BQ;
+    const int so = (it % kBwdBufs) * SLICE;
+    const float* lt = (const float*)(smem + so + 2 * QTILE);
+
+    // phase 1: S = Q K^T or dP = dO V^T for both 32-row q-tiles (query on registers, key on lane);
+    // every A fragment is requested before the first MFMA so only the first read's latency shows
+    f32x16_t sp[2];
+    {
+      const TileAddr ta(lb, so + a1_off);
+      i16x8_t af0[KS], af1[KS];
+      static_for<0, KS>([&](auto KK) {
+        constexpr int ks = decltype(KK)::value;
+        af0[ks] = row_read_c<BQ, 0, 2 * ks>(smem, ta);
+        af1[ks] = row_read_c<BQ, 32, 2 * ks>(smem, ta);
       });
-      wait_dma_and_barrier();
-      ++it;
+      __builtin_amdgcn_sched_barrier(0);
+      const f32x16_t zero = {};
+      sp[0] = E::mfma(af0[0], kv[0], zero);
+      sp[1] = E::mfma(af1[0], kv[0], zero);
+#pragma unroll
+      for (int ks = 1; ks < KS; ++ks) {
+        sp[0] = E::mfma(af0[ks], kv[ks], sp[0]);
+        sp[1] = E::mfma(af1[ks], kv[ks], sp[1]);
+      }
     }
+
+    i16x8_t fr[4];
+    if (pwave) {
+      const bool fast = (q0 + BQ <= sq) && (n0 + kDkdvBN <= sk) && (!CAUSAL || q0 >= n0 + kDkdvBN - 1);
+      if (fast) p_step(std::false_type{}, sp, lt, q0, fr);
+      else p_step(std::true_type{}, sp, lt, q0, fr);
+    }
+    lds_barrier();
+    const TileAddr ta2(lb, so + a2_off);
+    i16x8_t tf[2][4];
+    auto tr_group = [&](auto DTC, i16x8_t (&t)[4]) {
+      constexpr int dt = decltype(DTC)::value;
+      t[0] = tr_frag_c<BQ, 0, dt>(smem, ta2);
+      t[1] = tr_frag_c<BQ, 16, dt>(smem, ta2);
+      t[2] = tr_frag_c<BQ, 32, dt>(smem, ta2);
+      t[3] = tr_frag_c<BQ, 48, dt>(smem, ta2);
+    };
+    tr_group(std::integral_constant<int, 0>{}, tf[0]);
+    if (!pwave) {
+      // dS = P o (dP - D)
+#pragma unroll
+      for (int qi = 0; qi < 2; ++qi) {
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+          const f32x4_t dv = *(const f32x4_t*)(lt + BQ + 32 * qi + 8 * u + 4 * hh);
+          const f32x4_t pv = *(const f32x4_t*)(xw + qi * XTILE + u * 1024);
+#pragma unroll
+          for (int j = 0; j < 4; ++j) sp[qi][4 * u + j] = pv[j] * (sp[qi][4 * u + j] - dv[j]);
+        }
+        fr[2 * qi] = pack_frag<BF16>(sp[qi], 0);
+        fr[2 * qi + 1] = pack_frag<BF16>(sp[qi], 1);
+      }
+    }
+
+    // phase 2: dV^T += dO^T P  /  dK^T += Q^T dS; the transposed fragments of group dt+1 are
+    // requested before the MFMAs of group dt
+    static_for<0, NP>([&](auto DTC) {
+      constexpr int dt = decltype(DTC)::value;
+      if constexpr (dt + 1 < NP) tr_group(std::integral_constant<int, dt + 1>{}, tf[(dt + 1) & 1]);
+      __builtin_amdgcn_sched_barrier(0);
+      acc[dt] = E::mfma(tf[dt & 1][0], fr[0], acc[dt]);
+      acc[dt] = E::mfma(tf[dt & 1][1], fr[1], acc[dt]);
+      acc[dt] = E::mfma(tf[dt & 1][2], fr[2], acc[dt]);
+      acc[dt] = E::mfma(tf[dt & 1][3], fr[3], acc[dt]);
+      __builtin_amdgcn_sched_barrier(0);
+    });
+    wait_dma_keep_and_barrier(ahead ? ndma : 0);
   }
 
-  // ---- epilogue: dK = scale * (dK^T)^T, dV = (dV^T)^T ----
+  // ---- epilogue: dV = (dV^T)^T from the P waves, dK = scale * (dK^T)^T from the dS waves ----
   if (key < sk) {
     const int hd = p.gqa_reduce ? kvh : hx;
-    u16* dkrow = (u16*)p.dk + geo.dk_off + (int64_t)hd * p.dk_head + (int64_t)key * p.dk_row;
-    u16* dvrow = (u16*)p.dv + geo.dv_off + (int64_t)hd * p.dv_head + (int64_t)key * p.dv_row;
-    const float sc = s.scale;
+    u16* row = pwave ? (u16*)p.dv + geo.dv_off + (int64_t)hd * p.dv_head + (int64_t)key * p.dv_row
+                     : (u16*)p.dk + geo.dk_off + (int64_t)hd * p.dk_head + (int64_t)key * p.dk_row;
+    const float sc = pwave ? 1.f : s.scale;
 #pragma unroll
     for (int dt = 0; dt < NP; ++dt)
 #pragma unroll
       for (int u = 0; u < 4; ++u) {
         const int d0 = dt * 32 + 8 * u + 4 * hh;
         if (d0 < dlim) {
-          u32x2_t wk, wv;
-          wk[0] = E::pack2(dkt[dt][4 * u + 0] * sc, dkt[dt][4 * u + 1] * sc);
-          wk[1] = E::pack2(dkt[dt][4 * u + 2] * sc, dkt[dt][4 * u + 3] * sc);
-          wv[0] = E::pack2(dvt[dt][4 * u + 0], dvt[dt][4 * u + 1]);
-          wv[1] = E::pack2(dvt[dt][4 * u + 2], dvt[dt][4 * u + 3]);
-          *(u32x2_t*)(dkrow + d0) = wk;
-          *(u32x2_t*)(dvrow + d0) = wv;
+          u32x2_t w;
+          w[0] = E::pack2(acc[dt][4 * u + 0] * sc, acc[dt][4 * u + 1] * sc);
+          w[1] = E::pack2(acc[dt][4 * u + 2] * sc, acc[dt][4 * u + 3] * sc);
+          *(u32x2_t*)(row + d0) = w;
         }
       }
   }
@@ -550,18 +521,24 @@ __global__ void __launch_bounds__(kDqWaves * 64, 2) bwd_dq_kernel(const BwdParam
     });
   };
 
+  int ndma = 0;   // DMA operations one issue() leaves outstanding in this wave
+#pragma unroll
+  for (int j = 0; j < PPW; ++j)
+    if (PIECES % NW == 0 || wave + j * NW < PIECES) ndma += 2;
+
   if (nblk > 0) issue(0);
+  wait_vmem_all();   // Q / dO fragments, LSE / D and tile 0 (compiler-visible)
   if (nblk > 1) issue(1);
-  wait_dma_and_barrier();
+  lds_barrier();
   for (int nb = 0; nb < nfast; ++nb) {
     if (nb + 2 < nblk) issue(nb + 2);
     tile(std::false_type{}, nb);
-    wait_dma_and_barrier();
+    wait_dma_keep_and_barrier(nb + 2 < nblk ? ndma : 0);
   }
   for (int nb = nfast; nb < nblk; ++nb) {
     if (nb + 2 < nblk) issue(nb + 2);
     if ((wq0 < sq) && (!CAUSAL || nb * BN <= wq0 + 31)) tile(std::true_type{}, nb);
-    wait_dma_and_barrier();
+    wait_dma_keep_and_barrier(nb + 2 < nblk ? ndma : 0);
   }
 
   if (q_ok) {

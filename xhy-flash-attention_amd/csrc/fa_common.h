@@ -212,17 +212,61 @@ typedef __amdgpu_buffer_rsrc_t buf_rsrc_t;
 __device__ inline buf_rsrc_t make_rsrc(const void* base, int bytes) {
   return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), (short)0, bytes, 0x00020000);
 }
+//
+// Issued as inline asm on purpose: for the buffer_load_lds builtin the compiler cannot prove that
+// later LDS reads (ds_read_b64_tr_b16 in particular) miss the DMA destination, and inserts an
+// `s_waitcnt vmcnt(0)` before them -- which waits for the tile just issued two steps ahead and
+// exposes its whole latency every iteration.  The kernels order DMA and LDS reads themselves
+// (counted vmcnt + barrier per ring step), so the compiler must not see these stores.
+__device__ inline unsigned lds_addr(const char* p) {
+  return wave_uniform((int)(unsigned)(size_t)(__attribute__((address_space(3))) const char*)p);
+}
 __device__ inline void dma16(buf_rsrc_t rsrc, char* lds_dst, int voffset) {
-  __builtin_amdgcn_raw_ptr_buffer_load_lds(rsrc, (__attribute__((address_space(3))) void*)lds_dst, 16,
-                                           voffset, 0, 0, 0);
+  asm volatile("s_nop 0\n\tbuffer_load_dwordx4 %1, %2, 0 offen lds"
+               :: "{m0}"(lds_addr(lds_dst)), "v"(voffset), "s"(rsrc) : "memory");
 }
 __device__ inline void dma4(buf_rsrc_t rsrc, char* lds_dst, int voffset) {
-  __builtin_amdgcn_raw_ptr_buffer_load_lds(rsrc, (__attribute__((address_space(3))) void*)lds_dst, 4,
-                                           voffset, 0, 0, 0);
+  asm volatile("s_nop 0\n\tbuffer_load_dword %1, %2, 0 offen lds"
+               :: "{m0}"(lds_addr(lds_dst)), "v"(voffset), "s"(rsrc) : "memory");
 }
 __device__ inline void wait_dma_and_barrier() {
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
+}
+
+// Workgroup barrier for LDS hand-offs only: drains this wave's LDS operations but leaves its
+// vector-memory operations (LDS-DMA of later tiles) in flight.  __syncthreads() would also wait
+// for vmcnt(0), i.e. for the DMA just issued two tiles ahead.
+__device__ inline void lds_barrier() {
+  asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+}
+
+// s_waitcnt vmcnt(n) for a wave-uniform n in [0, 8]: at most n of this wave's vector-memory
+// operations (in issue order, the youngest) may remain outstanding.
+__device__ inline void wait_vmcnt(int n) {
+  switch (n) {
+    case 8: asm volatile("s_waitcnt vmcnt(8)" ::: "memory"); break;
+    case 7: asm volatile("s_waitcnt vmcnt(7)" ::: "memory"); break;
+    case 6: asm volatile("s_waitcnt vmcnt(6)" ::: "memory"); break;
+    case 5: asm volatile("s_waitcnt vmcnt(5)" ::: "memory"); break;
+    case 4: asm volatile("s_waitcnt vmcnt(4)" ::: "memory"); break;
+    case 3: asm volatile("s_waitcnt vmcnt(3)" ::: "memory"); break;
+    case 2: asm volatile("s_waitcnt vmcnt(2)" ::: "memory"); break;
+    case 1: asm volatile("s_waitcnt vmcnt(1)" ::: "memory"); break;
+    default: asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); break;
+  }
+}
+
+// vmcnt(0) that the compiler's own wait-count tracking sees (the asm waits are opaque to it): after
+// this, register fragments loaded from global memory before a ring loop count as landed, so the
+// compiler inserts no vmcnt wait inside the loop (which would also wait for the in-flight DMA).
+__device__ inline void wait_vmem_all() { __builtin_amdgcn_s_waitcnt(0x0F70); }
+
+// End of a ring step: the tile issued `younger` DMA operations ago may stay in flight, everything
+// older must have landed (in every wave) before any wave passes the barrier.
+__device__ inline void wait_dma_keep_and_barrier(int younger) {
+  wait_vmcnt(younger);
+  lds_barrier();
 }
 
 // 16-byte global load with zero fill when !valid.

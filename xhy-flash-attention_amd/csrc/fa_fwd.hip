@@ -7,10 +7,11 @@
 //
 // MI355X mapping (not a translation of the CUDA tiling):
 //   * 8 waves x 32 query rows = 256-row query block per workgroup; BN = 64 keys per K/V tile.
-//   * K/V tiles arrive by LDS-DMA (buffer_load ... lds, one 1-KiB piece per wave instruction) two
-//     tiles ahead into a 3-deep LDS ring; the buffer descriptor's range check zero-fills rows past
+//   * K/V tiles arrive by LDS-DMA (buffer_load ... lds, one 1-KiB piece per wave instruction) three
+//     tiles ahead into a 4-deep LDS ring; the buffer descriptor's range check zero-fills rows past
 //     seqlen_k and padded head-dim columns, so the kernel never branches on the load side.  One
-//     s_waitcnt vmcnt(0) + barrier per tile (the DMA had a whole tile of compute to land).
+//     counted s_waitcnt vmcnt + barrier per tile: the tile issued in this step stays in flight, so
+//     each DMA has two tiles of compute to land.
 //   * "Swapped" QK^T: each wave computes S^T = K . Q^T with v_mfma_f32_32x32x16, so the query sits on
 //     the MFMA column (= lane) and every lane holds 32 scores of ONE query row: the row max / sum are
 //     in-lane reductions plus one v_permlane32_swap.
@@ -34,7 +35,7 @@ namespace fa {
 constexpr int kFwdWaves = 8;
 constexpr int kFwdBM = 32 * kFwdWaves;
 constexpr int kFwdBN = 64;
-constexpr int kFwdBufs = 3;
+constexpr int kFwdBufs = 4;   // ring depth: tiles nb, nb+1 read while nb+2, nb+3 land
 
 template <bool BF16, int D, bool CAUSAL>
 __global__ void __launch_bounds__(kFwdWaves * 64, 2) fwd_kernel(const FwdParams p) {
@@ -143,7 +144,14 @@ __global__ void __launch_bounds__(kFwdWaves * 64, 2) fwd_kernel(const FwdParams 
       }
     }
   };
-  auto tile_sync = [&]() { wait_dma_and_barrier(); };
+  // DMA operations one issue() leaves outstanding in this wave.  Step nb reads tiles nb (V) and
+  // nb+1 (K, software-pipelined QK^T) and issues nb+3; it ends waiting for nb+2 only, so nb+3
+  // stays in flight across the barrier.
+  int ndma = 0;
+#pragma unroll
+  for (int j = 0; j < PPW; ++j)
+    if (PIECES % NW == 0 || wave + j * NW < PIECES) ndma += 2;
+  auto tile_sync = [&](bool ahead) { wait_dma_keep_and_barrier(ahead ? ndma : 0); };
 
   // S^T = K Q^T for the tile in buffer kt (K fragments issued in groups of KG ahead of their MFMAs)
   constexpr int KG = (KS % 4 == 0) ? 4 : ((KS % 3 == 0) ? 3 : 2);
@@ -230,7 +238,9 @@ __global__ void __launch_bounds__(kFwdWaves * 64, 2) fwd_kernel(const FwdParams 
 
   if (nblk > 0) issue(0);
   if (nblk > 1) issue(1);
-  tile_sync();
+  wait_vmem_all();   // Q fragments, tiles 0 and 1 (compiler-visible: no vmcnt waits inside the loops)
+  if (nblk > 2) issue(2);
+  lds_barrier();
 
   // ---- fast path: unmasked tiles, QK^T of the next tile overlapped with this tile's softmax ----
   if (nfast > 0) {
@@ -238,7 +248,7 @@ __global__ void __launch_bounds__(kFwdWaves * 64, 2) fwd_kernel(const FwdParams 
     qk(0, sa);
     float mt = rowmax(sa);
     auto body = [&](int nb, f32x16_t (&scur)[NT], f32x16_t (&snxt)[NT]) {
-      if (nb + 2 < nblk) issue(nb + 2);
+      if (nb + 3 < nblk) issue(nb + 3);
       rescale(mt);
       const int cur = (nb % kFwdBufs) * 2 * TILE;
       const int nxt = ((nb + 1) % kFwdBufs) * 2 * TILE;
@@ -250,7 +260,7 @@ __global__ void __launch_bounds__(kFwdWaves * 64, 2) fwd_kernel(const FwdParams 
       __builtin_amdgcn_sched_barrier(0);   // bound the V-read hoisting (register pressure)
       pv(cur + TILE, pf);
       mt = rowmax(snxt);
-      tile_sync();
+      tile_sync(nb + 3 < nblk);
     };
     int nb = 0;
     for (; nb + 1 < nfast; nb += 2) {
@@ -263,7 +273,7 @@ __global__ void __launch_bounds__(kFwdWaves * 64, 2) fwd_kernel(const FwdParams 
   // ---- general path: causal diagonal / ragged tiles, per-element masks ----
   for (int nb = nfast; nb < nblk; ++nb) {
     const int n0 = nb * BN;
-    if (nb + 2 < nblk) issue(nb + 2);
+    if (nb + 3 < nblk) issue(nb + 3);
     const int cur = (nb % kFwdBufs) * 2 * TILE;
     const bool active = (wq0 < sq) && (!CAUSAL || n0 <= wq0 + 31);
     if (active) {
@@ -281,7 +291,7 @@ __global__ void __launch_bounds__(kFwdWaves * 64, 2) fwd_kernel(const FwdParams 
       softmax_pack(st, pf);
       pv(cur + TILE, pf);
     }
-    tile_sync();
+    tile_sync(nb + 3 < nblk);
   }
 
   // ---- epilogue ----
