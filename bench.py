@@ -80,30 +80,42 @@ def barrier(world):
         dist.barrier()
 
 
-def max_over_ranks(x, world):
+def max_over_ranks(x, world, device=None):
+    """MAX of a per-rank float over the job (one all-reduce outside the timed region)."""
     if world == 1:
         return x
     import torch
     import torch.distributed as dist
-    t = torch.tensor([x], dtype=torch.float64, device="cuda")
+    if device is None:
+        device = "cuda" if dist.get_backend() == "nccl" else "cpu"
+    t = torch.tensor([x], dtype=torch.float64, device=device)
     dist.all_reduce(t, op=dist.ReduceOp.MAX)
     return float(t.item())
 
 
-def timed(step, steps, warmup, world):
-    """W untimed steps, then EXACTLY `steps` steps bracketed by barrier + synchronize."""
-    import torch
+def timed(step, steps, warmup, world, sync=None):
+    """W untimed steps, then EXACTLY `steps` steps bracketed by barrier + synchronize on every
+    rank; returns the MAX elapsed seconds over ranks."""
+    if sync is None:
+        import torch
+        sync = torch.cuda.synchronize
     for _ in range(warmup):
         step()
     barrier(world)
-    torch.cuda.synchronize()
+    sync()
     t0 = time.perf_counter()
     for _ in range(steps):
         step()
-    torch.cuda.synchronize()
+    sync()
     t1 = time.perf_counter()
     barrier(world)
     return max_over_ranks(t1 - t0, world)
+
+
+def aggregate_tflops(flops_per_rank_step, steps, world, max_seconds):
+    """Whole-job throughput: every rank ran `steps` steps of `flops_per_rank_step` (weak scaling),
+    divided by the slowest rank's time."""
+    return world * flops_per_rank_step * steps / max_seconds / 1e12
 
 
 class KernelTimer:
@@ -166,8 +178,8 @@ def main():
     kt = timer.stop()
     # the timer also saw the warm-up launches; averages are per launch, so that is harmless
 
-    value = world * f_step * args.steps / t_step / 1e12
-    fwd_tflops = world * f_fwd * args.steps / t_fwd / 1e12
+    value = aggregate_tflops(f_step, args.steps, world, t_step)
+    fwd_tflops = aggregate_tflops(f_fwd, args.steps, world, t_fwd)
 
     # roofline of the dominant kernel (largest total device time in the fwd+bwd leg)
     alg = {"fwd_kernel": f_fwd, "bwd_dkdv_kernel": 2.0 * f_fwd, "bwd_dq_kernel": 1.5 * f_fwd}
