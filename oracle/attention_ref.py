@@ -91,7 +91,7 @@ def attention_lse_ref(q, k, causal=False, softmax_scale=None, key_padding_mask=N
         scores.masked_fill_(~key_padding_mask[:, None, None, :], float("-inf"))
     if causal:
         sq, sk = q.shape[1], k.shape[1]
-        scores.masked_fill_(torch.triu(torch.ones(sq, sk, dtype=torch.bool), 1), float("-inf"))
+        scores.masked_fill_(torch.triu(torch.ones(sq, sk, dtype=torch.bool, device=q.device), 1), float("-inf"))
     lse = torch.logsumexp(scores, dim=-1)
     lse = torch.where(torch.isneginf(lse), torch.full_like(lse, float("inf")), lse)
     return lse.float()

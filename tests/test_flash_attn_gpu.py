@@ -3,8 +3,8 @@
 Structure follows the reference's tests/test_flash_attn.py: the HIP result must satisfy the
 reference's acceptance rule ``max|x - ref| <= 2 * max|x_pt - ref|`` for out, dq, dk and dv, where
 ``ref`` is the oracle's fp32 attention and ``pt`` the same math in the input dtype with reordered
-ops (the reference's own estimate of PyTorch's numerical error).  The oracle runs on the host
-CPU; shapes are reduced in batch/heads (not in the seqlen / head-dim grid) so it finishes in
+ops (the reference's own estimate of PyTorch's numerical error).  The oracle's torch
+restatement runs on the kernel's device (as the reference's tests do); shapes are reduced in batch/heads (not in the seqlen / head-dim grid) so it finishes in
 seconds.  Headline-size runs are checked through sampled rows against a float64 restatement.
 """
 import math
@@ -30,12 +30,19 @@ def _need_gpu():
     import flash_attn_2_cuda  # noqa: F401  (fails loudly if the library is missing)
 
 
+# The oracle's torch restatement runs on the same device as the kernel under test, exactly as the
+# reference's own tests run attention_ref on cuda (tests/test_flash_attn.py:575-578): fp32 ``ref``
+# and the low-precision ``pt`` estimate then share the device BLAS, and the suite finishes in
+# minutes instead of hours of host matmuls.
+REF_DEV = DEV
+
+
 def _cpu_leaf(*xs):
-    return [x.detach().cpu().requires_grad_() for x in xs]
+    return [x.detach().to(REF_DEV).clone().requires_grad_() for x in xs]
 
 
 def _assert_bound(name, got, ref, pt, factor=2.0, floor=0.0):
-    ok, err, bound = check_within_bound(got.detach().cpu(), ref, pt, factor=factor, floor=floor)
+    ok, err, bound = check_within_bound(got.detach().to(ref.device), ref, pt.to(ref.device), factor=factor, floor=floor)
     assert ok, f"{name}: max|err| {err:.3e} > bound {bound:.3e}"
 
 
@@ -122,7 +129,7 @@ def test_flash_attn_output(seqlen_q, seqlen_k, d, causal, mha_type, dtype, kvpac
     qc, kc, vc = _cpu_leaf(q, k, v)
     out_ref, out_pt = _ref_and_pt(qc, kc, vc, causal=causal)
     _assert_bound("out", out, out_ref, out_pt)
-    gc = g.cpu()
+    gc = g.to(REF_DEV)
     gr = torch.autograd.grad(out_ref, (qc, kc, vc), gc)
     gp = torch.autograd.grad(out_pt, (qc, kc, vc), gc)
     for name, got, r, p in zip(("dq", "dk", "dv"), (dq, dk, dv), gr, gp):
@@ -145,15 +152,15 @@ def test_flash_attn_qkvpacked(seqlen, d, causal, dtype):
     assert s_dmask is None
     g = torch.randn_like(out)
     dqkv, = torch.autograd.grad(out, qkv, g)
-    qkvc = qkv.detach().cpu().requires_grad_()
+    qkvc = qkv.detach().to(REF_DEV).clone().requires_grad_()
     out_ref, _ = attention_ref(qkvc[:, :, 0], qkvc[:, :, 1], qkvc[:, :, 2], causal=causal)
     out_pt, _ = attention_ref(qkvc[:, :, 0], qkvc[:, :, 1], qkvc[:, :, 2], causal=causal,
                               upcast=False, reorder_ops=True)
     _assert_bound("out", out, out_ref, out_pt)
-    torch.testing.assert_close(lse.cpu(), attention_lse_ref(qkvc[:, :, 0], qkvc[:, :, 1], causal=causal),
+    torch.testing.assert_close(lse.to(REF_DEV), attention_lse_ref(qkvc[:, :, 0], qkvc[:, :, 1], causal=causal),
                                rtol=1e-4, atol=1e-3)
-    dref, = torch.autograd.grad(out_ref, qkvc, g.cpu())
-    dpt, = torch.autograd.grad(out_pt, qkvc, g.cpu())
+    dref, = torch.autograd.grad(out_ref, qkvc, g.to(REF_DEV))
+    dpt, = torch.autograd.grad(out_pt, qkvc, g.to(REF_DEV))
     _assert_bound("dqkv", dqkv, dref, dpt)
 
 
@@ -196,10 +203,10 @@ def test_flash_attn_varlen_output(seqlen_q, seqlen_k, d, causal, mha_type, dtype
     dq = dq_pad_fn(dq_unpad)
 
     qc, kc, vc = _cpu_leaf(q, k, v)
-    qmc, kmc = qm.cpu(), km.cpu()
+    qmc, kmc = qm.to(REF_DEV), km.to(REF_DEV)
     out_ref, out_pt = _ref_and_pt(qc, kc, vc, qmc, kmc, causal=causal)
     _assert_bound("out", out, out_ref, out_pt)
-    gc = g.cpu().masked_fill(~qmc[:, :, None, None], 0)
+    gc = g.to(REF_DEV).masked_fill(~qmc[:, :, None, None], 0)
     gr = torch.autograd.grad(out_ref, (qc, kc, vc), gc)
     gp = torch.autograd.grad(out_pt, (qc, kc, vc), gc)
     for name, got, r, p in zip(("dq", "dk", "dv"), (dq, dk, dv), gr, gp):
@@ -250,8 +257,8 @@ def test_flash_attn_bwd_overflow(seqlen, d, causal):
     qc, kc, vc = _cpu_leaf(q, k, v)
     out_ref, out_pt = _ref_and_pt(qc, kc, vc, causal=causal)
     _assert_bound("out", out, out_ref, out_pt)
-    gr = torch.autograd.grad(out_ref, (qc, kc, vc), g.cpu())
-    gp = torch.autograd.grad(out_pt, (qc, kc, vc), g.cpu())
+    gr = torch.autograd.grad(out_ref, (qc, kc, vc), g.to(REF_DEV))
+    gp = torch.autograd.grad(out_pt, (qc, kc, vc), g.to(REF_DEV))
     for name, got, r, p in zip(("dq", "dk", "dv"), (q.grad, k.grad, v.grad), gr, gp):
         _assert_bound(name, got, r, p, factor=5.0, floor=1e-3)
 
@@ -270,7 +277,7 @@ def test_flash_attn_bwd_transpose(seqlen, d, causal, dtype):
     out.backward(g)
     qc, kc, vc = _cpu_leaf(q, k, v)
     out_ref, out_pt = _ref_and_pt(qc, kc, vc, causal=causal)
-    gc = g.cpu().transpose(0, 1)
+    gc = g.to(REF_DEV).transpose(0, 1)
     gr = torch.autograd.grad(out_ref, (qc, kc, vc), gc)
     gp = torch.autograd.grad(out_pt, (qc, kc, vc), gc)
     _assert_bound("out", out.transpose(0, 1), out_ref, out_pt)
