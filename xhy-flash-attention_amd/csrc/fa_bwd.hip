@@ -12,8 +12,9 @@
 //   2. bwd_dkdv_kernel  one workgroup (8 waves) per 128-key block of a (batch, kv-head), the waves
 //                       specialised by role: 4 "P" waves hold K and accumulate dV^T, 4 "dS" waves
 //                       hold V and accumulate dK^T, P passing between them through LDS; (Q, dO,
-//                       LSE, D) slices of 64 query rows arrive by LDS-DMA two slices ahead into a
-//                       3-deep ring; dK^T / dV^T accumulate in registers over every slice (and, for
+//                       LSE, D) slices of 64 query rows arrive by LDS-DMA one slice ahead; the
+//                       dS waves run one slice behind the P waves so one wave's VALU hides under
+//                       the other's MFMAs with one barrier per slice; dK^T / dV^T accumulate in registers over every slice (and, for
 //                       GQA, every query head of the group) and are written once: no atomics.
 //   3. bwd_dq_kernel    one workgroup (8 waves) per 256-row query block, structured like the
 //                       forward: Q and dO fragments in registers, K/V tiles by LDS-DMA ring,
@@ -127,16 +128,20 @@ __global__ void __launch_bounds__(256) bwd_pre_kernel(const BwdParams p) {
 // ------------------------------------------------------------------------------------------------
 // 2. dK / dV  (wave-specialised: 4 "P" waves + 4 "dS" waves per 128-key block)
 // ------------------------------------------------------------------------------------------------
-// Waves 0-3 ("P" waves) hold K of their 32 keys and accumulate dV^T:
-//     S = Q K^T  ->  P = exp2(c S - LSE log2e) (masked)  ->  P to LDS  ->  dV^T += dO^T P
-// Waves 4-7 ("dS" waves) hold V of the same 32 keys and accumulate dK^T:
-//     dP = dO V^T  ->  (barrier, P from LDS)  dS = P o (dP - D)  ->  dK^T += Q^T dS
-// Both roles run the same instruction skeleton (row-read A operand x register B operand, then
-// transpose-read A operand x packed B operand); only the operand offsets and the elementwise step
-// differ.  Each wave needs one 32-key operand set and one D x 32 accumulator set (<= 256 registers),
-// so two waves share every SIMD and the hardware interleaves one wave's VALU / LDS work with the
-// other's MFMAs -- the single-wave-per-SIMD design that kept K, V, dK^T and dV^T in one wave could
-// not overlap them.  P crosses between the roles as an fp32 32x32 tile per (key group, q-tile).
+// Waves 0-3 ("P" waves) hold K of their 32 keys and accumulate dV^T; waves 4-7 ("dS" waves) hold
+// -V of the same 32 keys and accumulate -dK^T.  Per 64-row query slice `it` (ONE barrier per step):
+//   P waves:  S(it) = Q K^T -> P(it) = exp2(c S - LSE log2e) (masked) -> P(it) to LDS (fp32)
+//             -> dV^T += dO(it)^T P(it)
+//   dS waves: dS''(it-1) = P(it-1) o dP''(it-1)      (P of the previous slice, from LDS)
+//             -> dK''^T += Q(it-1)^T dS''(it-1)
+//             -> dP''(it) = D - dO(it) V^T           (MFMA chain started from D, on -V)
+// so dS'' = -dS and dK'' = -dK (sign folded into the epilogue scale): the dS step is one multiply
+// per element.  On every SIMD one P wave and one dS wave run side by side with complementary
+// phases -- the P wave's softmax VALU sits between its two MFMA blocks, the dS wave's VALU at the
+// start of its step -- so one wave's VALU hides under the other's MFMAs without a second barrier.
+// Slice lifetimes: Q (+ LSE, D) is read in steps it and it+1 (3-deep ring, one slice of DMA in
+// flight), dO only in step it (2-deep ring), P(it) in steps it and it+1 (2 buffers).
+// Each wave needs one 32-key operand set and one D x 32 accumulator set (<= 256 registers).
 template <bool BF16, int D, bool CAUSAL>
 __global__ void __launch_bounds__(kDkdvWaves * 64, 1) bwd_dkdv_kernel(const BwdParams p) {
   using E = Elt<BF16>;
@@ -145,14 +150,16 @@ __global__ void __launch_bounds__(kDkdvWaves * 64, 1) bwd_dkdv_kernel(const BwdP
   constexpr int KS = D / 16;
   constexpr int NP = D / 32;
   constexpr int QTILE = BQ * D * 2;                 // bytes of a Q or dO slice
-  constexpr int SLICE = 2 * QTILE + 2 * BQ * 4;     // Q | dO | lse[BQ] | D[BQ]
+  constexpr int QSLOT = QTILE + 2 * BQ * 4;         // Q | lse[BQ] | D[BQ]
+  constexpr int OBASE = 3 * QSLOT;                  // dO ring (2 slots)
   constexpr int XTILE = 32 * 32 * 4;                // one fp32 32x32 P tile
-  constexpr int XBASE = kBwdBufs * SLICE;
+  constexpr int XBUF = 4 * 2 * XTILE;               // P of one slice: 4 key groups x 2 q-tiles
+  constexpr int XBASE = OBASE + 2 * QTILE;
   constexpr int PIECES = QTILE / 1024;
   constexpr int PPW = (PIECES + NW - 1) / NW;
   static_assert(QTILE % 1024 == 0, "slice must be whole DMA pieces");
   static_assert(BQ == 64 && NW == 8, "two 32-row q-tiles per slice, 4 key groups x 2 roles");
-  __shared__ __attribute__((aligned(16))) char smem[XBASE + 4 * 2 * XTILE];
+  __shared__ __attribute__((aligned(16))) char smem[XBASE + 2 * XBUF];
 
   const AttnShape s = p.s;
   const int tid = threadIdx.x, lane = tid & 63;
@@ -175,7 +182,7 @@ __global__ void __launch_bounds__(kDkdvWaves * 64, 1) bwd_dkdv_kernel(const BwdP
   if (n0 >= sk) return;
   const int dlim = s.d;
 
-  // ---- this wave's 32 keys: K (P waves) or V (dS waves) fragments, the B operand of phase 1 ----
+  // ---- this wave's 32 keys: K (P waves) or -V (dS waves) fragments, the B operand of phase 1 ----
   const int kw0 = n0 + 32 * kg;
   const int key = kw0 + r;
   i16x8_t kv[KS];
@@ -183,10 +190,13 @@ __global__ void __launch_bounds__(kDkdvWaves * 64, 1) bwd_dkdv_kernel(const BwdP
     const bool ok = key < sk;
     const u16* src = pwave ? (const u16*)p.k + geo.k_off + (int64_t)kvh * p.k_head + (int64_t)(ok ? key : 0) * p.k_row
                            : (const u16*)p.v + geo.v_off + (int64_t)kvh * p.v_head + (int64_t)(ok ? key : 0) * p.v_row;
+    const unsigned flip = pwave ? 0u : 0x80008000u;   // sign bits of both 16-bit halves
 #pragma unroll
     for (int ks = 0; ks < KS; ++ks) {
       const int d0 = 16 * ks + 8 * hh;
-      kv[ks] = __builtin_bit_cast(i16x8_t, ld16(src + d0, ok && d0 < dlim));
+      u32x4_t w = ld16(src + d0, ok && d0 < dlim);
+      w[0] ^= flip; w[1] ^= flip; w[2] ^= flip; w[3] ^= flip;
+      kv[ks] = __builtin_bit_cast(i16x8_t, w);
     }
   }
 
@@ -205,7 +215,8 @@ __global__ void __launch_bounds__(kDkdvWaves * 64, 1) bwd_dkdv_kernel(const BwdP
   auto issue = [&](int it) {
     const int hq = h_begin + it / ns;
     const int q0 = (m_first + it % ns) * BQ;
-    char* dst = smem + (it % kBwdBufs) * SLICE;
+    char* qdst = smem + (it % 3) * QSLOT;
+    char* odst = smem + OBASE + (it & 1) * QTILE;
     const u16* Qp = (const u16*)p.q + geo.q_off + (int64_t)hq * p.q_head + (int64_t)q0 * p.q_row;
     const u16* Dp = (const u16*)p.dout + geo.do_off + (int64_t)hq * p.do_head + (int64_t)q0 * p.do_row;
     const buf_rsrc_t rq = make_rsrc(Qp, rec_bytes(sq - q0, p.q_row, 2));
@@ -214,18 +225,18 @@ __global__ void __launch_bounds__(kDkdvWaves * 64, 1) bwd_dkdv_kernel(const BwdP
     for (int j = 0; j < PPW; ++j) {
       const int pc = wave + j * NW;
       if (PIECES % NW == 0 || pc < PIECES) {
-        dma16(rq, dst + pc * 1024, voff_q[j]);
-        dma16(ro, dst + QTILE + pc * 1024, voff_o[j]);
+        dma16(rq, qdst + pc * 1024, voff_q[j]);
+        dma16(ro, odst + pc * 1024, voff_o[j]);
       }
     }
     if (wave < 2) {   // wave 0: LSE rows, wave 1: D rows (64 x 4 bytes each)
       const int64_t bhi = (int64_t)bidb * s.h + hq;
       const float* src = (wave == 0) ? p.lse + bhi * s.lse_pitch + q0 : p.dsum + bhi * p.seqlen_q_rounded + q0;
-      dma4(make_rsrc(src, rec_bytes(sq - q0, 1, 4)), dst + 2 * QTILE + wave * BQ * 4, lane * 4);
+      dma4(make_rsrc(src, rec_bytes(sq - q0, 1, 4)), qdst + QTILE + wave * BQ * 4, lane * 4);
     }
   };
 
-  // dV^T (P waves) or dK^T (dS waves): D x 32 keys
+  // dV^T (P waves) or -dK^T (dS waves): D x 32 keys
   f32x16_t acc[NP];
 #pragma unroll
   for (int t = 0; t < NP; ++t)
@@ -233,19 +244,54 @@ __global__ void __launch_bounds__(kDkdvWaves * 64, 1) bwd_dkdv_kernel(const BwdP
     for (int g = 0; g < 16; ++g) acc[t][g] = 0.f;
 
   const float c = s.scale_log2;
-  // phase-1 A operand rows: Q (P waves) / dO (dS waves); phase-2 transposed A operand: the other
-  const int a1_off = pwave ? 0 : QTILE;
-  const int a2_off = pwave ? QTILE : 0;
-  char* const xw = smem + XBASE + kg * 2 * XTILE + lane * 16;   // this key group's P tiles
 
-  // DMA operations one issue() leaves outstanding in this wave (for the counted vmcnt wait)
-  int ndma = wave < 2 ? 1 : 0;
+  // phase 1: S = Q K^T (P waves) / dP'' = D - dO V^T (dS waves) for both 32-row q-tiles of the
+  // slice at `a1` (query on registers, key on lane), chains started from `init`
+  auto phase1 = [&](int a1, f32x16_t (&sp)[2]) {
+    const TileAddr ta(lb, a1);
+    constexpr int G = KS >= 4 ? KS / 2 : KS;   // A fragments in flight per group (register budget)
+    static_for<0, KS / G>([&](auto GG) {
+      constexpr int g0 = decltype(GG)::value * G;
+      i16x8_t af0[G], af1[G];
+      static_for<0, G>([&](auto KK) {
+        constexpr int ks = g0 + decltype(KK)::value;
+        af0[ks - g0] = row_read_c<BQ, 0, 2 * ks>(smem, ta);
+        af1[ks - g0] = row_read_c<BQ, 32, 2 * ks>(smem, ta);
+      });
 #pragma unroll
-  for (int j = 0; j < PPW; ++j)
-    if (PIECES % NW == 0 || wave + j * NW < PIECES) ndma += 2;
+      for (int k = 0; k < G; ++k) {
+        sp[0] = E::mfma(af0[k], kv[g0 + k], sp[0]);
+        sp[1] = E::mfma(af1[k], kv[g0 + k], sp[1]);
+      }
+    });
+  };
+  // phase 2: acc += A^T frag, transposed A operand of the slice tile at `a2`; the fragments of
+  // d-group dt+1 are requested before the MFMAs of group dt
+  auto phase2 = [&](int a2, const i16x8_t (&fr)[4]) {
+    const TileAddr ta2(lb, a2);
+    i16x8_t tf[2][4];
+    auto tr_group = [&](auto DTC, i16x8_t (&t)[4]) {
+      constexpr int dt = decltype(DTC)::value;
+      t[0] = tr_frag_c<BQ, 0, dt>(smem, ta2);
+      t[1] = tr_frag_c<BQ, 16, dt>(smem, ta2);
+      t[2] = tr_frag_c<BQ, 32, dt>(smem, ta2);
+      t[3] = tr_frag_c<BQ, 48, dt>(smem, ta2);
+    };
+    tr_group(std::integral_constant<int, 0>{}, tf[0]);
+    static_for<0, NP>([&](auto DTC) {
+      constexpr int dt = decltype(DTC)::value;
+      if constexpr (dt + 1 < NP) tr_group(std::integral_constant<int, dt + 1>{}, tf[(dt + 1) & 1]);
+      __builtin_amdgcn_sched_barrier(0);
+      acc[dt] = E::mfma(tf[dt & 1][0], fr[0], acc[dt]);
+      acc[dt] = E::mfma(tf[dt & 1][1], fr[1], acc[dt]);
+      acc[dt] = E::mfma(tf[dt & 1][2], fr[2], acc[dt]);
+      acc[dt] = E::mfma(tf[dt & 1][3], fr[3], acc[dt]);
+      __builtin_amdgcn_sched_barrier(0);
+    });
+  };
 
-  // P = exp2(c S - LSE log2e) for both q-tiles, published for the dS waves of this key group
-  auto p_step = [&](auto MASKC, f32x16_t (&sp)[2], const float* lt, int q0, i16x8_t (&fr)[4]) {
+  // P = exp2(c S - LSE log2e) for both q-tiles into `xw` (this key group's P tiles), packed to `fr`
+  auto p_step = [&](auto MASKC, f32x16_t (&sp)[2], const float* lt, int q0, char* xw, i16x8_t (&fr)[4]) {
     constexpr bool MASK = decltype(MASKC)::value;
 #pragma unroll
     for (int qi = 0; qi < 2; ++qi) {
@@ -269,95 +315,73 @@ __global__ void __launch_bounds__(kDkdvWaves * 64, 1) bwd_dkdv_kernel(const BwdP
       fr[2 * qi + 1] = pack_frag<BF16>(sp[qi], 1);
     }
   };
+  // dS'' = P o dP'' of the slice whose P tiles are at `xw`, packed to `fr`
+  auto ds_step = [&](const f32x16_t (&sp)[2], const char* xw, i16x8_t (&fr)[4]) {
+#pragma unroll
+    for (int qi = 0; qi < 2; ++qi) {
+      f32x16_t x;
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const f32x4_t pv = *(const f32x4_t*)(xw + qi * XTILE + u * 1024);
+#pragma unroll
+        for (int j = 0; j < 4; ++j) x[4 * u + j] = pv[j] * sp[qi][4 * u + j];
+      }
+      fr[2 * qi] = pack_frag<BF16>(x, 0);
+      fr[2 * qi + 1] = pack_frag<BF16>(x, 1);
+    }
+  };
+  auto xw_of = [&](int it) { return smem + XBASE + (it & 1) * XBUF + kg * 2 * XTILE + lane * 16; };
 
   if (total > 0) issue(0);
   wait_vmem_all();   // K/V fragments and slice 0 (compiler-visible: no vmcnt waits inside the loop)
-  if (total > 1) issue(1);
   lds_barrier();
 
+  f32x16_t dpp[2];   // dS waves: dP'' of the previous slice
   for (int it = 0; it < total; ++it) {
-    const bool ahead = it + 2 < total;
-    if (ahead) issue(it + 2);
+    if (it + 1 < total) issue(it + 1);
     const int q0 = (m_first + it % ns) * BQ;
-    const int so = (it % kBwdBufs) * SLICE;
-    const float* lt = (const float*)(smem + so + 2 * QTILE);
-
-    // phase 1: S = Q K^T or dP = dO V^T for both 32-row q-tiles (query on registers, key on lane);
-    // every A fragment is requested before the first MFMA so only the first read's latency shows
-    f32x16_t sp[2];
-    {
-      const TileAddr ta(lb, so + a1_off);
-      i16x8_t af0[KS], af1[KS];
-      static_for<0, KS>([&](auto KK) {
-        constexpr int ks = decltype(KK)::value;
-        af0[ks] = row_read_c<BQ, 0, 2 * ks>(smem, ta);
-        af1[ks] = row_read_c<BQ, 32, 2 * ks>(smem, ta);
-      });
-      __builtin_amdgcn_sched_barrier(0);
-      const f32x16_t zero = {};
-      sp[0] = E::mfma(af0[0], kv[0], zero);
-      sp[1] = E::mfma(af1[0], kv[0], zero);
-#pragma unroll
-      for (int ks = 1; ks < KS; ++ks) {
-        sp[0] = E::mfma(af0[ks], kv[ks], sp[0]);
-        sp[1] = E::mfma(af1[ks], kv[ks], sp[1]);
-      }
-    }
-
+    const int qs = (it % 3) * QSLOT;
+    const float* lt = (const float*)(smem + qs + QTILE);
+    const int os = OBASE + (it & 1) * QTILE;
     i16x8_t fr[4];
     if (pwave) {
+      f32x16_t sp[2];
+      sp[0] = f32x16_t{};
+      sp[1] = f32x16_t{};
+      phase1(qs, sp);
       const bool fast = (q0 + BQ <= sq) && (n0 + kDkdvBN <= sk) && (!CAUSAL || q0 >= n0 + kDkdvBN - 1);
-      if (fast) p_step(std::false_type{}, sp, lt, q0, fr);
-      else p_step(std::true_type{}, sp, lt, q0, fr);
-    }
-    lds_barrier();
-    const TileAddr ta2(lb, so + a2_off);
-    i16x8_t tf[2][4];
-    auto tr_group = [&](auto DTC, i16x8_t (&t)[4]) {
-      constexpr int dt = decltype(DTC)::value;
-      t[0] = tr_frag_c<BQ, 0, dt>(smem, ta2);
-      t[1] = tr_frag_c<BQ, 16, dt>(smem, ta2);
-      t[2] = tr_frag_c<BQ, 32, dt>(smem, ta2);
-      t[3] = tr_frag_c<BQ, 48, dt>(smem, ta2);
-    };
-    tr_group(std::integral_constant<int, 0>{}, tf[0]);
-    if (!pwave) {
-      // dS = P o (dP - D)
+      if (fast) p_step(std::false_type{}, sp, lt, q0, xw_of(it), fr);
+      else p_step(std::true_type{}, sp, lt, q0, xw_of(it), fr);
+      phase2(os, fr);                                    // dV^T += dO^T P
+    } else {
+      if (it > 0) {
+        ds_step(dpp, xw_of(it - 1), fr);
+        phase2(((it + 2) % 3) * QSLOT, fr);              // dK''^T += Q(it-1)^T dS''(it-1)
+      }
 #pragma unroll
-      for (int qi = 0; qi < 2; ++qi) {
+      for (int qi = 0; qi < 2; ++qi)
 #pragma unroll
         for (int u = 0; u < 4; ++u) {
           const f32x4_t dv = *(const f32x4_t*)(lt + BQ + 32 * qi + 8 * u + 4 * hh);
-          const f32x4_t pv = *(const f32x4_t*)(xw + qi * XTILE + u * 1024);
 #pragma unroll
-          for (int j = 0; j < 4; ++j) sp[qi][4 * u + j] = pv[j] * (sp[qi][4 * u + j] - dv[j]);
+          for (int j = 0; j < 4; ++j) dpp[qi][4 * u + j] = dv[j];
         }
-        fr[2 * qi] = pack_frag<BF16>(sp[qi], 0);
-        fr[2 * qi + 1] = pack_frag<BF16>(sp[qi], 1);
-      }
+      phase1(os, dpp);                                   // dP'' = D - dO V^T
     }
-
-    // phase 2: dV^T += dO^T P  /  dK^T += Q^T dS; the transposed fragments of group dt+1 are
-    // requested before the MFMAs of group dt
-    static_for<0, NP>([&](auto DTC) {
-      constexpr int dt = decltype(DTC)::value;
-      if constexpr (dt + 1 < NP) tr_group(std::integral_constant<int, dt + 1>{}, tf[(dt + 1) & 1]);
-      __builtin_amdgcn_sched_barrier(0);
-      acc[dt] = E::mfma(tf[dt & 1][0], fr[0], acc[dt]);
-      acc[dt] = E::mfma(tf[dt & 1][1], fr[1], acc[dt]);
-      acc[dt] = E::mfma(tf[dt & 1][2], fr[2], acc[dt]);
-      acc[dt] = E::mfma(tf[dt & 1][3], fr[3], acc[dt]);
-      __builtin_amdgcn_sched_barrier(0);
-    });
-    wait_dma_keep_and_barrier(ahead ? ndma : 0);
+    wait_dma_keep_and_barrier(0);
+  }
+  if (!pwave && total > 0) {   // the last slice's dK update (no DMA after it: its Q is resident)
+    i16x8_t fr[4];
+    ds_step(dpp, xw_of(total - 1), fr);
+    phase2(((total - 1) % 3) * QSLOT, fr);
   }
 
-  // ---- epilogue: dV = (dV^T)^T from the P waves, dK = scale * (dK^T)^T from the dS waves ----
+  // ---- epilogue: dV = (dV^T)^T from the P waves, dK = -scale * (dK''^T)^T from the dS waves ----
   if (key < sk) {
     const int hd = p.gqa_reduce ? kvh : hx;
     u16* row = pwave ? (u16*)p.dv + geo.dv_off + (int64_t)hd * p.dv_head + (int64_t)key * p.dv_row
                      : (u16*)p.dk + geo.dk_off + (int64_t)hd * p.dk_head + (int64_t)key * p.dk_row;
-    const float sc = pwave ? 1.f : s.scale;
+    const float sc = pwave ? 1.f : -s.scale;
 #pragma unroll
     for (int dt = 0; dt < NP; ++dt)
 #pragma unroll
