@@ -22,9 +22,13 @@
  *     compatibility but must be NULL (out of scope for this build: the call
  *     fails with a message otherwise);
  *   - backward: softmax_d (b, h, seqlen_q_rounded) fp32 is a caller-owned
- *     output (D = rowsum(dO * O)); dq_accum is accepted but unused and may be
- *     NULL (the MI355X backward computes dQ in its own kernel, without the
- *     reference's fp32 atomic accumulator); for MQA/GQA the caller passes dk/dv
+ *     output (D = rowsum(dO * O)); dq_accum is caller-owned fp32 SCRATCH of at
+ *     least batch * num_heads * seqlen_q_rounded floats (the reference's
+ *     (b, h, sq_r, d_r) dq_accum always qualifies).  The MI355X backward needs
+ *     no fp32 dQ accumulator (dQ has its own kernel, no atomics); it stores
+ *     -LSE / softmax_scale per query row there.  dq_accum may be NULL: the
+ *     library then takes the scratch from the stream-ordered allocator
+ *     (hipMallocAsync / hipFreeAsync on `stream`); for MQA/GQA the caller passes dk/dv
  *     with num_heads heads ("expanded", reference flash_api.cpp:628-635) and
  *     sums the groups itself;
  *   - num_splits is accepted and ignored: the MI355X backward uses no atomics,

@@ -122,7 +122,12 @@ __global__ void __launch_bounds__(256) bwd_pre_kernel(const BwdParams p) {
   }
 #pragma unroll
   for (int m = 8; m >= 1; m >>= 1) acc += __shfl_xor(acc, m, 16);
-  if (l16 == 0) p.dsum[((int64_t)bidb * s.h + head) * p.seqlen_q_rounded + row] = acc;
+  if (l16 == 0) {
+    const int64_t bhi = (int64_t)bidb * s.h + head;
+    p.dsum[bhi * p.seqlen_q_rounded + row] = acc;
+    // -LSE / scale: the initial accumulator of the dK/dV kernel's S chain (scale != 0: launch_bwd)
+    p.lse_s[bhi * p.seqlen_q_rounded + row] = -p.lse[bhi * s.lse_pitch + row] / s.scale;
+  }
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -130,7 +135,8 @@ __global__ void __launch_bounds__(256) bwd_pre_kernel(const BwdParams p) {
 // ------------------------------------------------------------------------------------------------
 // Waves 0-3 ("P" waves) hold K of their 32 keys and accumulate dV^T; waves 4-7 ("dS" waves) hold
 // -V of the same 32 keys and accumulate -dK^T.  Per 64-row query slice `it` (ONE barrier per step):
-//   P waves:  S(it) = Q K^T -> P(it) = exp2(c S - LSE log2e) (masked) -> P(it) to LDS (fp32)
+//   P waves:  S'(it) = Q K^T - LSE/scale (MFMA chain started from -LSE/scale, computed by
+//             bwd_pre_kernel) -> P(it) = exp2(c S') (masked) -> P(it) to LDS (fp32)
 //             -> dV^T += dO(it)^T P(it)
 //   dS waves: dS''(it-1) = P(it-1) o dP''(it-1)      (P of the previous slice, from LDS)
 //             -> dK''^T += Q(it-1)^T dS''(it-1)
@@ -231,7 +237,7 @@ __global__ void __launch_bounds__(kDkdvWaves * 64, 1) bwd_dkdv_kernel(const BwdP
     }
     if (wave < 2) {   // wave 0: LSE rows, wave 1: D rows (64 x 4 bytes each)
       const int64_t bhi = (int64_t)bidb * s.h + hq;
-      const float* src = (wave == 0) ? p.lse + bhi * s.lse_pitch + q0 : p.dsum + bhi * p.seqlen_q_rounded + q0;
+      const float* src = ((wave == 0) ? p.lse_s : p.dsum) + bhi * p.seqlen_q_rounded + q0;
       dma4(make_rsrc(src, rec_bytes(sq - q0, 1, 4)), qdst + QTILE + wave * BQ * 4, lane * 4);
     }
   };
@@ -291,17 +297,18 @@ __global__ void __launch_bounds__(kDkdvWaves * 64, 1) bwd_dkdv_kernel(const BwdP
   };
 
   // P = exp2(c S - LSE log2e) for both q-tiles into `xw` (this key group's P tiles), packed to `fr`
-  auto p_step = [&](auto MASKC, f32x16_t (&sp)[2], const float* lt, int q0, char* xw, i16x8_t (&fr)[4]) {
+  // P = exp2(c S') with S' = S - LSE / scale (the chain started from -LSE / scale) for both q-tiles
+  // into `xw` (this key group's P tiles), packed to `fr`
+  auto p_step = [&](auto MASKC, f32x16_t (&sp)[2], int q0, char* xw, i16x8_t (&fr)[4]) {
     constexpr bool MASK = decltype(MASKC)::value;
 #pragma unroll
     for (int qi = 0; qi < 2; ++qi) {
 #pragma unroll
       for (int u = 0; u < 4; ++u) {
-        const f32x4_t lv = *(const f32x4_t*)(lt + 32 * qi + 8 * u + 4 * hh);
         f32x4_t pv;
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
-          float x = fast_exp2(fmaf(sp[qi][4 * u + j], c, -lv[j] * kLog2e));
+          float x = fast_exp2(sp[qi][4 * u + j] * c);
           if constexpr (MASK) {
             const int q = q0 + 32 * qi + 8 * u + 4 * hh + j;
             x = (key >= sk || q >= sq || (CAUSAL && key > q)) ? 0.f : x;
@@ -336,7 +343,11 @@ __global__ void __launch_bounds__(kDkdvWaves * 64, 1) bwd_dkdv_kernel(const BwdP
   wait_vmem_all();   // K/V fragments and slice 0 (compiler-visible: no vmcnt waits inside the loop)
   lds_barrier();
 
-  f32x16_t dpp[2];   // dS waves: dP'' of the previous slice
+  // One instruction skeleton for both roles (phase 1 and phase 2 each have ONE call site, so the
+  // register assignment of `sp` / `acc` is shared and no accumulator copies appear at the joins):
+  //   dS waves: dS''(it-1) from sp (VALU) | sp = dP''(it) (MFMA) |                 | dK'' += Q(it-1)^T dS''
+  //   P waves:                            | sp = S(it)     (MFMA) | P(it) (VALU)    | dV   += dO(it)^T P
+  f32x16_t sp[2];    // S of this slice (P waves) / dP'' of the previous slice (dS waves)
   for (int it = 0; it < total; ++it) {
     if (it + 1 < total) issue(it + 1);
     const int q0 = (m_first + it % ns) * BQ;
@@ -344,35 +355,29 @@ __global__ void __launch_bounds__(kDkdvWaves * 64, 1) bwd_dkdv_kernel(const BwdP
     const float* lt = (const float*)(smem + qs + QTILE);
     const int os = OBASE + (it & 1) * QTILE;
     i16x8_t fr[4];
-    if (pwave) {
-      f32x16_t sp[2];
-      sp[0] = f32x16_t{};
-      sp[1] = f32x16_t{};
-      phase1(qs, sp);
-      const bool fast = (q0 + BQ <= sq) && (n0 + kDkdvBN <= sk) && (!CAUSAL || q0 >= n0 + kDkdvBN - 1);
-      if (fast) p_step(std::false_type{}, sp, lt, q0, xw_of(it), fr);
-      else p_step(std::true_type{}, sp, lt, q0, xw_of(it), fr);
-      phase2(os, fr);                                    // dV^T += dO^T P
-    } else {
-      if (it > 0) {
-        ds_step(dpp, xw_of(it - 1), fr);
-        phase2(((it + 2) % 3) * QSLOT, fr);              // dK''^T += Q(it-1)^T dS''(it-1)
+    if (!pwave && it > 0) ds_step(sp, xw_of(it - 1), fr);
+    // chain start: -LSE / scale (P waves) or D (dS waves), per accumulator row
+    const float* init = lt + (pwave ? 0 : BQ);
+#pragma unroll
+    for (int qi = 0; qi < 2; ++qi)
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const f32x4_t iv = *(const f32x4_t*)(init + 32 * qi + 8 * u + 4 * hh);
+#pragma unroll
+        for (int j = 0; j < 4; ++j) sp[qi][4 * u + j] = iv[j];
       }
-#pragma unroll
-      for (int qi = 0; qi < 2; ++qi)
-#pragma unroll
-        for (int u = 0; u < 4; ++u) {
-          const f32x4_t dv = *(const f32x4_t*)(lt + BQ + 32 * qi + 8 * u + 4 * hh);
-#pragma unroll
-          for (int j = 0; j < 4; ++j) dpp[qi][4 * u + j] = dv[j];
-        }
-      phase1(os, dpp);                                   // dP'' = D - dO V^T
+    phase1(pwave ? qs : os, sp);                       // S' = Q K^T - LSE/scale  /  dP'' = D - dO V^T
+    if (pwave) {
+      const bool fast = (q0 + BQ <= sq) && (n0 + kDkdvBN <= sk) && (!CAUSAL || q0 >= n0 + kDkdvBN - 1);
+      if (fast) p_step(std::false_type{}, sp, q0, xw_of(it), fr);
+      else p_step(std::true_type{}, sp, q0, xw_of(it), fr);
     }
+    if (pwave || it > 0) phase2(pwave ? os : ((it + 2) % 3) * QSLOT, fr);   // dV^T / dK''^T
     wait_dma_keep_and_barrier(0);
   }
   if (!pwave && total > 0) {   // the last slice's dK update (no DMA after it: its Q is resident)
     i16x8_t fr[4];
-    ds_step(dpp, xw_of(total - 1), fr);
+    ds_step(sp, xw_of(total - 1), fr);
     phase2(((total - 1) % 3) * QSLOT, fr);
   }
 
@@ -619,6 +624,7 @@ void bwd_block_size(int d, int* block_m, int* block_n) {
 
 template <bool BF16>
 static void launch_bwd_t(const BwdParams& p, hipStream_t stream) {
+  if (p.lse_s == nullptr) throw std::runtime_error("flash_attn_bwd: no scratch for the scaled LSE");
   {
     dim3 grid(p.s.b * p.s.h, (p.s.seqlen_q + 15) / 16);
     prof_begin(kTimeBwdPre, stream);
@@ -628,11 +634,35 @@ static void launch_bwd_t(const BwdParams& p, hipStream_t stream) {
   if (p.s.causal) dispatch_bwd_d<BF16, true>(p, stream); else dispatch_bwd_d<BF16, false>(p, stream);
 }
 
-void launch_bwd(const BwdParams& p, bool is_bf16, hipStream_t stream) {
-  if (p.s.b <= 0 || p.s.h <= 0 || p.s.seqlen_q <= 0) return;
-  if ((p.s.seqlen_q + kDqBM - 1) / kDqBM > 65535 || (p.s.seqlen_q + 15) / 16 > 65535)
+void launch_bwd(const BwdParams& p_in, bool is_bf16, hipStream_t stream) {
+  if (p_in.s.b <= 0 || p_in.s.h <= 0 || p_in.s.seqlen_q <= 0) return;
+  if ((p_in.s.seqlen_q + kDqBM - 1) / kDqBM > 65535 || (p_in.s.seqlen_q + 15) / 16 > 65535)
     throw std::runtime_error("flash_attn_bwd: seqlen_q too large for the grid");
+  BwdParams p = p_in;
+  // softmax_scale == 0 (uniform attention) would make -LSE / scale infinite: a tiny positive scale
+  // gives the same P to fp32 precision (P deviates from uniform by 1e-30 |S|) and dQ, dK ~ 1e-30.
+  if (p.s.scale == 0.f) { p.s.scale = 1e-30f; p.s.scale_log2 = 1e-30f * kLog2e; }
+  // scratch for -LSE / scale: the caller's dq_accum, else the stream-ordered allocator
+  void* ws = nullptr;
+  p.lse_s = p.dq_accum;
+  if (p.lse_s == nullptr) {
+    static bool pool_kept = false;
+    if (!pool_kept) {   // keep freed blocks in the device pool across synchronisations
+      int dev = 0;
+      hipMemPool_t pool;
+      if (hipGetDevice(&dev) == hipSuccess && hipDeviceGetDefaultMemPool(&pool, dev) == hipSuccess) {
+        uint64_t thr = UINT64_MAX;
+        (void)hipMemPoolSetAttribute(pool, hipMemPoolAttrReleaseThreshold, &thr);
+      }
+      pool_kept = true;
+    }
+    const size_t bytes = (size_t)p.s.b * p.s.h * p.seqlen_q_rounded * sizeof(float);
+    if (hipMallocAsync(&ws, bytes, stream) != hipSuccess)
+      throw std::runtime_error("flash_attn_bwd: hipMallocAsync of the LSE scratch failed");
+    p.lse_s = static_cast<float*>(ws);
+  }
   if (is_bf16) launch_bwd_t<true>(p, stream); else launch_bwd_t<false>(p, stream);
+  if (ws != nullptr) (void)hipFreeAsync(ws, stream);
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) throw std::runtime_error(std::string("flash_attn_bwd launch: ") + hipGetErrorString(e));
 }

@@ -131,7 +131,6 @@ bool bwd_impl(const void* dout, const void* q, const void* k, const void* v, con
   FA_BEGIN
   check_common(b, h, hk, d, d_r, p_dropout, attn_mask, flashmask);
   FA_CHECK(dout && q && k && v && out && softmax_d && lse && dq && dk && dv);
-  (void)dq_accum;  // workspace of the reference's atomic dQ path; the MI355X backward needs none
   FA_CHECK(d_r % 32 == 0);
   FA_CHECK(sq_r >= sq);
   fa::BwdParams p;

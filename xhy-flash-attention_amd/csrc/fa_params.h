@@ -48,7 +48,9 @@ struct BwdParams {
   void* dq; void* dk; void* dv;
   const float* lse;
   float* dsum;      // softmax_d: (b, h, seqlen_q_rounded) fp32, D = rowsum(dO * O)
-  float* dq_accum;  // (b, h, seqlen_q_rounded, d_rounded) fp32
+  float* dq_accum;  // caller scratch (reference: (b, h, seqlen_q_rounded, d_rounded) fp32)
+  float* lse_s;     // scratch (b, h, seqlen_q_rounded) fp32: -LSE / scale, written by bwd_pre_kernel
+                    // (dq_accum when given, else stream-ordered allocation in launch_bwd)
   int64_t q_batch, q_row, q_head;
   int64_t k_batch, k_row, k_head;
   int64_t v_batch, v_row, v_head;

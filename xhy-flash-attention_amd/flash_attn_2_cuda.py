@@ -320,7 +320,9 @@ def bwd(dout, q, k, v, out, softmax_lse, dq_, dk_, dv_, p_dropout, softmax_scale
 
     with torch.cuda.device(q.device):
         softmax_d = torch.empty((batch_size, num_heads, seqlen_q_rounded), dtype=torch.float32, device=q.device)
-        dq_accum = None  # the MI355X backward has no fp32 dQ accumulator (see include/flash_attn.h)
+        # scratch for the kernels' -LSE/scale rows (the reference allocates (b, h, sq_r, d_r) here for
+        # its fp32 atomic dQ accumulator; the MI355X backward needs only (b, h, sq_r))
+        dq_accum = torch.empty((batch_size, num_heads, seqlen_q_rounded), dtype=torch.float32, device=q.device)
         fn = _lib.flash_attn_bwd if num_heads == num_heads_k else _lib.flash_attn_bwd_gqa
         st = [_strides(x, 4) for x in (qk, kk, vk, ok_, dq, dk, dv, dok)]
         (qb, qr, qh), (kb, kr, kh), (vb, vr, vh), (ob, orr, oh) = st[:4]
@@ -376,7 +378,9 @@ def varlen_bwd(dout, q, k, v, out, softmax_lse, dq_, dk_, dv_, cu_seqlens_q, cu_
 
     with torch.cuda.device(q.device):
         softmax_d = torch.empty((batch_size, num_heads, seqlen_q_rounded), dtype=torch.float32, device=q.device)
-        dq_accum = None  # the MI355X backward has no fp32 dQ accumulator (see include/flash_attn.h)
+        # scratch for the kernels' -LSE/scale rows (the reference allocates (b, h, sq_r, d_r) here for
+        # its fp32 atomic dQ accumulator; the MI355X backward needs only (b, h, sq_r))
+        dq_accum = torch.empty((batch_size, num_heads, seqlen_q_rounded), dtype=torch.float32, device=q.device)
         if zero_tensors:
             dq.zero_(); dk.zero_(); dv.zero_(); softmax_d.zero_()
         fn = _lib.flash_attn_varlen_bwd if num_heads == num_heads_k else _lib.flash_attn_varlen_bwd_gqa
