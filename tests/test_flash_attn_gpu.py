@@ -433,3 +433,46 @@ def test_headline_sizes_sampled(cfg):
             gv = dv[bi, keys, hi].double().cpu().numpy()
             np.testing.assert_allclose(gk, ref["dK"], atol=tol * max(1.0, np.abs(ref["dK"]).max()), rtol=0)
             np.testing.assert_allclose(gv, ref["dV"], atol=tol * max(1.0, np.abs(ref["dV"]).max()), rtol=0)
+
+
+# ------------------------------------------------------------------------------------------------
+# deferred-max rescale (fa_fwd.hip kFwdRescaleThr): inputs that FORCE the rare branches
+# (cdna_hip_programming.md §5.4 rule 26) -- a key that jumps a row's max far past the threshold
+# at a late tile, and keys that raise the max gradually (each step below the threshold, so P grows
+# towards 2^8 before a rescale) -- checked with the reference's 2x rule on out and grads.
+# ------------------------------------------------------------------------------------------------
+@pytest.mark.parametrize("dtype", DTYPES)
+@pytest.mark.parametrize("causal", [False, True])
+@pytest.mark.parametrize("mode", ["jump", "ramp"])
+def test_fwd_deferred_max_forced(mode, causal, dtype):
+    from flash_attn import flash_attn_func
+
+    torch.manual_seed(0)
+    b, s, h, d = 2, 1024, 2, 128
+    q = torch.randn(b, s, h, d, device=DEV, dtype=torch.float32)
+    k = torch.randn(b, s, h, d, device=DEV, dtype=torch.float32)
+    v = torch.randn(b, s, h, d, device=DEV, dtype=torch.float32)
+    qn = q / q.norm(dim=-1, keepdim=True)
+    rows = [700, 901, 1023, 777]
+    for i in rows:
+        if mode == "jump":
+            # one key at a late tile with score ~ +24 (natural log) above the rest for row i
+            j = i - 3
+            k[:, j] = qn[:, i] * (24.0 * d ** 0.5)
+        else:
+            # keys 64 apart whose scores for row i rise by ~2 per tile: many sub-threshold steps
+            for t, j in enumerate(range(i % 64, i + 1, 64)):
+                k[:, j] = qn[:, i] * ((2.0 * t) * d ** 0.5 / 1.0)
+    q, k, v = (x.to(dtype).requires_grad_() for x in (q, k, v))
+    out = flash_attn_func(q, k, v, causal=causal)
+    g = torch.randn_like(out)
+    dq, dk, dv = torch.autograd.grad(out, (q, k, v), g)
+    assert torch.isfinite(out).all() and torch.isfinite(dq).all()
+    qc, kc, vc = _cpu_leaf(q, k, v)
+    out_ref, out_pt = _ref_and_pt(qc, kc, vc, causal=causal)
+    _assert_bound("out", out, out_ref, out_pt)
+    gc = g.to(REF_DEV)
+    gr = torch.autograd.grad(out_ref, (qc, kc, vc), gc)
+    gp = torch.autograd.grad(out_pt, (qc, kc, vc), gc)
+    for name, got, r, p in zip(("dq", "dk", "dv"), (dq, dk, dv), gr, gp):
+        _assert_bound(name, got, r, p)

@@ -18,12 +18,15 @@
 //   * O^T = V^T . P^T: the S^T accumulator, converted to bf16/f16 in registers, is directly the B
 //     operand of the PV MFMA (no LDS round trip for P); V^T fragments come from the row-major V tile
 //     through ds_read_b64_tr_b16.  O^T keeps the query on the lane, so the online-softmax rescale is
-//     a per-lane scalar multiply, skipped (wave-uniformly, exactly) when no row max of the wave moved.
+//     a per-lane scalar multiply, deferred (wave-uniformly) until some row max of the wave grew by
+//     more than 2^8 (P <= 256 meanwhile; exact in the LSE since m_run is the offset actually used).
 //   * Software pipeline over the tiles that need no mask (all but the causal diagonal / the ragged
 //     last tile): one basic block per tile holds QK^T(n+1) (MFMA), the exp / sum / pack of tile n
 //     (VALU) and PV(n) (MFMA), so the matrix pipe has independent work while the softmax runs.
 //   * Every LDS address is one of four per-lane bases + an immediate (fa_common.h LdsBases).
 //   * Heaviest causal query blocks are dispatched first (blockIdx.y reversed) to shorten the tail.
+//   * Epilogue: v_permlane32_swap pairs column groups so each lane stores 16 bytes of its O row.
+//   * Waves 4-7 (the younger half of the workgroup) run at s_setprio 1 for the whole kernel.
 #include <stdexcept>
 #include <string>
 
@@ -36,6 +39,7 @@ constexpr int kFwdWaves = 8;
 constexpr int kFwdBM = 32 * kFwdWaves;
 constexpr int kFwdBN = 64;
 constexpr int kFwdBufs = 4;   // ring depth: tiles nb, nb+1 read while nb+2, nb+3 land
+constexpr float kFwdRescaleThr = 8.f;   // deferred-max threshold, log2 units (P <= 256)
 
 template <bool BF16, int D, bool CAUSAL>
 __global__ void __launch_bounds__(kFwdWaves * 64, 2) fwd_kernel(const FwdParams p) {
@@ -194,7 +198,9 @@ __global__ void __launch_bounds__(kFwdWaves * 64, 2) fwd_kernel(const FwdParams 
   // online-softmax update for a tile whose row max (incl. the other lane half) is mt
   auto rescale = [&](float mt) {
     const float m_new = fmaxf(m_run, mt);
-    if (__any(m_new != m_run)) {
+    // deferred max (T13): keep the running max while no row of the wave grew by more than
+    // kFwdRescaleThr (log2 units), so P <= 2^kFwdRescaleThr; the first finite tile always rescales
+    if (__any(m_run == kNegInf ? m_new != m_run : (mt - m_run) * c > kFwdRescaleThr)) {
       const float alpha = fast_exp2(m_run * c - ((m_new == kNegInf) ? 0.f : m_new * c));
       l_run *= alpha;
 #pragma unroll
@@ -236,6 +242,7 @@ __global__ void __launch_bounds__(kFwdWaves * 64, 2) fwd_kernel(const FwdParams 
     });
   };
 
+  if (wave >= NW / 2) __builtin_amdgcn_s_setprio(1);   // younger half: static priority (T5 static form)
   if (nblk > 0) issue(0);
   if (nblk > 1) issue(1);
   wait_vmem_all();   // Q fragments, tiles 0 and 1 (compiler-visible: no vmcnt waits inside the loops)
@@ -299,21 +306,27 @@ __global__ void __launch_bounds__(kFwdWaves * 64, 2) fwd_kernel(const FwdParams 
   const bool bad = (l_tot == 0.f) || (l_tot != l_tot);
   const float inv = bad ? 1.f : fast_rcp(l_tot);
   const float lse = bad ? __builtin_huge_valf() : m_run * s.scale + __logf(l_tot);
-  if (qi < sq) {
-    u16* orow = O + (int64_t)qi * p.o_row;
+  {
+    // 16-byte stores: v_permlane32_swap pairs column groups (u, u+1) so that lane half 0 holds
+    // columns 8u..8u+7 and half 1 columns 8u+8..8u+15 of its row (T21)
+    u16* orow = O + (int64_t)(qi < sq ? qi : 0) * p.o_row;
 #pragma unroll
     for (int dt = 0; dt < NP; ++dt)
 #pragma unroll
-      for (int u = 0; u < 4; ++u) {
-        const int d0 = dt * 32 + 8 * u + 4 * hh;
-        if (d0 < dlim) {
-          u32x2_t w;
-          w[0] = E::pack2(o[dt][4 * u + 0] * inv, o[dt][4 * u + 1] * inv);
-          w[1] = E::pack2(o[dt][4 * u + 2] * inv, o[dt][4 * u + 3] * inv);
-          *(u32x2_t*)(orow + d0) = w;
+      for (int u = 0; u < 4; u += 2) {
+        unsigned a0 = E::pack2(o[dt][4 * u + 0] * inv, o[dt][4 * u + 1] * inv);
+        unsigned a1 = E::pack2(o[dt][4 * u + 2] * inv, o[dt][4 * u + 3] * inv);
+        unsigned b0 = E::pack2(o[dt][4 * u + 4] * inv, o[dt][4 * u + 5] * inv);
+        unsigned b1 = E::pack2(o[dt][4 * u + 6] * inv, o[dt][4 * u + 7] * inv);
+        auto r0 = __builtin_amdgcn_permlane32_swap(a0, b0, false, false);
+        auto r1 = __builtin_amdgcn_permlane32_swap(a1, b1, false, false);
+        const int col = dt * 32 + 8 * u + 8 * hh;
+        if (qi < sq && col < dlim) {
+          u32x4_t w = {(unsigned)r0[0], (unsigned)r1[0], (unsigned)r0[1], (unsigned)r1[1]};
+          *(u32x4_t*)(orow + col) = w;
         }
       }
-    if (hh == 0) LSE[qi] = lse;
+    if (qi < sq && hh == 0) LSE[qi] = lse;
   }
 }
 
