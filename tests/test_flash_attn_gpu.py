@@ -100,7 +100,7 @@ SEQ_PAIRS = [(113, 203), (128, 217), (113, 211), (108, 256), (256, 512), (512, 2
 @pytest.mark.parametrize("dtype", DTYPES)
 @pytest.mark.parametrize("mha_type", ["mha", "mqa", "gqa"])
 @pytest.mark.parametrize("causal", [False, True])
-@pytest.mark.parametrize("d", [32, 40, 59, 64, 80, 96, 111, 128])
+@pytest.mark.parametrize("d", [32, 40, 59, 64, 80, 96, 111, 128, 160, 192, 224, 256])
 @pytest.mark.parametrize("seqlen_q,seqlen_k", SEQ_PAIRS)
 def test_flash_attn_output(seqlen_q, seqlen_k, d, causal, mha_type, dtype, kvpacked):
     from flash_attn import flash_attn_func, flash_attn_kvpacked_func
@@ -141,7 +141,7 @@ def test_flash_attn_output(seqlen_q, seqlen_k, d, causal, mha_type, dtype, kvpac
 # ------------------------------------------------------------------------------------------------
 @pytest.mark.parametrize("dtype", DTYPES)
 @pytest.mark.parametrize("causal", [False, True])
-@pytest.mark.parametrize("d", [32, 64, 80, 128])
+@pytest.mark.parametrize("d", [32, 64, 80, 128, 192, 256])
 @pytest.mark.parametrize("seqlen", [97, 128, 200, 257, 384, 1025])
 def test_flash_attn_qkvpacked(seqlen, d, causal, dtype):
     from flash_attn import flash_attn_qkvpacked_func
@@ -168,7 +168,7 @@ def test_flash_attn_qkvpacked(seqlen, d, causal, dtype):
 @pytest.mark.parametrize("dtype", DTYPES)
 @pytest.mark.parametrize("mha_type", ["mha", "mqa", "gqa"])
 @pytest.mark.parametrize("causal", [False, True])
-@pytest.mark.parametrize("d", [32, 64, 96, 128])
+@pytest.mark.parametrize("d", [32, 64, 96, 128, 160, 256])
 @pytest.mark.parametrize("seqlen_q,seqlen_k", [(113, 203), (128, 217), (256, 512), (512, 256), (1023, 1024)])
 def test_flash_attn_varlen_output(seqlen_q, seqlen_k, d, causal, mha_type, dtype, kvpacked):
     from flash_attn import flash_attn_varlen_func, flash_attn_varlen_kvpacked_func
@@ -218,7 +218,7 @@ def test_flash_attn_varlen_output(seqlen_q, seqlen_k, d, causal, mha_type, dtype
 # ------------------------------------------------------------------------------------------------
 @pytest.mark.parametrize("dtype", DTYPES)
 @pytest.mark.parametrize("causal", [False, True])
-@pytest.mark.parametrize("d", [32, 64, 96, 128])
+@pytest.mark.parametrize("d", [32, 64, 96, 128, 256])
 def test_flash_attn_race_condition(d, causal, dtype):
     from flash_attn import flash_attn_qkvpacked_func
 

@@ -37,12 +37,22 @@ namespace fa {
 
 typedef unsigned short u16;
 
-constexpr int kDkdvWaves = 8;             // 4 P waves + 4 dS waves
-constexpr int kDkdvBN = 128;              // keys per dK/dV workgroup (32 per key group)
-constexpr int kDkdvBQ = 64;               // query rows per sweep step
-constexpr int kDqWaves = 8;
-constexpr int kDqBM = 32 * kDqWaves;      // query rows per dQ workgroup
-constexpr int kDqBN = 64;                 // keys per streamed K/V tile
+// Tile shapes per head dim.  d <= 128: two waves per SIMD.  d in (128, 256]: the D x 32
+// accumulators and the 32-key operand set need more than 256 registers per wave, so workgroups
+// are 4 waves (one per SIMD, 512 registers) and the LDS tiles shrink to fit.
+template <int D> struct DkdvTile {
+  static constexpr int NW = D <= 128 ? 8 : 4;      // NW/2 "P" waves + NW/2 "dS" waves
+  static constexpr int NKG = NW / 2;               // 32-key groups per workgroup
+  static constexpr int BN = 32 * NKG;              // keys per workgroup
+  static constexpr int BQ = D <= 128 ? 64 : 32;    // query rows per sweep step (32-row q-tiles)
+};
+template <int D> struct DqTile {
+  static constexpr int NW = D <= 128 ? 8 : 4;
+  static constexpr int BM = 32 * NW;               // query rows per dQ workgroup
+  static constexpr int BN = D <= 128 ? 64 : 32;    // keys per streamed K/V tile
+  static constexpr int MINB = D <= 128 ? 2 : 1;
+};
+constexpr int kDqMinBM = 128;                      // smallest dQ query block (grid-size check)
 constexpr int kBwdBufs = 3;
 
 // ------------------------------------------------------------------------------------------------
@@ -149,29 +159,32 @@ __global__ void __launch_bounds__(256) bwd_pre_kernel(const BwdParams p) {
 // flight), dO only in step it (2-deep ring), P(it) in steps it and it+1 (2 buffers).
 // Each wave needs one 32-key operand set and one D x 32 accumulator set (<= 256 registers).
 template <bool BF16, int D, bool CAUSAL>
-__global__ void __launch_bounds__(kDkdvWaves * 64, 1) bwd_dkdv_kernel(const BwdParams p) {
+__global__ void __launch_bounds__(DkdvTile<D>::NW * 64, 1) bwd_dkdv_kernel(const BwdParams p) {
   using E = Elt<BF16>;
-  constexpr int NW = kDkdvWaves;
-  constexpr int BQ = kDkdvBQ;
+  constexpr int NW = DkdvTile<D>::NW;
+  constexpr int NKG = DkdvTile<D>::NKG;
+  constexpr int BKN = DkdvTile<D>::BN;
+  constexpr int BQ = DkdvTile<D>::BQ;
+  constexpr int NQT = BQ / 32;                      // 32-row q-tiles per slice
   constexpr int KS = D / 16;
   constexpr int NP = D / 32;
   constexpr int QTILE = BQ * D * 2;                 // bytes of a Q or dO slice
-  constexpr int QSLOT = QTILE + 2 * BQ * 4;         // Q | lse[BQ] | D[BQ]
+  constexpr int QSLOT = QTILE + 2 * 64 * 4;         // Q | lse[64] | D[64] (one dword per lane)
   constexpr int OBASE = 3 * QSLOT;                  // dO ring (2 slots)
   constexpr int XTILE = 32 * 32 * 4;                // one fp32 32x32 P tile
-  constexpr int XBUF = 4 * 2 * XTILE;               // P of one slice: 4 key groups x 2 q-tiles
+  constexpr int XBUF = NKG * NQT * XTILE;           // P of one slice: key groups x q-tiles
   constexpr int XBASE = OBASE + 2 * QTILE;
   constexpr int PIECES = QTILE / 1024;
   constexpr int PPW = (PIECES + NW - 1) / NW;
   static_assert(QTILE % 1024 == 0, "slice must be whole DMA pieces");
-  static_assert(BQ == 64 && NW == 8, "two 32-row q-tiles per slice, 4 key groups x 2 roles");
+  static_assert(BQ % 32 == 0 && NW % 2 == 0, "32-row q-tiles, two roles");
   __shared__ __attribute__((aligned(16))) char smem[XBASE + 2 * XBUF];
 
   const AttnShape s = p.s;
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = wave_uniform(tid >> 6);
-  const bool pwave = wave < 4;
-  const int kg = wave & 3;
+  const bool pwave = wave < NKG;
+  const int kg = wave % NKG;
   const int r = lane & 31, hh = lane >> 5;
   const LdsBases lb(lane);
   const int group = s.h / s.hk;
@@ -184,7 +197,7 @@ __global__ void __launch_bounds__(kDkdvWaves * 64, 1) bwd_dkdv_kernel(const BwdP
   const int nh = p.gqa_reduce ? group : 1;
   const SeqGeom geo = seq_geom(p, bidb);
   const int sq = geo.sq, sk = geo.sk;
-  const int n0 = blockIdx.y * kDkdvBN;
+  const int n0 = blockIdx.y * BKN;
   if (n0 >= sk) return;
   const int dlim = s.d;
 
@@ -235,10 +248,11 @@ __global__ void __launch_bounds__(kDkdvWaves * 64, 1) bwd_dkdv_kernel(const BwdP
         dma16(ro, odst + pc * 1024, voff_o[j]);
       }
     }
-    if (wave < 2) {   // wave 0: LSE rows, wave 1: D rows (64 x 4 bytes each)
+    if (wave < 2) {   // wave 0: -LSE/scale rows, wave 1: D rows (64 x 4 bytes each; rows past
+                      // the slice land in the slot's padding or are never read)
       const int64_t bhi = (int64_t)bidb * s.h + hq;
       const float* src = ((wave == 0) ? p.lse_s : p.dsum) + bhi * p.seqlen_q_rounded + q0;
-      dma4(make_rsrc(src, rec_bytes(sq - q0, 1, 4)), qdst + QTILE + wave * BQ * 4, lane * 4);
+      dma4(make_rsrc(src, rec_bytes(sq - q0, 1, 4)), qdst + QTILE + wave * 64 * 4, lane * 4);
     }
   };
 
@@ -253,56 +267,54 @@ __global__ void __launch_bounds__(kDkdvWaves * 64, 1) bwd_dkdv_kernel(const BwdP
 
   // phase 1: S = Q K^T (P waves) / dP'' = D - dO V^T (dS waves) for both 32-row q-tiles of the
   // slice at `a1` (query on registers, key on lane), chains started from `init`
-  auto phase1 = [&](int a1, f32x16_t (&sp)[2]) {
+  auto phase1 = [&](int a1, f32x16_t (&sp)[NQT]) {
     const TileAddr ta(lb, a1);
-    constexpr int G = KS >= 4 ? KS / 2 : KS;   // A fragments in flight per group (register budget)
+    constexpr int G = KS >= 4 ? (NQT == 2 ? KS / 2 : KS / 4) : KS;   // A fragments in flight per group
     static_for<0, KS / G>([&](auto GG) {
       constexpr int g0 = decltype(GG)::value * G;
-      i16x8_t af0[G], af1[G];
+      i16x8_t af[NQT][G];
       static_for<0, G>([&](auto KK) {
         constexpr int ks = g0 + decltype(KK)::value;
-        af0[ks - g0] = row_read_c<BQ, 0, 2 * ks>(smem, ta);
-        af1[ks - g0] = row_read_c<BQ, 32, 2 * ks>(smem, ta);
+        static_for<0, NQT>([&](auto QT) {
+          constexpr int qt = decltype(QT)::value;
+          af[qt][ks - g0] = row_read_c<BQ, 32 * qt, 2 * ks>(smem, ta);
+        });
       });
 #pragma unroll
-      for (int k = 0; k < G; ++k) {
-        sp[0] = E::mfma(af0[k], kv[g0 + k], sp[0]);
-        sp[1] = E::mfma(af1[k], kv[g0 + k], sp[1]);
-      }
+      for (int k = 0; k < G; ++k)
+#pragma unroll
+        for (int qt = 0; qt < NQT; ++qt) sp[qt] = E::mfma(af[qt][k], kv[g0 + k], sp[qt]);
     });
   };
   // phase 2: acc += A^T frag, transposed A operand of the slice tile at `a2`; the fragments of
   // d-group dt+1 are requested before the MFMAs of group dt
-  auto phase2 = [&](int a2, const i16x8_t (&fr)[4]) {
+  auto phase2 = [&](int a2, const i16x8_t (&fr)[2 * NQT]) {
     const TileAddr ta2(lb, a2);
-    i16x8_t tf[2][4];
-    auto tr_group = [&](auto DTC, i16x8_t (&t)[4]) {
+    i16x8_t tf[2][2 * NQT];
+    auto tr_group = [&](auto DTC, i16x8_t (&t)[2 * NQT]) {
       constexpr int dt = decltype(DTC)::value;
-      t[0] = tr_frag_c<BQ, 0, dt>(smem, ta2);
-      t[1] = tr_frag_c<BQ, 16, dt>(smem, ta2);
-      t[2] = tr_frag_c<BQ, 32, dt>(smem, ta2);
-      t[3] = tr_frag_c<BQ, 48, dt>(smem, ta2);
+      static_for<0, 2 * NQT>([&](auto KC) {
+        constexpr int kk = decltype(KC)::value;
+        t[kk] = tr_frag_c<BQ, 16 * kk, dt>(smem, ta2);
+      });
     };
     tr_group(std::integral_constant<int, 0>{}, tf[0]);
     static_for<0, NP>([&](auto DTC) {
       constexpr int dt = decltype(DTC)::value;
       if constexpr (dt + 1 < NP) tr_group(std::integral_constant<int, dt + 1>{}, tf[(dt + 1) & 1]);
       __builtin_amdgcn_sched_barrier(0);
-      acc[dt] = E::mfma(tf[dt & 1][0], fr[0], acc[dt]);
-      acc[dt] = E::mfma(tf[dt & 1][1], fr[1], acc[dt]);
-      acc[dt] = E::mfma(tf[dt & 1][2], fr[2], acc[dt]);
-      acc[dt] = E::mfma(tf[dt & 1][3], fr[3], acc[dt]);
+#pragma unroll
+      for (int kk = 0; kk < 2 * NQT; ++kk) acc[dt] = E::mfma(tf[dt & 1][kk], fr[kk], acc[dt]);
       __builtin_amdgcn_sched_barrier(0);
     });
   };
 
-  // P = exp2(c S - LSE log2e) for both q-tiles into `xw` (this key group's P tiles), packed to `fr`
   // P = exp2(c S') with S' = S - LSE / scale (the chain started from -LSE / scale) for both q-tiles
   // into `xw` (this key group's P tiles), packed to `fr`
-  auto p_step = [&](auto MASKC, f32x16_t (&sp)[2], int q0, char* xw, i16x8_t (&fr)[4]) {
+  auto p_step = [&](auto MASKC, f32x16_t (&sp)[NQT], int q0, char* xw, i16x8_t (&fr)[2 * NQT]) {
     constexpr bool MASK = decltype(MASKC)::value;
 #pragma unroll
-    for (int qi = 0; qi < 2; ++qi) {
+    for (int qi = 0; qi < NQT; ++qi) {
 #pragma unroll
       for (int u = 0; u < 4; ++u) {
         f32x4_t pv;
@@ -323,9 +335,9 @@ __global__ void __launch_bounds__(kDkdvWaves * 64, 1) bwd_dkdv_kernel(const BwdP
     }
   };
   // dS'' = P o dP'' of the slice whose P tiles are at `xw`, packed to `fr`
-  auto ds_step = [&](const f32x16_t (&sp)[2], const char* xw, i16x8_t (&fr)[4]) {
+  auto ds_step = [&](const f32x16_t (&sp)[NQT], const char* xw, i16x8_t (&fr)[2 * NQT]) {
 #pragma unroll
-    for (int qi = 0; qi < 2; ++qi) {
+    for (int qi = 0; qi < NQT; ++qi) {
       f32x16_t x;
 #pragma unroll
       for (int u = 0; u < 4; ++u) {
@@ -337,7 +349,7 @@ __global__ void __launch_bounds__(kDkdvWaves * 64, 1) bwd_dkdv_kernel(const BwdP
       fr[2 * qi + 1] = pack_frag<BF16>(x, 1);
     }
   };
-  auto xw_of = [&](int it) { return smem + XBASE + (it & 1) * XBUF + kg * 2 * XTILE + lane * 16; };
+  auto xw_of = [&](int it) { return smem + XBASE + (it & 1) * XBUF + kg * NQT * XTILE + lane * 16; };
 
   if (total > 0) issue(0);
   wait_vmem_all();   // K/V fragments and slice 0 (compiler-visible: no vmcnt waits inside the loop)
@@ -347,19 +359,19 @@ __global__ void __launch_bounds__(kDkdvWaves * 64, 1) bwd_dkdv_kernel(const BwdP
   // register assignment of `sp` / `acc` is shared and no accumulator copies appear at the joins):
   //   dS waves: dS''(it-1) from sp (VALU) | sp = dP''(it) (MFMA) |                 | dK'' += Q(it-1)^T dS''
   //   P waves:                            | sp = S(it)     (MFMA) | P(it) (VALU)    | dV   += dO(it)^T P
-  f32x16_t sp[2];    // S of this slice (P waves) / dP'' of the previous slice (dS waves)
+  f32x16_t sp[NQT];  // S of this slice (P waves) / dP'' of the previous slice (dS waves)
   for (int it = 0; it < total; ++it) {
     if (it + 1 < total) issue(it + 1);
     const int q0 = (m_first + it % ns) * BQ;
     const int qs = (it % 3) * QSLOT;
     const float* lt = (const float*)(smem + qs + QTILE);
     const int os = OBASE + (it & 1) * QTILE;
-    i16x8_t fr[4];
+    i16x8_t fr[2 * NQT];
     if (!pwave && it > 0) ds_step(sp, xw_of(it - 1), fr);
     // chain start: -LSE / scale (P waves) or D (dS waves), per accumulator row
-    const float* init = lt + (pwave ? 0 : BQ);
+    const float* init = lt + (pwave ? 0 : 64);
 #pragma unroll
-    for (int qi = 0; qi < 2; ++qi)
+    for (int qi = 0; qi < NQT; ++qi)
 #pragma unroll
       for (int u = 0; u < 4; ++u) {
         const f32x4_t iv = *(const f32x4_t*)(init + 32 * qi + 8 * u + 4 * hh);
@@ -368,7 +380,7 @@ __global__ void __launch_bounds__(kDkdvWaves * 64, 1) bwd_dkdv_kernel(const BwdP
       }
     phase1(pwave ? qs : os, sp);                       // S' = Q K^T - LSE/scale  /  dP'' = D - dO V^T
     if (pwave) {
-      const bool fast = (q0 + BQ <= sq) && (n0 + kDkdvBN <= sk) && (!CAUSAL || q0 >= n0 + kDkdvBN - 1);
+      const bool fast = (q0 + BQ <= sq) && (n0 + BKN <= sk) && (!CAUSAL || q0 >= n0 + BKN - 1);
       if (fast) p_step(std::false_type{}, sp, q0, xw_of(it), fr);
       else p_step(std::true_type{}, sp, q0, xw_of(it), fr);
     }
@@ -376,7 +388,7 @@ __global__ void __launch_bounds__(kDkdvWaves * 64, 1) bwd_dkdv_kernel(const BwdP
     wait_dma_keep_and_barrier(0);
   }
   if (!pwave && total > 0) {   // the last slice's dK update (no DMA after it: its Q is resident)
-    i16x8_t fr[4];
+    i16x8_t fr[2 * NQT];
     ds_step(sp, xw_of(total - 1), fr);
     phase2(((total - 1) % 3) * QSLOT, fr);
   }
@@ -406,11 +418,11 @@ __global__ void __launch_bounds__(kDkdvWaves * 64, 1) bwd_dkdv_kernel(const BwdP
 // 3. dQ  (forward-shaped: query on the lane, K/V streamed)
 // ------------------------------------------------------------------------------------------------
 template <bool BF16, int D, bool CAUSAL>
-__global__ void __launch_bounds__(kDqWaves * 64, 2) bwd_dq_kernel(const BwdParams p) {
+__global__ void __launch_bounds__(DqTile<D>::NW * 64, DqTile<D>::MINB) bwd_dq_kernel(const BwdParams p) {
   using E = Elt<BF16>;
-  constexpr int NW = kDqWaves;
-  constexpr int BN = kDqBN;
-  constexpr int BM = kDqBM;
+  constexpr int NW = DqTile<D>::NW;
+  constexpr int BN = DqTile<D>::BN;
+  constexpr int BM = DqTile<D>::BM;
   constexpr int KS = D / 16;
   constexpr int NT = BN / 32;
   constexpr int NP = D / 32;
@@ -595,13 +607,13 @@ static void run_bwd(const BwdParams& p, hipStream_t stream) {
   {
     dim3 grid(p.s.b * nheads_grid, p.num_n_blocks);
     prof_begin(kTimeBwdMain, stream);
-    hipLaunchKernelGGL((bwd_dkdv_kernel<BF16, D, CAUSAL>), grid, dim3(kDkdvWaves * 64), 0, stream, p);
+    hipLaunchKernelGGL((bwd_dkdv_kernel<BF16, D, CAUSAL>), grid, dim3(DkdvTile<D>::NW * 64), 0, stream, p);
     prof_end(kTimeBwdMain, stream);
   }
   {
-    dim3 grid(p.s.b * p.s.h, (p.s.seqlen_q + kDqBM - 1) / kDqBM);
+    dim3 grid(p.s.b * p.s.h, (p.s.seqlen_q + DqTile<D>::BM - 1) / DqTile<D>::BM);
     prof_begin(kTimeBwdDq, stream);
-    hipLaunchKernelGGL((bwd_dq_kernel<BF16, D, CAUSAL>), grid, dim3(kDqWaves * 64), 0, stream, p);
+    hipLaunchKernelGGL((bwd_dq_kernel<BF16, D, CAUSAL>), grid, dim3(DqTile<D>::NW * 64), 0, stream, p);
     prof_end(kTimeBwdDq, stream);
   }
 }
@@ -613,13 +625,14 @@ static void dispatch_bwd_d(const BwdParams& p, hipStream_t stream) {
   else if (d <= 64) run_bwd<BF16, 64, CAUSAL>(p, stream);
   else if (d <= 96) run_bwd<BF16, 96, CAUSAL>(p, stream);
   else if (d <= 128) run_bwd<BF16, 128, CAUSAL>(p, stream);
-  else throw std::runtime_error("flash_attn_bwd: head dim " + std::to_string(d) + " > 128 not built yet");
+  else if (d <= 192) run_bwd<BF16, 192, CAUSAL>(p, stream);
+  else if (d <= 256) run_bwd<BF16, 256, CAUSAL>(p, stream);
+  else throw std::runtime_error("flash_attn_bwd: head dim " + std::to_string(d) + " > 256");
 }
 
 void bwd_block_size(int d, int* block_m, int* block_n) {
-  *block_m = kDkdvBQ;
-  *block_n = kDkdvBN;
-  (void)d;
+  *block_m = d <= 128 ? DkdvTile<128>::BQ : DkdvTile<256>::BQ;
+  *block_n = d <= 128 ? DkdvTile<128>::BN : DkdvTile<256>::BN;
 }
 
 template <bool BF16>
@@ -636,7 +649,7 @@ static void launch_bwd_t(const BwdParams& p, hipStream_t stream) {
 
 void launch_bwd(const BwdParams& p_in, bool is_bf16, hipStream_t stream) {
   if (p_in.s.b <= 0 || p_in.s.h <= 0 || p_in.s.seqlen_q <= 0) return;
-  if ((p_in.s.seqlen_q + kDqBM - 1) / kDqBM > 65535 || (p_in.s.seqlen_q + 15) / 16 > 65535)
+  if ((p_in.s.seqlen_q + kDqMinBM - 1) / kDqMinBM > 65535 || (p_in.s.seqlen_q + 15) / 16 > 65535)
     throw std::runtime_error("flash_attn_bwd: seqlen_q too large for the grid");
   BwdParams p = p_in;
   // softmax_scale == 0 (uniform attention) would make -LSE / scale infinite: a tiny positive scale

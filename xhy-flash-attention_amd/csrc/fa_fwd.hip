@@ -6,7 +6,8 @@
 // flash_fwd_kernel.h:509-518); causal mask is top-left aligned (key <= query, softmax.h:143-178).
 //
 // MI355X mapping (not a translation of the CUDA tiling):
-//   * 8 waves x 32 query rows = 256-row query block per workgroup; BN = 64 keys per K/V tile.
+//   * 8 waves x 32 query rows = 256-row query block per workgroup; BN = 64 keys per K/V tile
+//     (d > 128: 4 waves, one per SIMD, and 32-key tiles -- FwdTile).
 //   * K/V tiles arrive by LDS-DMA (buffer_load ... lds, one 1-KiB piece per wave instruction) three
 //     tiles ahead into a 4-deep LDS ring; the buffer descriptor's range check zero-fills rows past
 //     seqlen_k and padded head-dim columns, so the kernel never branches on the load side.  One
@@ -35,18 +36,25 @@
 
 namespace fa {
 
-constexpr int kFwdWaves = 8;
-constexpr int kFwdBM = 32 * kFwdWaves;
-constexpr int kFwdBN = 64;
+// Tile shape per head dim.  d <= 128: 8 waves x 32 rows, 64-key tiles, two waves per SIMD.
+// d in (128, 256]: the O accumulator (D/2 registers) and the Q fragments (D/4) no longer fit two
+// waves per SIMD next to the scores, so a workgroup is 4 waves (one per SIMD, 512 registers each)
+// and K/V tiles are 32 keys (the 4-deep ring stays at 4 x 2 x 16 KiB at d = 256).
+template <int D> struct FwdTile {
+  static constexpr int NW = D <= 128 ? 8 : 4;
+  static constexpr int BM = 32 * NW;
+  static constexpr int BN = D <= 128 ? 64 : 32;
+  static constexpr int MINB = D <= 128 ? 2 : 1;   // __launch_bounds__ blocks per CU (register budget)
+};
 constexpr int kFwdBufs = 4;   // ring depth: tiles nb, nb+1 read while nb+2, nb+3 land
 constexpr float kFwdRescaleThr = 8.f;   // deferred-max threshold, log2 units (P <= 256)
 
 template <bool BF16, int D, bool CAUSAL>
-__global__ void __launch_bounds__(kFwdWaves * 64, 2) fwd_kernel(const FwdParams p) {
+__global__ void __launch_bounds__(FwdTile<D>::NW * 64, FwdTile<D>::MINB) fwd_kernel(const FwdParams p) {
   using E = Elt<BF16>;
-  constexpr int NW = kFwdWaves;
-  constexpr int BN = kFwdBN;
-  constexpr int BM = kFwdBM;
+  constexpr int NW = FwdTile<D>::NW;
+  constexpr int BN = FwdTile<D>::BN;
+  constexpr int BM = FwdTile<D>::BM;
   constexpr int KS = D / 16;            // QK^T k-steps (16 along d)
   constexpr int NT = BN / 32;           // 32-key subtiles per K/V tile
   constexpr int NP = D / 32;            // 32-wide d panels == PV output tiles
@@ -334,7 +342,7 @@ template <bool BF16, int D, bool CAUSAL>
 static void run_fwd(const FwdParams& p, hipStream_t stream) {
   dim3 grid(p.s.b * p.s.h, p.num_m_blocks);
   prof_begin(kTimeFwd, stream);
-  hipLaunchKernelGGL((fwd_kernel<BF16, D, CAUSAL>), grid, dim3(kFwdWaves * 64), 0, stream, p);
+  hipLaunchKernelGGL((fwd_kernel<BF16, D, CAUSAL>), grid, dim3(FwdTile<D>::NW * 64), 0, stream, p);
   prof_end(kTimeFwd, stream);
 }
 
@@ -345,13 +353,14 @@ static void dispatch_d(const FwdParams& p, hipStream_t stream) {
   else if (d <= 64) run_fwd<BF16, 64, CAUSAL>(p, stream);
   else if (d <= 96) run_fwd<BF16, 96, CAUSAL>(p, stream);
   else if (d <= 128) run_fwd<BF16, 128, CAUSAL>(p, stream);
-  else throw std::runtime_error("flash_attn_fwd: head dim " + std::to_string(d) + " > 128 not built yet");
+  else if (d <= 192) run_fwd<BF16, 192, CAUSAL>(p, stream);
+  else if (d <= 256) run_fwd<BF16, 256, CAUSAL>(p, stream);
+  else throw std::runtime_error("flash_attn_fwd: head dim " + std::to_string(d) + " > 256");
 }
 
 void fwd_block_size(int d, int* block_m, int* block_n) {
-  *block_m = kFwdBM;
-  *block_n = kFwdBN;
-  (void)d;
+  *block_m = d <= 128 ? FwdTile<128>::BM : FwdTile<256>::BM;
+  *block_n = d <= 128 ? FwdTile<128>::BN : FwdTile<256>::BN;
 }
 
 void launch_fwd(const FwdParams& p, bool is_bf16, hipStream_t stream) {
