@@ -344,14 +344,23 @@ def test_capi_expanded_gqa_matches_fused_reduction():
     torch.testing.assert_close(dv_sum, dv.float(), atol=3e-2, rtol=2e-2)
 
 
-def test_capi_rejects_dropout_and_masks():
+def test_return_softmax_requires_dropout_and_masks_rejected():
+    """Reference mha_fwd: return_softmax only with p_dropout > 0 (flash_api.cpp:276-279); the
+    Paddle dense mask / FlashMask arguments of the C ABI are out of scope and rejected loudly."""
     import flash_attn_2_cuda as m
-    from flash_attn import flash_attn_func
 
     q = torch.randn(1, 64, 2, 64, device=DEV, dtype=torch.float16)
-    with pytest.raises(RuntimeError, match="dropout"):
-        flash_attn_func(q, q, q, dropout_p=0.1)
-    assert m._lib.flash_attn_error()
+    with pytest.raises(RuntimeError, match="return_softmax"):
+        m.fwd(q, q, q, None, 0.0, 0.125, False, True, None)
+    lse = torch.empty(1, 2, 64, device=DEV)
+    out = torch.empty_like(q)
+    st = (q.stride(1), q.stride(1), q.stride(1), q.stride(2), q.stride(2), q.stride(2), out.stride(1),
+          out.stride(2), q.stride(0), q.stride(0), q.stride(0), out.stride(0))
+    ok = m._lib.flash_attn_fwd(m._ptr(q), m._ptr(q), m._ptr(q), None, m._ptr(out), None, m._ptr(lse),
+                               1, 64, 64, 128, 128, 2, 2, 64, 64, 0.0, 0.125, 1.0, False, False, False,
+                               m._stream(q), 0, 0, m._ptr(lse), None, None, None, None, None, None,
+                               None, *st)
+    assert not ok and b"attn_mask" in m._lib.flash_attn_error()
 
 
 # ------------------------------------------------------------------------------------------------

@@ -31,6 +31,7 @@
 #include <string>
 
 #include "fa_common.h"
+#include "fa_dropout.h"
 #include "fa_params.h"
 
 namespace fa {
@@ -134,7 +135,8 @@ __global__ void __launch_bounds__(256) bwd_pre_kernel(const BwdParams p) {
   for (int m = 8; m >= 1; m >>= 1) acc += __shfl_xor(acc, m, 16);
   if (l16 == 0) {
     const int64_t bhi = (int64_t)bidb * s.h + head;
-    p.dsum[bhi * p.seqlen_q_rounded + row] = acc;
+    // with dropout the reference keeps D scaled down by the keep probability (flash_bwd_kernel.h:178-182)
+    p.dsum[bhi * p.seqlen_q_rounded + row] = s.dropout ? acc * s.p_keep : acc;
     // -LSE / scale: the initial accumulator of the dK/dV kernel's S chain (scale != 0: launch_bwd)
     p.lse_s[bhi * p.seqlen_q_rounded + row] = -p.lse[bhi * s.lse_pitch + row] / s.scale;
   }
@@ -158,7 +160,7 @@ __global__ void __launch_bounds__(256) bwd_pre_kernel(const BwdParams p) {
 // Slice lifetimes: Q (+ LSE, D) is read in steps it and it+1 (3-deep ring, one slice of DMA in
 // flight), dO only in step it (2-deep ring), P(it) in steps it and it+1 (2 buffers).
 // Each wave needs one 32-key operand set and one D x 32 accumulator set (<= 256 registers).
-template <bool BF16, int D, bool CAUSAL>
+template <bool BF16, int D, bool CAUSAL, bool DROPOUT>
 __global__ void __launch_bounds__(DkdvTile<D>::NW * 64, 1) bwd_dkdv_kernel(const BwdParams p) {
   using E = Elt<BF16>;
   constexpr int NW = DkdvTile<D>::NW;
@@ -178,7 +180,8 @@ __global__ void __launch_bounds__(DkdvTile<D>::NW * 64, 1) bwd_dkdv_kernel(const
   constexpr int PPW = (PIECES + NW - 1) / NW;
   static_assert(QTILE % 1024 == 0, "slice must be whole DMA pieces");
   static_assert(BQ % 32 == 0 && NW % 2 == 0, "32-row q-tiles, two roles");
-  __shared__ __attribute__((aligned(16))) char smem[XBASE + 2 * XBUF];
+  // ... then (dropout) one 1-KiB random-byte scratch per P wave
+  __shared__ __attribute__((aligned(16))) char smem[XBASE + 2 * XBUF + (DROPOUT ? NKG * 1024 : 0)];
 
   const AttnShape s = p.s;
   const int tid = threadIdx.x, lane = tid & 63;
@@ -311,10 +314,21 @@ __global__ void __launch_bounds__(DkdvTile<D>::NW * 64, 1) bwd_dkdv_kernel(const
 
   // P = exp2(c S') with S' = S - LSE / scale (the chain started from -LSE / scale) for both q-tiles
   // into `xw` (this key group's P tiles), packed to `fr`
-  auto p_step = [&](auto MASKC, f32x16_t (&sp)[NQT], int q0, char* xw, i16x8_t (&fr)[2 * NQT]) {
+  // With dropout the LDS tile carries P sign-encoded (negative where dropped, reference
+  // apply_dropout<encode_dropout_in_sign_bit=true>, flash_bwd_kernel.h:848-857) and the packed
+  // operand of dV^T carries P o Z (zeros where dropped).
+  char* const dscr = smem + XBASE + 2 * XBUF + kg * 1024;
+  auto p_step = [&](auto MASKC, f32x16_t (&sp)[NQT], int q0, int it_head, char* xw, i16x8_t (&fr)[2 * NQT]) {
     constexpr bool MASK = decltype(MASKC)::value;
 #pragma unroll
     for (int qi = 0; qi < NQT; ++qi) {
+      unsigned rb[4];
+      if constexpr (DROPOUT) {
+        const uint64_t doff = s.philox_offset + (uint64_t)(bidb * s.h + h_begin + it_head) * 32;
+        dropout_block_bytes<true>(dscr, s.philox_seed, doff, q0 + 32 * qi, kw0, lane);
+#pragma unroll
+        for (int u = 0; u < 4; ++u) rb[u] = dropout_group_bytes(dscr, r, hh, u);
+      }
 #pragma unroll
       for (int u = 0; u < 4; ++u) {
         f32x4_t pv;
@@ -325,8 +339,14 @@ __global__ void __launch_bounds__(DkdvTile<D>::NW * 64, 1) bwd_dkdv_kernel(const
             const int q = q0 + 32 * qi + 8 * u + 4 * hh + j;
             x = (key >= sk || q >= sq || (CAUSAL && key > q)) ? 0.f : x;
           }
-          pv[j] = x;
-          sp[qi][4 * u + j] = x;
+          if constexpr (DROPOUT) {
+            const bool keep = dropout_keep(rb[u], j, s.keep_u8);
+            pv[j] = keep ? x : -x;
+            sp[qi][4 * u + j] = keep ? x : 0.f;
+          } else {
+            pv[j] = x;
+            sp[qi][4 * u + j] = x;
+          }
         }
         *(f32x4_t*)(xw + qi * XTILE + u * 1024) = pv;
       }
@@ -335,15 +355,24 @@ __global__ void __launch_bounds__(DkdvTile<D>::NW * 64, 1) bwd_dkdv_kernel(const
     }
   };
   // dS'' = P o dP'' of the slice whose P tiles are at `xw`, packed to `fr`
-  auto ds_step = [&](const f32x16_t (&sp)[NQT], const char* xw, i16x8_t (&fr)[2 * NQT]) {
+  // (dropout: P'' = sign-encoded P;  dS'' = P o dP'' where kept, -P''... = P o D where dropped,
+  //  reference flash_bwd_kernel.h:897-899 with our dS'' = -dS, dP'' = D - dP)
+  auto ds_step = [&](const f32x16_t (&sp)[NQT], const char* xw, const float* dl, i16x8_t (&fr)[2 * NQT]) {
 #pragma unroll
     for (int qi = 0; qi < NQT; ++qi) {
       f32x16_t x;
 #pragma unroll
       for (int u = 0; u < 4; ++u) {
         const f32x4_t pv = *(const f32x4_t*)(xw + qi * XTILE + u * 1024);
+        if constexpr (DROPOUT) {
+          const f32x4_t dv = *(const f32x4_t*)(dl + 32 * qi + 8 * u + 4 * hh);
 #pragma unroll
-        for (int j = 0; j < 4; ++j) x[4 * u + j] = pv[j] * sp[qi][4 * u + j];
+          for (int j = 0; j < 4; ++j) x[4 * u + j] = pv[j] >= 0.f ? pv[j] * sp[qi][4 * u + j] : -pv[j] * dv[j];
+        } else {
+          (void)dl;
+#pragma unroll
+          for (int j = 0; j < 4; ++j) x[4 * u + j] = pv[j] * sp[qi][4 * u + j];
+        }
       }
       fr[2 * qi] = pack_frag<BF16>(x, 0);
       fr[2 * qi + 1] = pack_frag<BF16>(x, 1);
@@ -363,11 +392,13 @@ __global__ void __launch_bounds__(DkdvTile<D>::NW * 64, 1) bwd_dkdv_kernel(const
   for (int it = 0; it < total; ++it) {
     if (it + 1 < total) issue(it + 1);
     const int q0 = (m_first + it % ns) * BQ;
+    const int it_head = it / ns;   // query head of this slice within the group
     const int qs = (it % 3) * QSLOT;
     const float* lt = (const float*)(smem + qs + QTILE);
     const int os = OBASE + (it & 1) * QTILE;
     i16x8_t fr[2 * NQT];
-    if (!pwave && it > 0) ds_step(sp, xw_of(it - 1), fr);
+    if (!pwave && it > 0)
+      ds_step(sp, xw_of(it - 1), (const float*)(smem + ((it + 2) % 3) * QSLOT + QTILE) + 64, fr);
     // chain start: -LSE / scale (P waves) or D (dS waves), per accumulator row
     const float* init = lt + (pwave ? 0 : 64);
 #pragma unroll
@@ -381,15 +412,15 @@ __global__ void __launch_bounds__(DkdvTile<D>::NW * 64, 1) bwd_dkdv_kernel(const
     phase1(pwave ? qs : os, sp);                       // S' = Q K^T - LSE/scale  /  dP'' = D - dO V^T
     if (pwave) {
       const bool fast = (q0 + BQ <= sq) && (n0 + BKN <= sk) && (!CAUSAL || q0 >= n0 + BKN - 1);
-      if (fast) p_step(std::false_type{}, sp, q0, xw_of(it), fr);
-      else p_step(std::true_type{}, sp, q0, xw_of(it), fr);
+      if (fast) p_step(std::false_type{}, sp, q0, it_head, xw_of(it), fr);
+      else p_step(std::true_type{}, sp, q0, it_head, xw_of(it), fr);
     }
     if (pwave || it > 0) phase2(pwave ? os : ((it + 2) % 3) * QSLOT, fr);   // dV^T / dK''^T
     wait_dma_keep_and_barrier(0);
   }
   if (!pwave && total > 0) {   // the last slice's dK update (no DMA after it: its Q is resident)
     i16x8_t fr[2 * NQT];
-    ds_step(sp, xw_of(total - 1), fr);
+    ds_step(sp, xw_of(total - 1), (const float*)(smem + ((total - 1) % 3) * QSLOT + QTILE) + 64, fr);
     phase2(((total - 1) % 3) * QSLOT, fr);
   }
 
@@ -398,7 +429,8 @@ __global__ void __launch_bounds__(DkdvTile<D>::NW * 64, 1) bwd_dkdv_kernel(const
     const int hd = p.gqa_reduce ? kvh : hx;
     u16* row = pwave ? (u16*)p.dv + geo.dv_off + (int64_t)hd * p.dv_head + (int64_t)key * p.dv_row
                      : (u16*)p.dk + geo.dk_off + (int64_t)hd * p.dk_head + (int64_t)key * p.dk_row;
-    const float sc = pwave ? 1.f : -s.scale;
+    const float rp = DROPOUT ? s.rp_dropout : 1.f;
+    const float sc = pwave ? rp : -s.scale * rp;
 #pragma unroll
     for (int dt = 0; dt < NP; ++dt)
 #pragma unroll
@@ -417,7 +449,7 @@ __global__ void __launch_bounds__(DkdvTile<D>::NW * 64, 1) bwd_dkdv_kernel(const
 // ------------------------------------------------------------------------------------------------
 // 3. dQ  (forward-shaped: query on the lane, K/V streamed)
 // ------------------------------------------------------------------------------------------------
-template <bool BF16, int D, bool CAUSAL>
+template <bool BF16, int D, bool CAUSAL, bool DROPOUT>
 __global__ void __launch_bounds__(DqTile<D>::NW * 64, DqTile<D>::MINB) bwd_dq_kernel(const BwdParams p) {
   using E = Elt<BF16>;
   constexpr int NW = DqTile<D>::NW;
@@ -431,7 +463,8 @@ __global__ void __launch_bounds__(DqTile<D>::NW * 64, DqTile<D>::MINB) bwd_dq_ke
   constexpr int PPW = (PIECES + NW - 1) / NW;
   constexpr int KG = (KS % 4 == 0) ? 4 : ((KS % 3 == 0) ? 3 : 2);
   static_assert(TILE % 1024 == 0 && KS % KG == 0, "tile shape");
-  __shared__ __attribute__((aligned(16))) char smem[kBwdBufs * 2 * TILE];  // [buffer][K | V]
+  // [buffer][K | V], then (dropout) one 1-KiB random-byte scratch per wave
+  __shared__ __attribute__((aligned(16))) char smem[kBwdBufs * 2 * TILE + (DROPOUT ? NW * 1024 : 0)];
 
   const AttnShape s = p.s;
   const int tid = threadIdx.x, lane = tid & 63;
@@ -533,7 +566,15 @@ __global__ void __launch_bounds__(DqTile<D>::NW * 64, DqTile<D>::MINB) bwd_dq_ke
       });
     });
 #pragma unroll
-    for (int t = 0; t < NT; ++t)
+    for (int t = 0; t < NT; ++t) {
+      unsigned rb[4];
+      if constexpr (DROPOUT) {
+        char* dscr = smem + kBwdBufs * 2 * TILE + wave * 1024;
+        const uint64_t doff = s.philox_offset + (uint64_t)bhi * 32;
+        dropout_block_bytes<false>(dscr, s.philox_seed, doff, wq0, n0 + 32 * t, lane);
+#pragma unroll
+        for (int u = 0; u < 4; ++u) rb[u] = dropout_group_bytes(dscr, r, hh, u);
+      }
 #pragma unroll
       for (int g = 0; g < 16; ++g) {
         float pv = fast_exp2(fmaf(st[t][g], c, -lse_l2));
@@ -541,8 +582,13 @@ __global__ void __launch_bounds__(DqTile<D>::NW * 64, DqTile<D>::MINB) bwd_dq_ke
           const int kk = n0 + t * 32 + acc_row(g, hh);
           if (kk >= sk || (CAUSAL && kk > qi)) pv = 0.f;
         }
-        pt[t][g] = pv * pt[t][g];     // dS^T = P^T o (dP^T - D)
+        // dS^T = P^T o (dP^T - D); dropped elements: -P D (reference flash_bwd_kernel.h:897-899)
+        if constexpr (DROPOUT)
+          pt[t][g] = dropout_keep(rb[g >> 2], g & 3, s.keep_u8) ? pv * pt[t][g] : -pv * dsum_q;
+        else
+          pt[t][g] = pv * pt[t][g];
       }
+    }
     // dQ^T[d][q] += K^T[d][key] dS^T[key][q]
     i16x8_t df[2 * NT];
 #pragma unroll
@@ -584,7 +630,7 @@ __global__ void __launch_bounds__(DqTile<D>::NW * 64, DqTile<D>::MINB) bwd_dq_ke
 
   if (q_ok) {
     u16* drow = (u16*)p.dq + geo.dq_off + (int64_t)head * p.dq_head + (int64_t)qi * p.dq_row;
-    const float sc = s.scale;
+    const float sc = s.scale * (DROPOUT ? s.rp_dropout : 1.f);
 #pragma unroll
     for (int dt = 0; dt < NP; ++dt)
 #pragma unroll
@@ -601,32 +647,32 @@ __global__ void __launch_bounds__(DqTile<D>::NW * 64, DqTile<D>::MINB) bwd_dq_ke
 }
 
 // ------------------------------------------------------------------------------------------------
-template <bool BF16, int D, bool CAUSAL>
+template <bool BF16, int D, bool CAUSAL, bool DROPOUT>
 static void run_bwd(const BwdParams& p, hipStream_t stream) {
   const int nheads_grid = p.gqa_reduce ? p.s.hk : p.s.h;
   {
     dim3 grid(p.s.b * nheads_grid, p.num_n_blocks);
     prof_begin(kTimeBwdMain, stream);
-    hipLaunchKernelGGL((bwd_dkdv_kernel<BF16, D, CAUSAL>), grid, dim3(DkdvTile<D>::NW * 64), 0, stream, p);
+    hipLaunchKernelGGL((bwd_dkdv_kernel<BF16, D, CAUSAL, DROPOUT>), grid, dim3(DkdvTile<D>::NW * 64), 0, stream, p);
     prof_end(kTimeBwdMain, stream);
   }
   {
     dim3 grid(p.s.b * p.s.h, (p.s.seqlen_q + DqTile<D>::BM - 1) / DqTile<D>::BM);
     prof_begin(kTimeBwdDq, stream);
-    hipLaunchKernelGGL((bwd_dq_kernel<BF16, D, CAUSAL>), grid, dim3(DqTile<D>::NW * 64), 0, stream, p);
+    hipLaunchKernelGGL((bwd_dq_kernel<BF16, D, CAUSAL, DROPOUT>), grid, dim3(DqTile<D>::NW * 64), 0, stream, p);
     prof_end(kTimeBwdDq, stream);
   }
 }
 
-template <bool BF16, bool CAUSAL>
+template <bool BF16, bool CAUSAL, bool DROPOUT>
 static void dispatch_bwd_d(const BwdParams& p, hipStream_t stream) {
   const int d = p.s.d;
-  if (d <= 32) run_bwd<BF16, 32, CAUSAL>(p, stream);
-  else if (d <= 64) run_bwd<BF16, 64, CAUSAL>(p, stream);
-  else if (d <= 96) run_bwd<BF16, 96, CAUSAL>(p, stream);
-  else if (d <= 128) run_bwd<BF16, 128, CAUSAL>(p, stream);
-  else if (d <= 192) run_bwd<BF16, 192, CAUSAL>(p, stream);
-  else if (d <= 256) run_bwd<BF16, 256, CAUSAL>(p, stream);
+  if (d <= 32) run_bwd<BF16, 32, CAUSAL, DROPOUT>(p, stream);
+  else if (d <= 64) run_bwd<BF16, 64, CAUSAL, DROPOUT>(p, stream);
+  else if (d <= 96) run_bwd<BF16, 96, CAUSAL, DROPOUT>(p, stream);
+  else if (d <= 128) run_bwd<BF16, 128, CAUSAL, DROPOUT>(p, stream);
+  else if (d <= 192) run_bwd<BF16, 192, CAUSAL, DROPOUT>(p, stream);
+  else if (d <= 256) run_bwd<BF16, 256, CAUSAL, DROPOUT>(p, stream);
   else throw std::runtime_error("flash_attn_bwd: head dim " + std::to_string(d) + " > 256");
 }
 
@@ -644,7 +690,11 @@ static void launch_bwd_t(const BwdParams& p, hipStream_t stream) {
     hipLaunchKernelGGL((bwd_pre_kernel<BF16>), grid, dim3(256), 0, stream, p);
     prof_end(kTimeBwdPre, stream);
   }
-  if (p.s.causal) dispatch_bwd_d<BF16, true>(p, stream); else dispatch_bwd_d<BF16, false>(p, stream);
+  if (p.s.causal) {
+    if (p.s.dropout) dispatch_bwd_d<BF16, true, true>(p, stream); else dispatch_bwd_d<BF16, true, false>(p, stream);
+  } else {
+    if (p.s.dropout) dispatch_bwd_d<BF16, false, true>(p, stream); else dispatch_bwd_d<BF16, false, false>(p, stream);
+  }
 }
 
 void launch_bwd(const BwdParams& p_in, bool is_bf16, hipStream_t stream) {

@@ -72,24 +72,33 @@ void check_common(int batch_size, int num_heads, int num_heads_k, int head_size,
   FA_CHECK(head_size_rounded >= head_size);
   if (attn_mask != nullptr) throw std::runtime_error("attn_mask (dense Paddle mask) is not supported by the MI355X build");
   if (flashmask != nullptr) throw std::runtime_error("FlashMask is not supported by the MI355X build");
-  if (p_dropout > 0.f) throw std::runtime_error("dropout is not implemented in the MI355X build yet (p_dropout must be 0)");
-  FA_CHECK(p_dropout < 1.f);
+  FA_CHECK(p_dropout >= 0.f && p_dropout < 1.f);
 }
 
 fa::AttnShape make_shape(int b, int h, int hk, int sq, int sk, int d, float scale, bool causal,
-                         const int* cu_q, const int* cu_k, bool padded) {
+                         const int* cu_q, const int* cu_k, bool padded, float p_dropout,
+                         uint64_t seed, uint64_t offset) {
   fa::AttnShape s;
+  std::memset(&s, 0, sizeof(s));
   s.b = b; s.h = h; s.hk = hk; s.seqlen_q = sq; s.seqlen_k = sk; s.d = d;
   s.lse_pitch = sq;
   s.cu_seqlens_q = cu_q; s.cu_seqlens_k = cu_k; s.varlen_padded_input = padded;
   s.causal = causal;
   s.scale = scale;
   s.scale_log2 = scale * 1.4426950408889634f;
+  // reference set_params_fprop (flash_api.cpp:94-100): keep prob, its uint8 threshold, 1 / keep prob
+  s.dropout = p_dropout > 0.f;
+  s.p_keep = 1.f - p_dropout;
+  s.keep_u8 = (unsigned)(uint8_t)std::floor(s.p_keep * 255.0);
+  s.rp_dropout = 1.f / s.p_keep;
+  s.philox_seed = seed;
+  s.philox_offset = offset;
   return s;
 }
 
 bool fwd_impl(const void* q, const void* k, const void* v, const int32_t* cu_q, const int32_t* cu_k,
               void* rng_state, void* out, void* softmax_ptr, void* lse, int b, int sq, int sk,
+              int sq_r, int sk_r,
               int h, int hk, int d, int d_r, float p_dropout, float scale, bool causal,
               bool return_softmax, bool is_bf16, hipStream_t stream, uint64_t seed, uint64_t offset,
               const void* attn_mask, const void* flashmask, int q_row, int k_row, int v_row,
@@ -97,12 +106,19 @@ bool fwd_impl(const void* q, const void* k, const void* v, const int32_t* cu_q, 
               int v_batch, int o_batch, bool padded) {
   FA_BEGIN
   check_common(b, h, hk, d, d_r, p_dropout, attn_mask, flashmask);
-  if (return_softmax) throw std::runtime_error("return_softmax requires dropout, which is not implemented yet");
-  (void)softmax_ptr;
+  // reference mha_fwd: "return_softmax is only supported when p_dropout > 0.0" (flash_api.cpp:276-279)
+  if (return_softmax && !(p_dropout > 0.f))
+    throw std::runtime_error("return_softmax is only supported when p_dropout > 0.0");
   FA_CHECK(q && k && v && out && lse);
   fa::FwdParams p;
   std::memset(&p, 0, sizeof(p));
-  p.s = make_shape(b, h, hk, sq, sk, d, scale, causal, cu_q, cu_k, padded);
+  p.s = make_shape(b, h, hk, sq, sk, d, scale, causal, cu_q, cu_k, padded, p_dropout, seed, offset);
+  if (return_softmax) {
+    FA_CHECK(softmax_ptr != nullptr && sq_r >= sq && sk_r >= sk);
+    p.p_out = softmax_ptr;
+    p.p_rows = sq_r;
+    p.p_cols = sk_r;
+  }
   p.q = q; p.k = k; p.v = v; p.o = out; p.lse = static_cast<float*>(lse);
   p.q_batch = q_batch; p.q_row = q_row; p.q_head = q_head;
   p.k_batch = k_batch; p.k_row = k_row; p.k_head = k_head;
@@ -127,7 +143,7 @@ bool bwd_impl(const void* dout, const void* q, const void* k, const void* v, con
               int o_head, int q_batch, int k_batch, int v_batch, int o_batch, int dq_row,
               int dk_row, int dv_row, int dq_head, int dk_head, int dv_head, int do_row,
               int do_head, int dq_batch, int dk_batch, int dv_batch, int do_batch, bool padded,
-              bool gqa_reduce) {
+              bool gqa_reduce, void* rng_state, uint64_t seed, uint64_t offset) {
   FA_BEGIN
   check_common(b, h, hk, d, d_r, p_dropout, attn_mask, flashmask);
   FA_CHECK(dout && q && k && v && out && softmax_d && lse && dq && dk && dv);
@@ -135,8 +151,13 @@ bool bwd_impl(const void* dout, const void* q, const void* k, const void* v, con
   FA_CHECK(sq_r >= sq);
   fa::BwdParams p;
   std::memset(&p, 0, sizeof(p));
-  p.s = make_shape(b, h, hk, sq, sk, d, scale, causal, cu_q, cu_k, padded);
-  p.s.lse_pitch = sq;  // softmax_lse is (b, h, seqlen_q) as written by the forward
+  p.s = make_shape(b, h, hk, sq, sk, d, scale, causal, cu_q, cu_k, padded, p_dropout, seed, offset);
+  p.s.lse_pitch = sq;
+  if (p.s.dropout && rng_state != nullptr) {   // reference capi flash_attn.cu:943-947
+    const uint64_t st[2] = {seed, offset};
+    if (hipMemcpyAsync(rng_state, st, sizeof(st), hipMemcpyHostToDevice, stream) != hipSuccess)
+      throw std::runtime_error("flash_attn_bwd: rng_state copy failed");
+  }  // softmax_lse is (b, h, seqlen_q) as written by the forward
   p.q = q; p.k = k; p.v = v; p.o = out; p.dout = dout;
   p.dq = dq; p.dk = dk; p.dv = dv;
   p.lse = static_cast<const float*>(lse);
@@ -188,11 +209,12 @@ bool flash_attn_fwd(const void* const q, const void* const k, const void* const 
                     const int q_head_stride, const int k_head_stride, const int v_head_stride,
                     const int o_row_stride, const int o_head_stride, const int q_batch_stride,
                     const int k_batch_stride, const int v_batch_stride, const int o_batch_stride) {
-  (void)seqlen_q_rounded; (void)seqlen_k_rounded; (void)softmax_unscale; (void)mask_dims;
+  (void)softmax_unscale; (void)mask_dims;
   (void)flashmask_dims; (void)flashmask_upend_ptr; (void)flashmask_downend_ptr;
   (void)flashmask_upstart_ptr; (void)flashmask_maxmin_ptr;
   return fwd_impl(q, k, v, nullptr, nullptr, rng_state, out, softmax_ptr, softmax_lse_ptr,
-                  batch_size, seqlen_q, seqlen_k, num_heads, num_heads_k, head_size,
+                  batch_size, seqlen_q, seqlen_k, seqlen_q_rounded, seqlen_k_rounded,
+                  num_heads, num_heads_k, head_size,
                   head_size_rounded, p_dropout, softmax_scale, is_causal, return_softmax, is_bf16,
                   stream, seed, offset, attn_mask, flashmask_downstart_ptr, q_row_stride,
                   k_row_stride, v_row_stride, q_head_stride, k_head_stride, v_head_stride,
@@ -218,13 +240,14 @@ bool flash_attn_varlen_fwd(const void* const q, const void* const k, const void*
                            const int o_head_stride, const int q_batch_stride,
                            const int k_batch_stride, const int v_batch_stride,
                            const int o_batch_stride, bool varlen_padded_input) {
-  (void)seqlen_q_rounded; (void)seqlen_k_rounded; (void)softmax_unscale; (void)mask_dims;
+  (void)softmax_unscale; (void)mask_dims;
   if (cu_seqlens_q == nullptr || cu_seqlens_k == nullptr) {
     set_error("flash_attn_varlen_fwd: cu_seqlens_q / cu_seqlens_k must not be null");
     return false;
   }
   return fwd_impl(q, k, v, cu_seqlens_q, cu_seqlens_k, rng_state, out, softmax_ptr,
-                  softmax_lse_ptr, batch_size, max_seqlen_q, max_seqlen_k, num_heads, num_heads_k,
+                  softmax_lse_ptr, batch_size, max_seqlen_q, max_seqlen_k, seqlen_q_rounded,
+                  seqlen_k_rounded, num_heads, num_heads_k,
                   head_size, head_size_rounded, p_dropout, softmax_scale, is_causal,
                   return_softmax, is_bf16, stream, seed, offset, attn_mask, nullptr, q_row_stride,
                   k_row_stride, v_row_stride, q_head_stride, k_head_stride, v_head_stride,
@@ -256,8 +279,8 @@ bool flash_attn_varlen_fwd(const void* const q, const void* const k, const void*
       const int do_batch_stride
 
 #define FA_BWD_CALL(GQA)                                                                          \
-  (void)rng_state; (void)seqlen_k_rounded; (void)softmax_unscale; (void)num_splits; (void)seed;   \
-  (void)offset; (void)mask_dims; (void)flashmask_dims; (void)flashmask_upend_ptr;                  \
+  (void)seqlen_k_rounded; (void)softmax_unscale; (void)num_splits;                                \
+  (void)mask_dims; (void)flashmask_dims; (void)flashmask_upend_ptr;                                \
   (void)flashmask_downend_ptr; (void)flashmask_upstart_ptr; (void)flashmask_maxmin_ptr;            \
   return bwd_impl(dout, q, k, v, out, softmax_d, softmax_lse, nullptr, nullptr, dq, dk, dv,        \
                   dq_accum, batch_size, seqlen_q, seqlen_k, seqlen_q_rounded, num_heads,           \
@@ -267,7 +290,7 @@ bool flash_attn_varlen_fwd(const void* const q, const void* const k, const void*
                   o_head_stride, q_batch_stride, k_batch_stride, v_batch_stride, o_batch_stride,   \
                   dq_row_stride, dk_row_stride, dv_row_stride, dq_head_stride, dk_head_stride,     \
                   dv_head_stride, do_row_stride, do_head_stride, dq_batch_stride, dk_batch_stride, \
-                  dv_batch_stride, do_batch_stride, false, GQA)
+                  dv_batch_stride, do_batch_stride, false, GQA, rng_state, seed, offset)
 
 bool flash_attn_bwd(FA_BWD_ARGS) { FA_BWD_CALL(false); }
 bool flash_attn_bwd_gqa(FA_BWD_ARGS) { FA_BWD_CALL(true); }
@@ -294,8 +317,7 @@ bool flash_attn_bwd_gqa(FA_BWD_ARGS) { FA_BWD_CALL(true); }
       const int dv_batch_stride, const int do_batch_stride, const bool varlen_padded_input
 
 #define FA_VARLEN_BWD_CALL(GQA)                                                                   \
-  (void)rng_state; (void)seqlen_k_rounded; (void)softmax_unscale; (void)num_splits; (void)seed;   \
-  (void)offset; (void)mask_dims;                                                                   \
+  (void)seqlen_k_rounded; (void)softmax_unscale; (void)num_splits; (void)mask_dims;               \
   if (cu_seqlens_q == nullptr || cu_seqlens_k == nullptr) {                                        \
     set_error("flash_attn_varlen_bwd: cu_seqlens_q / cu_seqlens_k must not be null");             \
     return false;                                                                                  \
@@ -308,7 +330,8 @@ bool flash_attn_bwd_gqa(FA_BWD_ARGS) { FA_BWD_CALL(true); }
                   o_head_stride, q_batch_stride, k_batch_stride, v_batch_stride, o_batch_stride,   \
                   dq_row_stride, dk_row_stride, dv_row_stride, dq_head_stride, dk_head_stride,     \
                   dv_head_stride, do_row_stride, do_head_stride, dq_batch_stride, dk_batch_stride, \
-                  dv_batch_stride, do_batch_stride, varlen_padded_input, GQA)
+                  dv_batch_stride, do_batch_stride, varlen_padded_input, GQA, rng_state, seed,     \
+                  offset)
 
 bool flash_attn_varlen_bwd(FA_VARLEN_BWD_ARGS) { FA_VARLEN_BWD_CALL(false); }
 bool flash_attn_varlen_bwd_gqa(FA_VARLEN_BWD_ARGS) { FA_VARLEN_BWD_CALL(true); }

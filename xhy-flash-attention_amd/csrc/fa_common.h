@@ -51,12 +51,12 @@ template <> struct Elt<true> {
     return __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf16x8_t, a),
                                                    __builtin_bit_cast(bf16x8_t, b), c, 0, 0, 0);
   }
-  // v_cvt_pk_bf16_f32 (RNE, NaN-preserving).  Written as (non-volatile) asm: from the plain
-  // {(__bf16)lo, (__bf16)hi} form hipcc sometimes emits per-element converts plus v_perm/v_bfi.
+  // v_cvt_pk_bf16_f32 (RNE, NaN-preserving).  Kept compiler-visible on purpose: an asm convert is
+  // opaque to the hazard recognizer, which then omits the wait states between an MFMA and a
+  // following VALU write of that MFMA's source registers (observed: corrupted dQ operands).
   __device__ static inline unsigned pack2(float lo, float hi) {
-    unsigned r;
-    asm("v_cvt_pk_bf16_f32 %0, %1, %2" : "=v"(r) : "v"(lo), "v"(hi));
-    return r;
+    bf16x2_t v = {(__bf16)lo, (__bf16)hi};
+    return __builtin_bit_cast(unsigned, v);
   }
   __device__ static inline float to_f32(unsigned short x) {
     return __builtin_bit_cast(float, (unsigned)x << 16);
@@ -69,9 +69,8 @@ template <> struct Elt<false> {
                                                   __builtin_bit_cast(f16x8_t, b), c, 0, 0, 0);
   }
   __device__ static inline unsigned pack2(float lo, float hi) {   // v_cvt_pk_f16_f32 (RNE)
-    unsigned r;
-    asm("v_cvt_pk_f16_f32 %0, %1, %2" : "=v"(r) : "v"(lo), "v"(hi));
-    return r;
+    f16x2_t v = {(_Float16)lo, (_Float16)hi};
+    return __builtin_bit_cast(unsigned, v);
   }
   __device__ static inline float to_f32(unsigned short x) {
     return (float)__builtin_bit_cast(_Float16, x);

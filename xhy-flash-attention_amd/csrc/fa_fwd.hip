@@ -32,6 +32,7 @@
 #include <string>
 
 #include "fa_common.h"
+#include "fa_dropout.h"
 #include "fa_params.h"
 
 namespace fa {
@@ -49,7 +50,7 @@ template <int D> struct FwdTile {
 constexpr int kFwdBufs = 4;   // ring depth: tiles nb, nb+1 read while nb+2, nb+3 land
 constexpr float kFwdRescaleThr = 8.f;   // deferred-max threshold, log2 units (P <= 256)
 
-template <bool BF16, int D, bool CAUSAL>
+template <bool BF16, int D, bool CAUSAL, bool DROPOUT>
 __global__ void __launch_bounds__(FwdTile<D>::NW * 64, FwdTile<D>::MINB) fwd_kernel(const FwdParams p) {
   using E = Elt<BF16>;
   constexpr int NW = FwdTile<D>::NW;
@@ -62,7 +63,8 @@ __global__ void __launch_bounds__(FwdTile<D>::NW * 64, FwdTile<D>::MINB) fwd_ker
   constexpr int PIECES = TILE / 1024;   // 1-KiB LDS-DMA pieces per K (or V) tile
   constexpr int PPW = (PIECES + NW - 1) / NW;
   static_assert(TILE % 1024 == 0, "tile must be whole DMA pieces");
-  __shared__ __attribute__((aligned(16))) char smem[kFwdBufs * 2 * TILE];  // [buffer][K | V]
+  // [buffer][K | V], then (dropout) one 1-KiB random-byte scratch per wave
+  __shared__ __attribute__((aligned(16))) char smem[kFwdBufs * 2 * TILE + (DROPOUT ? NW * 1024 : 0)];
 
   const AttnShape s = p.s;
   const int tid = threadIdx.x, lane = tid & 63;
@@ -218,17 +220,28 @@ __global__ void __launch_bounds__(FwdTile<D>::NW * 64, FwdTile<D>::MINB) fwd_ker
       m_run = m_new;
     }
   };
-  // P = exp2(S c - m c) -> packed B operands; returns the partial row sum of this lane
-  auto softmax_pack = [&](f32x16_t (&st)[NT], i16x8_t (&pf)[2 * NT]) {
+  // P = exp2(S c - m c) -> packed B operands; adds the partial row sum of this lane to l_run (the
+  // sum is over the undropped P, as in the reference); with dropout the dropped elements of the
+  // packed P are zero (reference flash_fwd_kernel.h:429-432; O is scaled by 1/keep_prob at the end)
+  char* const dscr = smem + kFwdBufs * 2 * TILE + wave * 1024;
+  const uint64_t doff = s.philox_offset + (uint64_t)(bidb * s.h + head) * 32;
+  auto softmax_pack = [&](f32x16_t (&st)[NT], i16x8_t (&pf)[2 * NT], int n0) {
     const float ms = (m_run == kNegInf) ? 0.f : m_run * c;
     float ls[4] = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
     for (int t = 0; t < NT; ++t) {
+      unsigned rb[4];
+      if constexpr (DROPOUT) {
+        dropout_block_bytes<false>(dscr, s.philox_seed, doff, wq0, n0 + 32 * t, lane);
+#pragma unroll
+        for (int u = 0; u < 4; ++u) rb[u] = dropout_group_bytes(dscr, r, hh, u);
+      }
 #pragma unroll
       for (int g = 0; g < 16; ++g) {
         const float pv = fast_exp2(fmaf(st[t][g], c, -ms));
-        st[t][g] = pv;
         ls[g & 3] += pv;
+        if constexpr (DROPOUT) st[t][g] = dropout_keep(rb[g >> 2], g & 3, s.keep_u8) ? pv : 0.f;
+        else st[t][g] = pv;
       }
       pf[2 * t] = pack_frag<BF16>(st[t], 0);
       pf[2 * t + 1] = pack_frag<BF16>(st[t], 1);
@@ -268,7 +281,7 @@ __global__ void __launch_bounds__(FwdTile<D>::NW * 64, FwdTile<D>::MINB) fwd_ker
       const int cur = (nb % kFwdBufs) * 2 * TILE;
       const int nxt = ((nb + 1) % kFwdBufs) * 2 * TILE;
       i16x8_t pf[2 * NT];
-      softmax_pack(scur, pf);
+      softmax_pack(scur, pf, nb * BN);
       // tile nb+1 is resident (possibly past nblk: then its scores are simply discarded); its
       // MFMAs are independent of the softmax above, so the two interleave in this basic block
       qk(nxt, snxt);
@@ -303,7 +316,7 @@ __global__ void __launch_bounds__(FwdTile<D>::NW * 64, FwdTile<D>::MINB) fwd_ker
         }
       rescale(rowmax(st));
       i16x8_t pf[2 * NT];
-      softmax_pack(st, pf);
+      softmax_pack(st, pf, n0);
       pv(cur + TILE, pf);
     }
     tile_sync(nb + 3 < nblk);
@@ -312,7 +325,7 @@ __global__ void __launch_bounds__(FwdTile<D>::NW * 64, FwdTile<D>::MINB) fwd_ker
   // ---- epilogue ----
   const float l_tot = half_swap_sum(l_run);
   const bool bad = (l_tot == 0.f) || (l_tot != l_tot);
-  const float inv = bad ? 1.f : fast_rcp(l_tot);
+  const float inv = bad ? 1.f : fast_rcp(l_tot) * (DROPOUT ? s.rp_dropout : 1.f);
   const float lse = bad ? __builtin_huge_valf() : m_run * s.scale + __logf(l_tot);
   {
     // 16-byte stores: v_permlane32_swap pairs column groups (u, u+1) so that lane half 0 holds
@@ -338,24 +351,84 @@ __global__ void __launch_bounds__(FwdTile<D>::NW * 64, FwdTile<D>::MINB) fwd_ker
   }
 }
 
-template <bool BF16, int D, bool CAUSAL>
+// return_softmax (test-only, reference flash_api.cpp:276-279): S_dmask[b][h][i][j] =
+// exp(scale * q_i . k_j - LSE_i), negated where dropout drops the element, 0 where masked or padded.
+// A plain fp32 dot product per element: it runs only for the reference's dropout tests.
+template <bool BF16>
+__global__ void __launch_bounds__(256) dmask_kernel(const FwdParams p) {
+  using E = Elt<BF16>;
+  typedef unsigned short u16;
+  const AttnShape s = p.s;
+  const int bh = blockIdx.z;
+  const int bidb = bh / s.h, head = bh - bidb * s.h;
+  const int kvh = head / (s.h / s.hk);
+  const int col = blockIdx.x * 64 + (threadIdx.x & 63);
+  const int row = blockIdx.y * 4 + (threadIdx.x >> 6);
+  if (row >= p.p_rows || col >= p.p_cols) return;
+  int sq = s.seqlen_q, sk = s.seqlen_k;
+  int64_t q_off = (int64_t)bidb * p.q_batch, k_off = (int64_t)bidb * p.k_batch;
+  if (s.cu_seqlens_q) {
+    const int c0 = s.cu_seqlens_q[bidb];
+    sq = s.cu_seqlens_q[bidb + 1] - c0;
+    if (!s.varlen_padded_input) q_off = (int64_t)c0 * p.q_row;
+  }
+  if (s.cu_seqlens_k) {
+    const int c0 = s.cu_seqlens_k[bidb];
+    sk = s.cu_seqlens_k[bidb + 1] - c0;
+    if (!s.varlen_padded_input) k_off = (int64_t)c0 * p.k_row;
+  }
+  float val = 0.f;
+  if (row < sq && col < sk && !(s.causal && col > row)) {
+    const u16* qr = (const u16*)p.q + q_off + (int64_t)head * p.q_head + (int64_t)row * p.q_row;
+    const u16* kr = (const u16*)p.k + k_off + (int64_t)kvh * p.k_head + (int64_t)col * p.k_row;
+    float acc = 0.f;
+    for (int d = 0; d < s.d; ++d) acc += E::to_f32(qr[d]) * E::to_f32(kr[d]);
+    const float lse = p.lse[((int64_t)bidb * s.h + head) * s.lse_pitch + row];
+    val = __expf(acc * s.scale - lse);
+    // the reference's byte for (row, col), computed directly (one Philox call per element)
+    const int rr = row % 16, cc = col % 32;
+    const int lanec = 4 * (rr % 8) + (cc % 8) / 2;
+    const int bidx = 8 * (cc / 16) + (cc % 2) + 2 * (rr / 8) + 4 * ((cc % 16) / 8);
+    const uint64_t sub = (uint64_t)(unsigned)(row / 16) | ((uint64_t)(unsigned)(col / 32) << 32);
+    const u32x4_t w = philox(s.philox_seed, sub, s.philox_offset + (uint64_t)bh * 32 + lanec);
+    const unsigned byte = (w[bidx >> 2] >> (8 * (bidx & 3))) & 0xffu;
+    if (byte > s.keep_u8) val = -val;
+  }
+  u16* out = (u16*)p.p_out + ((int64_t)bh * p.p_rows + row) * p.p_cols + col;
+  *out = (u16)(E::pack2(val, 0.f) & 0xffff);
+}
+
+template <bool BF16, int D, bool CAUSAL, bool DROPOUT>
 static void run_fwd(const FwdParams& p, hipStream_t stream) {
   dim3 grid(p.s.b * p.s.h, p.num_m_blocks);
   prof_begin(kTimeFwd, stream);
-  hipLaunchKernelGGL((fwd_kernel<BF16, D, CAUSAL>), grid, dim3(FwdTile<D>::NW * 64), 0, stream, p);
+  hipLaunchKernelGGL((fwd_kernel<BF16, D, CAUSAL, DROPOUT>), grid, dim3(FwdTile<D>::NW * 64), 0, stream, p);
   prof_end(kTimeFwd, stream);
 }
 
-template <bool BF16, bool CAUSAL>
+template <bool BF16, bool CAUSAL, bool DROPOUT>
 static void dispatch_d(const FwdParams& p, hipStream_t stream) {
   const int d = p.s.d;
-  if (d <= 32) run_fwd<BF16, 32, CAUSAL>(p, stream);
-  else if (d <= 64) run_fwd<BF16, 64, CAUSAL>(p, stream);
-  else if (d <= 96) run_fwd<BF16, 96, CAUSAL>(p, stream);
-  else if (d <= 128) run_fwd<BF16, 128, CAUSAL>(p, stream);
-  else if (d <= 192) run_fwd<BF16, 192, CAUSAL>(p, stream);
-  else if (d <= 256) run_fwd<BF16, 256, CAUSAL>(p, stream);
+  if (d <= 32) run_fwd<BF16, 32, CAUSAL, DROPOUT>(p, stream);
+  else if (d <= 64) run_fwd<BF16, 64, CAUSAL, DROPOUT>(p, stream);
+  else if (d <= 96) run_fwd<BF16, 96, CAUSAL, DROPOUT>(p, stream);
+  else if (d <= 128) run_fwd<BF16, 128, CAUSAL, DROPOUT>(p, stream);
+  else if (d <= 192) run_fwd<BF16, 192, CAUSAL, DROPOUT>(p, stream);
+  else if (d <= 256) run_fwd<BF16, 256, CAUSAL, DROPOUT>(p, stream);
   else throw std::runtime_error("flash_attn_fwd: head dim " + std::to_string(d) + " > 256");
+}
+
+template <bool BF16>
+static void dispatch_fwd(const FwdParams& p, hipStream_t stream) {
+  if (p.s.causal) {
+    if (p.s.dropout) dispatch_d<BF16, true, true>(p, stream); else dispatch_d<BF16, true, false>(p, stream);
+  } else {
+    if (p.s.dropout) dispatch_d<BF16, false, true>(p, stream); else dispatch_d<BF16, false, false>(p, stream);
+  }
+  if (p.p_out != nullptr) {
+    dim3 grid((p.p_cols + 63) / 64, (p.p_rows + 3) / 4, p.s.b * p.s.h);
+    hipLaunchKernelGGL((dmask_kernel<BF16>), grid, dim3(256), 0, stream, p);
+  }
 }
 
 void fwd_block_size(int d, int* block_m, int* block_n) {
@@ -367,11 +440,9 @@ void launch_fwd(const FwdParams& p, bool is_bf16, hipStream_t stream) {
   if (p.s.b <= 0 || p.s.h <= 0) return;
   if (p.num_m_blocks <= 0) return;
   if (p.num_m_blocks > 65535) throw std::runtime_error("flash_attn_fwd: seqlen_q too large for grid.y");
-  if (is_bf16) {
-    if (p.s.causal) dispatch_d<true, true>(p, stream); else dispatch_d<true, false>(p, stream);
-  } else {
-    if (p.s.causal) dispatch_d<false, true>(p, stream); else dispatch_d<false, false>(p, stream);
-  }
+  if (p.p_out != nullptr && (p.p_rows > 65535 * 4 || p.s.b * p.s.h > 65535))
+    throw std::runtime_error("flash_attn_fwd: return_softmax grid too large");
+  if (is_bf16) dispatch_fwd<true>(p, stream); else dispatch_fwd<false>(p, stream);
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) throw std::runtime_error(std::string("flash_attn_fwd launch: ") + hipGetErrorString(e));
 }

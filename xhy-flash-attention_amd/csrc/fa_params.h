@@ -27,6 +27,12 @@ struct AttnShape {
   bool causal;
   float scale;      // softmax scale
   float scale_log2; // scale * log2(e)
+  // dropout (reference Flash_fwd_params p_dropout / p_dropout_in_uint8_t / rp_dropout, flash.h:88-95)
+  bool dropout;             // p_dropout > 0
+  unsigned keep_u8;         // floor(keep_prob * 255): an element is kept iff its random byte <= this
+  float p_keep;             // keep probability 1 - p_dropout
+  float rp_dropout;         // 1 / p_keep
+  uint64_t philox_seed, philox_offset;   // the reference's (seed, offset) pair (rng_state)
 };
 
 struct FwdParams {
@@ -40,6 +46,8 @@ struct FwdParams {
   int64_t v_batch, v_row, v_head;
   int64_t o_batch, o_row, o_head;
   int num_m_blocks;
+  void* p_out;              // return_softmax (dropout only): S_dmask (b, h, sq_rounded, sk_rounded)
+  int p_rows, p_cols;       // sq_rounded, sk_rounded
 };
 
 struct BwdParams {

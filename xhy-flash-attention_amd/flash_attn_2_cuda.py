@@ -123,9 +123,29 @@ def _pad8(x: torch.Tensor, d_og: int):
     return torch.nn.functional.pad(x, (0, 8 - d_og % 8))
 
 
-def _seed_offset(p_dropout, gen):
-    # Dropout is rejected by the C ABI until the Philox path lands; record zeros.
-    return 0, 0
+def _seed_offset(p_dropout, gen, device, counter_offset):
+    """Philox (seed, offset) for one dropout call, as the reference takes them from the CUDA
+    generator: gen->philox_cuda_state(batch * nheads * 32) (flash_api.cpp:297-312), i.e. the current
+    offset, then the generator's offset advanced by the increment rounded up to a multiple of 4.
+    Without dropout nothing is drawn and (0, 0) is recorded."""
+    if not p_dropout > 0.0:
+        return 0, 0
+    if gen is None:
+        idx = device.index if device.index is not None else torch.cuda.current_device()
+        gen = torch.cuda.default_generators[idx]
+    seed = gen.initial_seed()
+    offset = gen.get_offset()
+    gen.set_offset(offset + (counter_offset + 3) // 4 * 4)
+    return int(seed) & (2 ** 64 - 1), int(offset)
+
+
+def _rng_seed_offset(p_dropout, rng_state):
+    """(seed, offset) the forward recorded in rng_state (int64[2]); read back to the host, which
+    synchronises -- only on the dropout path."""
+    if not p_dropout > 0.0 or rng_state is None:
+        return 0, 0
+    seed, offset = (int(x) & (2 ** 64 - 1) for x in rng_state.cpu().tolist())
+    return seed, offset
 
 
 # --------------------------------------------------------------------------------------------------
@@ -170,14 +190,17 @@ def fwd(q, k, v, out_, p_dropout, softmax_scale, is_causal, return_softmax, gen_
     with torch.cuda.device(q.device):
         softmax_lse = torch.empty((batch_size, num_heads, seqlen_q), dtype=torch.float32, device=q.device)
         p = None
+        if return_softmax:   # S_dmask (b, h, sq_r, sk_r), dropped elements negated
+            p = torch.empty((batch_size, num_heads, seqlen_q_rounded, seqlen_k_rounded), dtype=q.dtype,
+                            device=q.device)
         rng_state = torch.empty((2,), dtype=torch.int64, device=q.device)
-        seed, offset = _seed_offset(p_dropout, gen_)
+        seed, offset = _seed_offset(p_dropout, gen_, q.device, batch_size * num_heads * 32)
         qb, qr, qh = _strides(qk, 4)
         kb, kr, kh = _strides(kk, 4)
         vb, vr, vh = _strides(vk, 4)
         ob, orr, oh = _strides(out, 4)
         ok = _lib.flash_attn_fwd(
-            _ptr(qk), _ptr(kk), _ptr(vk), _ptr(rng_state), _ptr(out), None, _ptr(softmax_lse),
+            _ptr(qk), _ptr(kk), _ptr(vk), _ptr(rng_state), _ptr(out), _ptr(p), _ptr(softmax_lse),
             batch_size, seqlen_q, seqlen_k, seqlen_q_rounded, seqlen_k_rounded,
             num_heads, num_heads_k, head_size, head_size_rounded,
             float(p_dropout), float(softmax_scale), 1.0, bool(is_causal), bool(return_softmax),
@@ -246,15 +269,18 @@ def varlen_fwd(q, k, v, out_, cu_seqlens_q, cu_seqlens_k, max_seqlen_q, max_seql
             out.zero_()
             softmax_lse.fill_(float("-inf"))
         p = None
+        if return_softmax:   # S_dmask (b, h, sq_r, sk_r), dropped elements negated
+            p = torch.empty((batch_size, num_heads, seqlen_q_rounded, seqlen_k_rounded), dtype=q.dtype,
+                            device=q.device)
         rng_state = torch.empty((2,), dtype=torch.int64, device=q.device)
-        seed, offset = _seed_offset(p_dropout, gen_)
+        seed, offset = _seed_offset(p_dropout, gen_, q.device, batch_size * num_heads * 32)
         _, qr, qh = _strides(qk, 3)
         _, kr, kh = _strides(kk, 3)
         _, vr, vh = _strides(vk, 3)
         _, orr, oh = _strides(out, 3)
         ok = _lib.flash_attn_varlen_fwd(
             _ptr(qk), _ptr(kk), _ptr(vk), _ptr(cu_seqlens_q), _ptr(cu_seqlens_k), _ptr(rng_state),
-            _ptr(out), None, _ptr(softmax_lse), batch_size, int(max_seqlen_q), int(max_seqlen_k),
+            _ptr(out), _ptr(p), _ptr(softmax_lse), batch_size, int(max_seqlen_q), int(max_seqlen_k),
             seqlen_q_rounded, seqlen_k_rounded, num_heads, num_heads_k, head_size,
             head_size_rounded, float(p_dropout), float(softmax_scale), 1.0, bool(is_causal),
             bool(return_softmax), q.dtype == torch.bfloat16, _stream(q), seed, offset, None, None,
@@ -332,7 +358,7 @@ def bwd(dout, q, k, v, out, softmax_lse, dq_, dk_, dv_, p_dropout, softmax_scale
                 batch_size, seqlen_q, seqlen_k, seqlen_q_rounded, seqlen_k_rounded,
                 num_heads, num_heads_k, head_size, head_size_rounded,
                 float(p_dropout), float(softmax_scale), 1.0, bool(is_causal),
-                q.dtype == torch.bfloat16, 0, _stream(q), 0, 0,
+                q.dtype == torch.bfloat16, 0, _stream(q), *_rng_seed_offset(p_dropout, rng_state),
                 None, None, None, None, None, None, None, None,
                 qr, kr, vr, qh, kh, vh, orr, oh, qb, kb, vb, ob,
                 dqr, dkr, dvr, dqh, dkh, dvh, dor, doh, dqb, dkb, dvb, dob)
@@ -392,7 +418,8 @@ def varlen_bwd(dout, q, k, v, out, softmax_lse, dq_, dk_, dv_, cu_seqlens_q, cu_
                 _ptr(dq), _ptr(dk), _ptr(dv), _ptr(dq_accum), batch_size, int(max_seqlen_q),
                 int(max_seqlen_k), seqlen_q_rounded, seqlen_k_rounded, num_heads, num_heads_k,
                 head_size, head_size_rounded, float(p_dropout), float(softmax_scale), 1.0,
-                bool(is_causal), q.dtype == torch.bfloat16, 0, _stream(q), 0, 0, None, None,
+                bool(is_causal), q.dtype == torch.bfloat16, 0, _stream(q),
+                *_rng_seed_offset(p_dropout, rng_state), None, None,
                 qr, kr, vr, qh, kh, vh, orr, oh, 0, 0, 0, 0,
                 dqr, dkr, dvr, dqh, dkh, dvh, dor, doh, 0, 0, 0, 0, False)
         if not ok:
