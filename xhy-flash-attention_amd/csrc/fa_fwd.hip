@@ -47,7 +47,7 @@ template <int D> struct FwdTile {
   static constexpr int BN = D <= 128 ? 64 : 32;
   static constexpr int MINB = D <= 128 ? 2 : 1;   // __launch_bounds__ blocks per CU (register budget)
 };
-constexpr int kFwdBufs = 4;   // ring depth: tiles nb, nb+1 read while nb+2, nb+3 land
+constexpr int kFwdBufs = 4;   // K ring depth: tiles nb, nb+1 read while nb+2, nb+3 land
 constexpr float kFwdRescaleThr = 8.f;   // deferred-max threshold, log2 units (P <= 256)
 
 template <bool BF16, int D, bool CAUSAL, bool DROPOUT>
@@ -63,8 +63,18 @@ __global__ void __launch_bounds__(FwdTile<D>::NW * 64, FwdTile<D>::MINB) fwd_ker
   constexpr int PIECES = TILE / 1024;   // 1-KiB LDS-DMA pieces per K (or V) tile
   constexpr int PPW = (PIECES + NW - 1) / NW;
   static_assert(TILE % 1024 == 0, "tile must be whole DMA pieces");
-  // [buffer][K | V], then (dropout) one 1-KiB random-byte scratch per wave
-  __shared__ __attribute__((aligned(16))) char smem[kFwdBufs * 2 * TILE + (DROPOUT ? NW * 1024 : 0)];
+  // Staggered halves (8-wave workgroups): waves 4-7 run the PV of each tile one step late, so on
+  // every SIMD one wave opens its step with the softmax VALU while its partner opens with PV MFMAs
+  // (MI355X_MICROARCH.md "Two waves per SIMD", item 9).  The late PV reads V(nb-1) while the DMA of
+  // V(nb+3) is in flight, hence a 5-deep V ring next to the 4-deep K ring.
+  constexpr bool STAGGER = NW == 8;
+  constexpr int VBUFS = STAGGER ? 5 : 4;
+  constexpr int VBASE = kFwdBufs * TILE;
+  constexpr int SCRATCH = VBASE + VBUFS * TILE;
+  // [K ring][V ring], then (dropout) one 1-KiB random-byte scratch per wave
+  __shared__ __attribute__((aligned(16))) char smem[SCRATCH + (DROPOUT ? NW * 1024 : 0)];
+  auto kslot = [&](int nb) { return (nb % kFwdBufs) * TILE; };
+  auto vslot = [&](int nb) { return VBASE + (nb % VBUFS) * TILE; };
 
   const AttnShape s = p.s;
   const int tid = threadIdx.x, lane = tid & 63;
@@ -143,7 +153,8 @@ __global__ void __launch_bounds__(FwdTile<D>::NW * 64, FwdTile<D>::MINB) fwd_ker
   }
   auto issue = [&](int nb) {
     const int n0 = nb * BN;
-    char* dst = smem + (nb % kFwdBufs) * 2 * TILE;
+    char* kdst = smem + kslot(nb);
+    char* vdst = smem + vslot(nb);
     const int64_t kb = (int64_t)(sk - n0) * p.k_row * 2, vb = (int64_t)(sk - n0) * p.v_row * 2;
     const int krec = (int)(kb > 0x7fffffff ? 0x7fffffff : kb);
     const int vrec = (int)(vb > 0x7fffffff ? 0x7fffffff : vb);
@@ -153,8 +164,8 @@ __global__ void __launch_bounds__(FwdTile<D>::NW * 64, FwdTile<D>::MINB) fwd_ker
     for (int j = 0; j < PPW; ++j) {
       const int pc = wave + j * NW;
       if (PIECES % NW == 0 || pc < PIECES) {
-        dma16(rk, dst + pc * 1024, voff_k[j]);
-        dma16(rv, dst + TILE + pc * 1024, voff_v[j]);
+        dma16(rk, kdst + pc * 1024, voff_k[j]);
+        dma16(rv, vdst + pc * 1024, voff_v[j]);
       }
     }
   };
@@ -223,7 +234,7 @@ __global__ void __launch_bounds__(FwdTile<D>::NW * 64, FwdTile<D>::MINB) fwd_ker
   // P = exp2(S c - m c) -> packed B operands; adds the partial row sum of this lane to l_run (the
   // sum is over the undropped P, as in the reference); with dropout the dropped elements of the
   // packed P are zero (reference flash_fwd_kernel.h:429-432; O is scaled by 1/keep_prob at the end)
-  char* const dscr = smem + kFwdBufs * 2 * TILE + wave * 1024;
+  char* const dscr = smem + SCRATCH + wave * 1024;
   const uint64_t doff = s.philox_offset + (uint64_t)(bidb * s.h + head) * 32;
   auto softmax_pack = [&](f32x16_t (&st)[NT], i16x8_t (&pf)[2 * NT], int n0) {
     const float ms = (m_run == kNegInf) ? 0.f : m_run * c;
@@ -273,40 +284,61 @@ __global__ void __launch_bounds__(FwdTile<D>::NW * 64, FwdTile<D>::MINB) fwd_ker
   // ---- fast path: unmasked tiles, QK^T of the next tile overlapped with this tile's softmax ----
   if (nfast > 0) {
     f32x16_t sa[NT], sb[NT];
-    qk(0, sa);
+    qk(kslot(0), sa);
     float mt = rowmax(sa);
     auto body = [&](int nb, f32x16_t (&scur)[NT], f32x16_t (&snxt)[NT]) {
       if (nb + 3 < nblk) issue(nb + 3);
       rescale(mt);
-      const int cur = (nb % kFwdBufs) * 2 * TILE;
-      const int nxt = ((nb + 1) % kFwdBufs) * 2 * TILE;
       i16x8_t pf[2 * NT];
       softmax_pack(scur, pf, nb * BN);
       // tile nb+1 is resident (possibly past nblk: then its scores are simply discarded); its
       // MFMAs are independent of the softmax above, so the two interleave in this basic block
-      qk(nxt, snxt);
+      qk(kslot(nb + 1), snxt);
       __builtin_amdgcn_sched_barrier(0);   // bound the V-read hoisting (register pressure)
-      pv(cur + TILE, pf);
+      pv(vslot(nb), pf);
+      mt = rowmax(snxt);
+      tile_sync(nb + 3 < nblk);
+    };
+    // staggered half: PV(nb-1) first (its P fragments carried across the barrier), then the
+    // softmax of nb and QK(nb+1); the rescale for nb follows the late PV, so O is complete up to
+    // nb-1 whenever it is scaled
+    i16x8_t pfp[2 * NT];
+    auto body_late = [&](int nb, f32x16_t (&scur)[NT], f32x16_t (&snxt)[NT]) {
+      if (nb + 3 < nblk) issue(nb + 3);
+      if (nb > 0) pv(vslot(nb - 1), pfp);
+      __builtin_amdgcn_sched_barrier(0);
+      rescale(mt);
+      softmax_pack(scur, pfp, nb * BN);
+      qk(kslot(nb + 1), snxt);
       mt = rowmax(snxt);
       tile_sync(nb + 3 < nblk);
     };
     int nb = 0;
-    for (; nb + 1 < nfast; nb += 2) {
-      body(nb, sa, sb);
-      body(nb + 1, sb, sa);
+    if (!STAGGER || wave < NW / 2) {
+      for (; nb + 1 < nfast; nb += 2) {
+        body(nb, sa, sb);
+        body(nb + 1, sb, sa);
+      }
+      if (nb < nfast) body(nb, sa, sb);
+    } else {
+      for (; nb + 1 < nfast; nb += 2) {
+        body_late(nb, sa, sb);
+        body_late(nb + 1, sb, sa);
+      }
+      if (nb < nfast) body_late(nb, sa, sb);
+      pv(vslot(nfast - 1), pfp);   // the last deferred PV (V(nfast-1) is not overwritten before
+                                   // the general path's issue(nfast+3) lands in another slot)
     }
-    if (nb < nfast) body(nb, sa, sb);
   }
 
   // ---- general path: causal diagonal / ragged tiles, per-element masks ----
   for (int nb = nfast; nb < nblk; ++nb) {
     const int n0 = nb * BN;
     if (nb + 3 < nblk) issue(nb + 3);
-    const int cur = (nb % kFwdBufs) * 2 * TILE;
     const bool active = (wq0 < sq) && (!CAUSAL || n0 <= wq0 + 31);
     if (active) {
       f32x16_t st[NT];
-      qk(cur, st);
+      qk(kslot(nb), st);
 #pragma unroll
       for (int t = 0; t < NT; ++t)
 #pragma unroll
@@ -317,7 +349,7 @@ __global__ void __launch_bounds__(FwdTile<D>::NW * 64, FwdTile<D>::MINB) fwd_ker
       rescale(rowmax(st));
       i16x8_t pf[2 * NT];
       softmax_pack(st, pf, n0);
-      pv(cur + TILE, pf);
+      pv(vslot(nb), pf);
     }
     tile_sync(nb + 3 < nblk);
   }
