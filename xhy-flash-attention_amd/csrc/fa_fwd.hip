@@ -49,6 +49,7 @@ template <int D> struct FwdTile {
 };
 constexpr int kFwdBufs = 4;   // K ring depth: tiles nb, nb+1 read while nb+2, nb+3 land
 constexpr float kFwdRescaleThr = 8.f;   // deferred-max threshold, log2 units (P <= 256)
+constexpr float kFwdSumThr = 256.f;     // fast-path guard on a lane's per-tile sum of P (= 2^8)
 
 template <bool BF16, int D, bool CAUSAL, bool DROPOUT>
 __global__ void __launch_bounds__(FwdTile<D>::NW * 64, FwdTile<D>::MINB) fwd_kernel(const FwdParams p) {
@@ -259,6 +260,59 @@ __global__ void __launch_bounds__(FwdTile<D>::NW * 64, FwdTile<D>::MINB) fwd_ker
     }
     l_run += (ls[0] + ls[1]) + (ls[2] + ls[3]);
   };
+  // Fast-path softmax, no max pass: P = exp2(S c - m_run c) against the running max of earlier
+  // tiles (finite here).  Returns this lane's partial row sum; the caller adds it to l_run only after
+  // the overflow check (guard_ok), so a tile that trips the check is simply recomputed.
+  auto softmax_fast = [&](const f32x16_t (&st)[NT], i16x8_t (&pf)[2 * NT], int n0) {
+    const float ms = m_run * c;
+    float ls[4];
+#pragma unroll
+    for (int t = 0; t < NT; ++t) {
+      unsigned rb[4];
+      if constexpr (DROPOUT) {
+        dropout_block_bytes<false>(dscr, s.philox_seed, doff, wq0, n0 + 32 * t, lane);
+#pragma unroll
+        for (int u = 0; u < 4; ++u) rb[u] = dropout_group_bytes(dscr, r, hh, u);
+      }
+      f32x16_t pt;
+#pragma unroll
+      for (int g = 0; g < 16; ++g) {
+        pt[g] = fast_exp2(fmaf(st[t][g], c, -ms));
+        ls[g & 3] = (t == 0 && g < 4) ? pt[g] : ls[g & 3] + pt[g];
+        if constexpr (DROPOUT) pt[g] = dropout_keep(rb[g >> 2], g & 3, s.keep_u8) ? pt[g] : 0.f;
+      }
+      pf[2 * t] = pack_frag<BF16>(pt, 0);
+      pf[2 * t + 1] = pack_frag<BF16>(pt, 1);
+    }
+    return (ls[0] + ls[1]) + (ls[2] + ls[3]);
+  };
+  // Deferred max without computing it: while every lane's partial sum of P over the tile stays
+  // <= 2^kFwdRescaleThr, every P is <= 2^kFwdRescaleThr (and finite), which is all the deferred-max
+  // rule needs.  A tile that exceeds it (a score jump, or +inf) takes the slow path below.
+  auto guard_ok = [&](float ls) { return !__any(!(ls <= kFwdSumThr)); };
+  // Slow path (wave-uniform, rare): recompute S of tile nb (still resident in the K ring), move the
+  // running max to the true max, rescale O / l_run, and redo P.  NaN sums (NaN inputs) also land
+  // here and end as the reference's NaN / +inf LSE through the normal epilogue.
+  auto refit = [&](int nb, i16x8_t (&pf)[2 * NT]) {
+    asm volatile("; refit" ::: "memory");   // not speculated into the fast path (if-conversion)
+    f32x16_t st[NT];
+    qk(kslot(nb), st);
+    float mx[4] = {kNegInf, kNegInf, kNegInf, kNegInf};
+#pragma unroll
+    for (int t = 0; t < NT; ++t)
+#pragma unroll
+      for (int g = 0; g < 16; ++g) mx[g & 3] = fmaxf(mx[g & 3], st[t][g]);
+    const float mt = half_swap_max(fmaxf(fmaxf(mx[0], mx[1]), fmaxf(mx[2], mx[3])));
+    const float m_new = fmaxf(m_run, mt);
+    const float alpha = fast_exp2((m_run - m_new) * c);
+    l_run *= alpha;
+#pragma unroll
+    for (int t = 0; t < NP; ++t)
+#pragma unroll
+      for (int g = 0; g < 16; ++g) o[t][g] *= alpha;
+    m_run = m_new;
+    return softmax_fast(st, pf, nb * BN);
+  };
   // O^T[d][q] += V^T[d][key] P^T[key][q], one 32-wide d tile at a time
   auto pv = [&](int vt_off, const i16x8_t (&pf)[2 * NT]) {
     const TileAddr ta(lb, vt_off);
@@ -285,32 +339,32 @@ __global__ void __launch_bounds__(FwdTile<D>::NW * 64, FwdTile<D>::MINB) fwd_ker
   if (nfast > 0) {
     f32x16_t sa[NT], sb[NT];
     qk(kslot(0), sa);
-    float mt = rowmax(sa);
+    rescale(rowmax(sa));   // first tile: running max from an explicit max pass
     auto body = [&](int nb, f32x16_t (&scur)[NT], f32x16_t (&snxt)[NT]) {
       if (nb + 3 < nblk) issue(nb + 3);
-      rescale(mt);
       i16x8_t pf[2 * NT];
-      softmax_pack(scur, pf, nb * BN);
+      float ls = softmax_fast(scur, pf, nb * BN);
       // tile nb+1 is resident (possibly past nblk: then its scores are simply discarded); its
       // MFMAs are independent of the softmax above, so the two interleave in this basic block
       qk(kslot(nb + 1), snxt);
+      if (!guard_ok(ls)) ls = refit(nb, pf);
+      l_run += ls;
       __builtin_amdgcn_sched_barrier(0);   // bound the V-read hoisting (register pressure)
       pv(vslot(nb), pf);
-      mt = rowmax(snxt);
       tile_sync(nb + 3 < nblk);
     };
     // staggered half: PV(nb-1) first (its P fragments carried across the barrier), then the
-    // softmax of nb and QK(nb+1); the rescale for nb follows the late PV, so O is complete up to
-    // nb-1 whenever it is scaled
+    // softmax of nb and QK(nb+1); a refit of nb follows the late PV, so O is complete up to nb-1
+    // whenever it is scaled
     i16x8_t pfp[2 * NT];
     auto body_late = [&](int nb, f32x16_t (&scur)[NT], f32x16_t (&snxt)[NT]) {
       if (nb + 3 < nblk) issue(nb + 3);
       if (nb > 0) pv(vslot(nb - 1), pfp);
       __builtin_amdgcn_sched_barrier(0);
-      rescale(mt);
-      softmax_pack(scur, pfp, nb * BN);
+      float ls = softmax_fast(scur, pfp, nb * BN);
       qk(kslot(nb + 1), snxt);
-      mt = rowmax(snxt);
+      if (!guard_ok(ls)) ls = refit(nb, pfp);
+      l_run += ls;
       tile_sync(nb + 3 < nblk);
     };
     int nb = 0;
