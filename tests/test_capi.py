@@ -111,3 +111,17 @@ def test_product_path_does_not_import_oracle():
                 src = open(os.path.join(dirpath, f)).read()
                 assert not re.search(r"^\s*(import|from)\s+oracle", src, flags=re.M), f
                 assert "attention_ref" not in src, f
+
+
+def test_mha_module_surface_on_cpu():
+    """The modules construct without a GPU and refuse the reference options outside this build."""
+    from flash_attn.modules.mha import MHA, FlashCrossAttention, FlashSelfAttention
+
+    FlashSelfAttention(causal=True, attention_dropout=0.1)
+    FlashCrossAttention()
+    m = MHA(128, 4, num_heads_kv=2)
+    assert m.Wqkv.out_features == 32 * (4 + 2 * 2)
+    with pytest.raises(NotImplementedError, match="rotary_emb_dim"):
+        MHA(128, 4, rotary_emb_dim=16)
+    with pytest.raises(AssertionError):
+        FlashSelfAttention()(torch.randn(1, 8, 3, 2, 64))

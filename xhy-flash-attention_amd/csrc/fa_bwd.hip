@@ -193,14 +193,18 @@ __global__ void __launch_bounds__(DkdvTile<D>::NW * 64, 1) bwd_dkdv_kernel(const
   const int group = s.h / s.hk;
 
   const int nheads_grid = p.gqa_reduce ? s.hk : s.h;
-  const int bidb = blockIdx.x / nheads_grid;
-  const int hx = blockIdx.x - bidb * nheads_grid;
+  // XCD-aware order: the key blocks of one (batch, kv-head) run together on one XCD and read the
+  // same Q / dO slices at about the same time (8.7% faster at C3 than head-fastest order)
+  int bhx, nblk_idx;
+  xcd_order(blockIdx.x, s.b * nheads_grid, p.num_n_blocks, bhx, nblk_idx);   // heaviest key block first
+  const int bidb = bhx / nheads_grid;
+  const int hx = bhx - bidb * nheads_grid;
   const int kvh = p.gqa_reduce ? hx : hx / group;
   const int h_begin = p.gqa_reduce ? hx * group : hx;
   const int nh = p.gqa_reduce ? group : 1;
   const SeqGeom geo = seq_geom(p, bidb);
   const int sq = geo.sq, sk = geo.sk;
-  const int n0 = blockIdx.y * BKN;
+  const int n0 = nblk_idx * BKN;
   if (n0 >= sk) return;
   const int dlim = s.d;
 
@@ -234,9 +238,14 @@ __global__ void __launch_bounds__(DkdvTile<D>::NW * 64, 1) bwd_dkdv_kernel(const
     voff_q[j] = dma_voff<BQ>(wave + j * NW, lane, p.q_row, dlim);
     voff_o[j] = dma_voff<BQ>(wave + j * NW, lane, p.do_row, dlim);
   }
+  // Sweep order: the query slices of one head, then the next head of the GQA group.  (Last slice
+  // first with the heads innermost -- every key block then starts on the same slice -- measured 3.5%
+  // slower at C3 than this order under xcd_order.)
+  auto slice_head = [&](int it) { return it / ns; };
+  auto slice_q0 = [&](int it) { return (m_first + it % ns) * BQ; };
   auto issue = [&](int it) {
-    const int hq = h_begin + it / ns;
-    const int q0 = (m_first + it % ns) * BQ;
+    const int hq = h_begin + slice_head(it);
+    const int q0 = slice_q0(it);
     char* qdst = smem + (it % 3) * QSLOT;
     char* odst = smem + OBASE + (it & 1) * QTILE;
     const u16* Qp = (const u16*)p.q + geo.q_off + (int64_t)hq * p.q_head + (int64_t)q0 * p.q_row;
@@ -391,8 +400,8 @@ __global__ void __launch_bounds__(DkdvTile<D>::NW * 64, 1) bwd_dkdv_kernel(const
   f32x16_t sp[NQT];  // S of this slice (P waves) / dP'' of the previous slice (dS waves)
   for (int it = 0; it < total; ++it) {
     if (it + 1 < total) issue(it + 1);
-    const int q0 = (m_first + it % ns) * BQ;
-    const int it_head = it / ns;   // query head of this slice within the group
+    const int q0 = slice_q0(it);
+    const int it_head = slice_head(it);   // query head of this slice within the group
     const int qs = (it % 3) * QSLOT;
     const float* lt = (const float*)(smem + qs + QTILE);
     const int os = OBASE + (it & 1) * QTILE;
@@ -471,11 +480,14 @@ __global__ void __launch_bounds__(DqTile<D>::NW * 64, DqTile<D>::MINB) bwd_dq_ke
   const int wave = wave_uniform(tid >> 6);
   const int r = lane & 31, hh = lane >> 5;
   const LdsBases lb(lane);
-  const int bidb = blockIdx.x / s.h;
-  const int head = blockIdx.x - bidb * s.h;
-  const int kvh = head / (s.h / s.hk);
   const int num_m = (s.seqlen_q + BM - 1) / BM;
-  const int m_block = num_m - 1 - (int)blockIdx.y;   // heaviest causal blocks first
+  // head-fastest, heaviest causal block first (as the forward; xcd_order measured 5% slower here)
+  const int bh = blockIdx.x % (s.b * s.h);
+  const int m_idx = blockIdx.x / (s.b * s.h);
+  const int bidb = bh / s.h;
+  const int head = bh - bidb * s.h;
+  const int kvh = head / (s.h / s.hk);
+  const int m_block = num_m - 1 - m_idx;   // heaviest causal block of a head first
   const SeqGeom geo = seq_geom(p, bidb);
   const int sq = geo.sq, sk = geo.sk;
   const int m0 = m_block * BM;
@@ -651,13 +663,13 @@ template <bool BF16, int D, bool CAUSAL, bool DROPOUT>
 static void run_bwd(const BwdParams& p, hipStream_t stream) {
   const int nheads_grid = p.gqa_reduce ? p.s.hk : p.s.h;
   {
-    dim3 grid(p.s.b * nheads_grid, p.num_n_blocks);
+    dim3 grid(p.s.b * nheads_grid * p.num_n_blocks);   // 1-D, xcd_order
     prof_begin(kTimeBwdMain, stream);
     hipLaunchKernelGGL((bwd_dkdv_kernel<BF16, D, CAUSAL, DROPOUT>), grid, dim3(DkdvTile<D>::NW * 64), 0, stream, p);
     prof_end(kTimeBwdMain, stream);
   }
   {
-    dim3 grid(p.s.b * p.s.h, (p.s.seqlen_q + DqTile<D>::BM - 1) / DqTile<D>::BM);
+    dim3 grid(p.s.b * p.s.h * ((p.s.seqlen_q + DqTile<D>::BM - 1) / DqTile<D>::BM));
     prof_begin(kTimeBwdDq, stream);
     hipLaunchKernelGGL((bwd_dq_kernel<BF16, D, CAUSAL, DROPOUT>), grid, dim3(DqTile<D>::NW * 64), 0, stream, p);
     prof_end(kTimeBwdDq, stream);
@@ -699,8 +711,10 @@ static void launch_bwd_t(const BwdParams& p, hipStream_t stream) {
 
 void launch_bwd(const BwdParams& p_in, bool is_bf16, hipStream_t stream) {
   if (p_in.s.b <= 0 || p_in.s.h <= 0 || p_in.s.seqlen_q <= 0) return;
-  if ((p_in.s.seqlen_q + kDqMinBM - 1) / kDqMinBM > 65535 || (p_in.s.seqlen_q + 15) / 16 > 65535)
-    throw std::runtime_error("flash_attn_bwd: seqlen_q too large for the grid");
+  if ((p_in.s.seqlen_q + 15) / 16 > 65535 ||
+      (int64_t)p_in.s.b * p_in.s.h * ((p_in.s.seqlen_q + kDqMinBM - 1) / kDqMinBM) > 0x7fffffff ||
+      (int64_t)p_in.s.b * p_in.s.h * p_in.num_n_blocks > 0x7fffffff)
+    throw std::runtime_error("flash_attn_bwd: problem too large for the grid");
   BwdParams p = p_in;
   // softmax_scale == 0 (uniform attention) would make -LSE / scale infinite: a tiny positive scale
   // gives the same P to fp32 precision (P deviates from uniform by 1e-30 |S|) and dQ, dK ~ 1e-30.

@@ -278,6 +278,24 @@ __device__ inline u32x4_t ld16(const void* p, bool valid) {
   return valid ? *(const u32x4_t*)p : z;
 }
 
+// XCD-aware workgroup order for a 1-D grid of nbh * nblk workgroups (nbh = batch x heads, nblk
+// blocks per head).  The dispatcher deals workgroups round-robin to the 8 XCDs (L % 8 share one,
+// MI355X_MICROARCH.md "Workgroup dispatch"), so the XCD of group j is given heads bh = j, j + 8, ...
+// one after another, each with all of its blocks in order: the workgroups that stream the same
+// head's K/V (or Q/dO) run together on one XCD and share its 4 MiB L2 instead of fetching the stream
+// once per XCD.  Falls back to head-fastest order when nbh is not a multiple of 8.
+__device__ inline void xcd_order(int L, int nbh, int nblk, int& bh, int& blk) {
+  if ((nbh & 7) == 0) {
+    const int i = L >> 3;
+    const int hl = i / nblk;
+    blk = i - hl * nblk;
+    bh = hl * 8 + (L & 7);
+  } else {
+    blk = L / nbh;
+    bh = L - blk * nbh;
+  }
+}
+
 // Accumulator element g -> row offset inside a 32x32 tile for lane half h.
 __device__ __host__ constexpr inline int acc_row(int g, int h) { return (g & 3) + 8 * (g >> 2) + 4 * h; }
 

@@ -25,7 +25,7 @@
 //     last tile): one basic block per tile holds QK^T(n+1) (MFMA), the exp / sum / pack of tile n
 //     (VALU) and PV(n) (MFMA), so the matrix pipe has independent work while the softmax runs.
 //   * Every LDS address is one of four per-lane bases + an immediate (fa_common.h LdsBases).
-//   * Heaviest causal query blocks are dispatched first (blockIdx.y reversed) to shorten the tail.
+//   * Heaviest causal query blocks are dispatched first (1-D grid, head-fastest) to shorten the tail.
 //   * Epilogue: v_permlane32_swap pairs column groups so each lane stores 16 bytes of its O row.
 //   * Waves 4-7 (the younger half of the workgroup) run at s_setprio 1 for the whole kernel.
 #include <stdexcept>
@@ -83,11 +83,15 @@ __global__ void __launch_bounds__(FwdTile<D>::NW * 64, FwdTile<D>::MINB) fwd_ker
   const int r = lane & 31, hh = lane >> 5;
   const LdsBases lb(lane);
 
-  const int bh = blockIdx.x;
+  // head-fastest, heaviest causal block first over the whole grid; with b * h a multiple of 8 every
+  // block of one head lands on the same XCD (L % 8).  Grouping a head's blocks in time as well
+  // (xcd_order, which the dK/dV kernel uses) measured 5% slower here: the causal tail grows.
+  const int bh = blockIdx.x % (s.b * s.h);
+  const int m_idx = blockIdx.x / (s.b * s.h);
   const int bidb = bh / s.h;
   const int head = bh - bidb * s.h;
   const int kvh = head / (s.h / s.hk);
-  const int m_block = p.num_m_blocks - 1 - (int)blockIdx.y;
+  const int m_block = p.num_m_blocks - 1 - m_idx;   // heaviest causal query block of a head first
 
   // ---- sequence geometry (reference BlockInfo, block_info.h:14-31) ----
   int sq = s.seqlen_q, sk = s.seqlen_k;
@@ -486,7 +490,7 @@ __global__ void __launch_bounds__(256) dmask_kernel(const FwdParams p) {
 
 template <bool BF16, int D, bool CAUSAL, bool DROPOUT>
 static void run_fwd(const FwdParams& p, hipStream_t stream) {
-  dim3 grid(p.s.b * p.s.h, p.num_m_blocks);
+  dim3 grid(p.s.b * p.s.h * p.num_m_blocks);   // 1-D: heads fastest, heaviest query block first
   prof_begin(kTimeFwd, stream);
   hipLaunchKernelGGL((fwd_kernel<BF16, D, CAUSAL, DROPOUT>), grid, dim3(FwdTile<D>::NW * 64), 0, stream, p);
   prof_end(kTimeFwd, stream);
@@ -525,7 +529,8 @@ void fwd_block_size(int d, int* block_m, int* block_n) {
 void launch_fwd(const FwdParams& p, bool is_bf16, hipStream_t stream) {
   if (p.s.b <= 0 || p.s.h <= 0) return;
   if (p.num_m_blocks <= 0) return;
-  if (p.num_m_blocks > 65535) throw std::runtime_error("flash_attn_fwd: seqlen_q too large for grid.y");
+  if ((int64_t)p.s.b * p.s.h * p.num_m_blocks > 0x7fffffff)
+    throw std::runtime_error("flash_attn_fwd: batch * heads * query blocks too large for the grid");
   if (p.p_out != nullptr && (p.p_rows > 65535 * 4 || p.s.b * p.s.h > 65535))
     throw std::runtime_error("flash_attn_fwd: return_softmax grid too large");
   if (is_bf16) dispatch_fwd<true>(p, stream); else dispatch_fwd<false>(p, stream);
