@@ -344,9 +344,9 @@ def test_capi_expanded_gqa_matches_fused_reduction():
     torch.testing.assert_close(dv_sum, dv.float(), atol=3e-2, rtol=2e-2)
 
 
-def test_return_softmax_requires_dropout_and_masks_rejected():
-    """Reference mha_fwd: return_softmax only with p_dropout > 0 (flash_api.cpp:276-279); the
-    Paddle dense mask / FlashMask arguments of the C ABI are out of scope and rejected loudly."""
+def test_return_softmax_requires_dropout_and_mask_needs_dims():
+    """Reference mha_fwd: return_softmax only with p_dropout > 0 (flash_api.cpp:276-279); a dense
+    Paddle mask without its mask_dims is rejected loudly (mask parity: tests/test_mask_gpu.py)."""
     import flash_attn_2_cuda as m
 
     q = torch.randn(1, 64, 2, 64, device=DEV, dtype=torch.float16)
@@ -360,7 +360,7 @@ def test_return_softmax_requires_dropout_and_masks_rejected():
                                1, 64, 64, 128, 128, 2, 2, 64, 64, 0.0, 0.125, 1.0, False, False, False,
                                m._stream(q), 0, 0, m._ptr(lse), None, None, None, None, None, None,
                                None, *st)
-    assert not ok and b"attn_mask" in m._lib.flash_attn_error()
+    assert not ok and b"mask_dims" in m._lib.flash_attn_error()
 
 
 # ------------------------------------------------------------------------------------------------

@@ -1,0 +1,155 @@
+"""GPU parity of the Paddle dense additive mask through the C ABI.
+
+Reference semantics (csrc/capi/flash_attn.cu:623-624, flash_fwd_kernel.h:640-660, softmax.h:361-379,
+flash_bwd_kernel.h:2421-2424): the raw scores Q K^T get mask[b][h % mask_h][q % mask_sq][k] *
+softmax_unscale added before the softmax scale, in the forward and in the backward's recomputed P.
+The mask has the input dtype and rows of seqlen_k elements.  The oracle below restates that in
+fp32 (``ref``) and in the input dtype (``pt``) and the kernels must meet the reference's 2x rule.
+mask_sq = seqlen_q is the reference's layout; mask_sq = 1 (one row broadcast to every query) is
+this build's reading of the modulus -- the reference kernel indexes past such a mask, so that case
+is parity-unpinned and checked against the broadcast restatement only.
+"""
+import math
+
+import pytest
+import torch
+
+from oracle.attention_ref import check_within_bound
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda"
+
+
+@pytest.fixture(scope="module", autouse=True)
+def _need_gpu():
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    import flash_attn_2_cuda  # noqa: F401
+
+
+def _mask_ref(q, k, v, mask, unscale, scale, causal, upcast=True):
+    """out (b, sq, h, d) of softmax(scale * (QK^T + M * unscale)) V with the kernel's indexing."""
+    dt = q.dtype
+    if upcast:
+        q, k, v, mask = q.float(), k.float(), v.float(), mask.float()
+    b, sq, h, d = q.shape
+    hk = k.shape[2]
+    k = k.repeat_interleave(h // hk, dim=2)
+    v = v.repeat_interleave(h // hk, dim=2)
+    mh, msq = mask.shape[1], mask.shape[2]
+    hi = torch.arange(h, device=q.device) % mh
+    qi = torch.arange(sq, device=q.device) % msq
+    m = mask[:, hi][:, :, qi]                                  # (b, h, sq, sk)
+    s = torch.einsum("bqhd,bkhd->bhqk", q, k) + m * unscale
+    s = s * scale
+    if causal:
+        s = s.masked_fill(torch.triu(torch.ones(sq, k.shape[1], dtype=torch.bool, device=q.device), 1),
+                          float("-inf"))
+    p = torch.softmax(s, dim=-1)
+    return torch.einsum("bhqk,bkhd->bqhd", p, v).to(dt)
+
+
+def _capi_fwd_bwd(q, k, v, mask, unscale, scale, causal, dout):
+    import flash_attn_2_cuda as m
+
+    b, sq, h, d = q.shape
+    sk, hk = k.shape[1], k.shape[2]
+    out = torch.empty_like(q)
+    lse = torch.empty(b, h, sq, device=DEV, dtype=torch.float32)
+    rng = torch.empty(2, device=DEV, dtype=torch.int64)
+    dims = torch.tensor(list(mask.shape), dtype=torch.int64)        # host array, as Paddle passes it
+    dims_p = dims.numpy().ctypes.data
+    st = lambda t: (t.stride(1), t.stride(2), t.stride(0))  # noqa: E731 (row, head, batch)
+    (qr, qh, qb), (kr, kh, kb), (vr, vh, vb), (orr, oh, ob) = st(q), st(k), st(v), st(out)
+    sq_r, sk_r = (sq + 127) // 128 * 128, (sk + 127) // 128 * 128
+    P = m._ptr
+    bf16 = q.dtype == torch.bfloat16
+    ok = m._lib.flash_attn_fwd(P(q), P(k), P(v), P(rng), P(out), None, P(lse), b, sq, sk, sq_r, sk_r,
+                               h, hk, d, d, 0.0, scale, unscale, causal, False, bf16,
+                               m._stream(q), 0, 0, P(mask), dims_p, None, None, None, None, None, None,
+                               qr, kr, vr, qh, kh, vh, orr, oh, qb, kb, vb, ob)
+    assert ok, m._lib.flash_attn_error()
+    dq, dk, dv = torch.empty_like(q), torch.empty_like(k), torch.empty_like(v)
+    softmax_d = torch.empty(b, h, sq_r, device=DEV)
+    (dqr, dqh, dqb), (dkr, dkh, dkb), (dvr, dvh, dvb), (dor, doh, dob) = st(dq), st(dk), st(dv), st(dout)
+    ok = m._lib.flash_attn_bwd_gqa(P(dout), P(q), P(k), P(v), P(out), P(softmax_d), P(lse), P(rng),
+                                   P(dq), P(dk), P(dv), None, b, sq, sk, sq_r, sk_r, h, hk, d, d,
+                                   0.0, scale, unscale, causal, bf16, 1,
+                                   m._stream(q), 0, 0, P(mask), dims_p, None, None, None, None, None,
+                                   None, qr, kr, vr, qh, kh, vh, orr, oh, qb, kb, vb, ob,
+                                   dqr, dkr, dvr, dqh, dkh, dvh, dor, doh, dqb, dkb, dvb, dob)
+    assert ok, m._lib.flash_attn_error()
+    torch.cuda.synchronize()
+    return out, dq, dk, dv
+
+
+@pytest.mark.parametrize("dtype", [torch.float16, torch.bfloat16])
+@pytest.mark.parametrize("causal", [False, True])
+@pytest.mark.parametrize("mask_heads", ["one", "all"])
+@pytest.mark.parametrize("mask_rows", ["all", "one"])
+@pytest.mark.parametrize("d,sq,sk,h,hk", [(64, 200, 333, 4, 2), (128, 513, 513, 4, 4), (256, 130, 97, 2, 1)])
+def test_dense_mask_fwd_bwd(d, sq, sk, h, hk, mask_rows, mask_heads, causal, dtype):
+    torch.manual_seed(0)
+    b = 2
+    q = torch.randn(b, sq, h, d, device=DEV, dtype=dtype)
+    k = torch.randn(b, sk, hk, d, device=DEV, dtype=dtype)
+    v = torch.randn(b, sk, hk, d, device=DEV, dtype=dtype)
+    dout = torch.randn(b, sq, h, d, device=DEV, dtype=dtype)
+    mh = 1 if mask_heads == "one" else h
+    msq = 1 if mask_rows == "one" else sq
+    # additive mask: a smooth bias plus Paddle-style large negatives (-3000 * unscale stays finite
+    # in fp16, so the low-precision estimate never sees an all -inf row)
+    mask = torch.randn(b, mh, msq, sk, device=DEV) * 2.0
+    mask = mask.masked_fill(torch.rand(b, mh, msq, sk, device=DEV) < 0.2, -3000.0).to(dtype)
+    scale = d ** -0.5
+    unscale = 1.0 / scale
+    out, dq, dk, dv = _capi_fwd_bwd(q, k, v, mask, unscale, scale, causal, dout)
+
+    qc, kc, vc = (x.clone().requires_grad_() for x in (q, k, v))
+    ref = _mask_ref(qc, kc, vc, mask, unscale, scale, causal)
+    pt = _mask_ref(qc, kc, vc, mask, unscale, scale, causal, upcast=False)
+    ok, err, bound = check_within_bound(out, ref, pt)
+    assert ok, f"out: {err:.3e} > {bound:.3e}"
+    gr = torch.autograd.grad(ref, (qc, kc, vc), dout)
+    gp = torch.autograd.grad(pt, (qc, kc, vc), dout)
+    for name, got, r, p in zip(("dq", "dk", "dv"), (dq, dk, dv), gr, gp):
+        ok, err, bound = check_within_bound(got, r, p, floor=1e-3)
+        assert ok, f"{name}: {err:.3e} > {bound:.3e}"
+
+
+def test_dense_mask_zero_is_no_mask():
+    """An all-zero mask gives the unmasked result (the masked path only adds)."""
+    from flash_attn import flash_attn_func
+
+    torch.manual_seed(0)
+    q, k, v = (torch.randn(2, 300, 4, 128, device=DEV, dtype=torch.bfloat16) for _ in range(3))
+    dout = torch.randn_like(q)
+    mask = torch.zeros(2, 1, 300, 300, device=DEV, dtype=torch.bfloat16)
+    out, dq, dk, dv = _capi_fwd_bwd(q, k, v, mask, math.sqrt(128), 128 ** -0.5, True, dout)
+    qr, kr, vr = (x.clone().requires_grad_() for x in (q, k, v))
+    o2 = flash_attn_func(qr, kr, vr, causal=True)
+    g2 = torch.autograd.grad(o2, (qr, kr, vr), dout)
+    torch.testing.assert_close(out, o2, atol=2e-3, rtol=0)
+    for a, bb in zip((dq, dk, dv), g2):
+        torch.testing.assert_close(a, bb, atol=4e-3, rtol=0)
+
+
+def test_flashmask_and_bad_mask_dims_rejected():
+    import flash_attn_2_cuda as m
+
+    q = torch.randn(1, 64, 2, 64, device=DEV, dtype=torch.float16)
+    lse = torch.empty(1, 2, 64, device=DEV)
+    out = torch.empty_like(q)
+    st = (q.stride(1), q.stride(1), q.stride(1), q.stride(2), q.stride(2), q.stride(2), out.stride(1),
+          out.stride(2), q.stride(0), q.stride(0), q.stride(0), out.stride(0))
+    P = m._ptr
+    ok = m._lib.flash_attn_fwd(P(q), P(q), P(q), None, P(out), None, P(lse), 1, 64, 64, 128, 128, 2, 2,
+                               64, 64, 0.0, 0.125, 8.0, False, False, False, m._stream(q), 0, 0,
+                               None, None, P(lse), None, None, None, None, None, *st)
+    assert not ok and b"FlashMask" in m._lib.flash_attn_error()
+    mask = torch.zeros(1, 1, 64, 32, device=DEV, dtype=torch.float16)   # wrong key extent
+    dims = torch.tensor([1, 1, 64, 32], dtype=torch.int64)
+    ok = m._lib.flash_attn_fwd(P(q), P(q), P(q), None, P(out), None, P(lse), 1, 64, 64, 128, 128, 2, 2,
+                               64, 64, 0.0, 0.125, 8.0, False, False, False, m._stream(q), 0, 0,
+                               P(mask), dims.numpy().ctypes.data, None, None, None, None, None, None, *st)
+    assert not ok and b"mask_dims" in m._lib.flash_attn_error()

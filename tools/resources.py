@@ -7,7 +7,7 @@ import sys
 
 src = sys.argv[1]
 out = subprocess.run(["/opt/rocm/bin/hipcc", "-O3", "-std=c++17", "-fPIC", "--offload-arch=gfx950", "-x", "hip",
-                      "-c", src, "-o", "/tmp/_res.o", "-Rpass-analysis=kernel-resource-usage"],
+                      "-c", src, "-o", "/tmp/_res.o", "-Rpass-analysis=kernel-resource-usage"] + [a for a in sys.argv[2:] if a.startswith("-f") or a.startswith("-D")],
                      capture_output=True, text=True).stderr
 cur, rows = None, []
 for line in out.splitlines():

@@ -343,10 +343,15 @@ __global__ void __launch_bounds__(DkdvTile<D>::NW * 64, 1) bwd_dkdv_kernel(const
         f32x4_t pv;
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
-          float x = fast_exp2(sp[qi][4 * u + j] * c);
+          float x;
           if constexpr (MASK) {
             const int q = q0 + 32 * qi + 8 * u + 4 * hh + j;
-            x = (key >= sk || q >= sq || (CAUSAL && key > q)) ? 0.f : x;
+            const bool out = key >= sk || q >= sq || (CAUSAL && key > q);
+            const u16* mrow = out ? nullptr : mask_row_ptr(s, bidb, h_begin + it_head, q);
+            const float add = mrow != nullptr ? E::to_f32(mrow[key]) * s.mask_unscale : 0.f;
+            x = out ? 0.f : fast_exp2((sp[qi][4 * u + j] + add) * c);
+          } else {
+            x = fast_exp2(sp[qi][4 * u + j] * c);
           }
           if constexpr (DROPOUT) {
             const bool keep = dropout_keep(rb[u], j, s.keep_u8);
@@ -420,7 +425,7 @@ __global__ void __launch_bounds__(DkdvTile<D>::NW * 64, 1) bwd_dkdv_kernel(const
       }
     phase1(pwave ? qs : os, sp);                       // S' = Q K^T - LSE/scale  /  dP'' = D - dO V^T
     if (pwave) {
-      const bool fast = (q0 + BQ <= sq) && (n0 + BKN <= sk) && (!CAUSAL || q0 >= n0 + BKN - 1);
+      const bool fast = !s.mask && (q0 + BQ <= sq) && (n0 + BKN <= sk) && (!CAUSAL || q0 >= n0 + BKN - 1);
       if (fast) p_step(std::false_type{}, sp, q0, it_head, xw_of(it), fr);
       else p_step(std::true_type{}, sp, q0, it_head, xw_of(it), fr);
     }
@@ -523,7 +528,8 @@ __global__ void __launch_bounds__(DqTile<D>::NW * 64, DqTile<D>::MINB) bwd_dq_ke
 
   const int n_end = CAUSAL ? min(sk, m0 + BM) : sk;
   const int nblk = n_end > 0 ? (n_end + BN - 1) / BN : 0;
-  const int nfast = min(nblk, (CAUSAL ? min(sk, m0 + 1) : sk) / BN);
+  const int nfast = s.mask ? 0 : min(nblk, (CAUSAL ? min(sk, m0 + 1) : sk) / BN);
+  const u16* mrow = mask_row_ptr(s, bidb, head, q_ok ? qi : 0);
 
   int voff_k[PPW], voff_v[PPW];
 #pragma unroll
@@ -589,10 +595,14 @@ __global__ void __launch_bounds__(DqTile<D>::NW * 64, DqTile<D>::MINB) bwd_dq_ke
       }
 #pragma unroll
       for (int g = 0; g < 16; ++g) {
-        float pv = fast_exp2(fmaf(st[t][g], c, -lse_l2));
+        float pv;
         if constexpr (MASK) {
           const int kk = n0 + t * 32 + acc_row(g, hh);
-          if (kk >= sk || (CAUSAL && kk > qi)) pv = 0.f;
+          const bool out = kk >= sk || (CAUSAL && kk > qi);
+          const float add = (!out && mrow != nullptr) ? E::to_f32(mrow[kk]) * s.mask_unscale : 0.f;
+          pv = out ? 0.f : fast_exp2(fmaf(st[t][g] + add, c, -lse_l2));
+        } else {
+          pv = fast_exp2(fmaf(st[t][g], c, -lse_l2));
         }
         // dS^T = P^T o (dP^T - D); dropped elements: -P D (reference flash_bwd_kernel.h:897-899)
         if constexpr (DROPOUT)

@@ -70,7 +70,7 @@ void check_common(int batch_size, int num_heads, int num_heads_k, int head_size,
   FA_CHECK(head_size <= 256);
   FA_CHECK(num_heads % num_heads_k == 0);
   FA_CHECK(head_size_rounded >= head_size);
-  if (attn_mask != nullptr) throw std::runtime_error("attn_mask (dense Paddle mask) is not supported by the MI355X build");
+  (void)attn_mask;
   if (flashmask != nullptr) throw std::runtime_error("FlashMask is not supported by the MI355X build");
   FA_CHECK(p_dropout >= 0.f && p_dropout < 1.f);
 }
@@ -96,6 +96,21 @@ fa::AttnShape make_shape(int b, int h, int hk, int sq, int sk, int d, float scal
   return s;
 }
 
+// Dense additive mask (reference capi flash_attn.cu:623-624: mask_head_mod_size = mask_dims[1],
+// mask_seq_q_mod_size = mask_dims[2]; the kernels index rows with seqlen_k as the stride,
+// flash_fwd_kernel.h:640-643).  mask_dims = {batch, heads or a divisor pattern, rows, seqlen_k}.
+void set_mask(fa::AttnShape& s, const void* attn_mask, const int64_t* mask_dims, float unscale) {
+  if (attn_mask == nullptr) return;
+  FA_CHECK(mask_dims != nullptr);
+  if (mask_dims[0] != s.b || mask_dims[1] < 1 || mask_dims[2] < 1 || mask_dims[3] != s.seqlen_k)
+    throw std::runtime_error("attn_mask: mask_dims must be {batch, heads_mod >= 1, rows_mod >= 1, seqlen_k}");
+  s.mask = attn_mask;
+  s.mask_h = (int)mask_dims[1];
+  s.mask_sq = (int)mask_dims[2];
+  s.mask_row = mask_dims[3];
+  s.mask_unscale = unscale;
+}
+
 bool fwd_impl(const void* q, const void* k, const void* v, const int32_t* cu_q, const int32_t* cu_k,
               void* rng_state, void* out, void* softmax_ptr, void* lse, int b, int sq, int sk,
               int sq_r, int sk_r,
@@ -103,7 +118,8 @@ bool fwd_impl(const void* q, const void* k, const void* v, const int32_t* cu_q, 
               bool return_softmax, bool is_bf16, hipStream_t stream, uint64_t seed, uint64_t offset,
               const void* attn_mask, const void* flashmask, int q_row, int k_row, int v_row,
               int q_head, int k_head, int v_head, int o_row, int o_head, int q_batch, int k_batch,
-              int v_batch, int o_batch, bool padded) {
+              int v_batch, int o_batch, bool padded, const int64_t* mask_dims = nullptr,
+              float unscale = 1.f) {
   FA_BEGIN
   check_common(b, h, hk, d, d_r, p_dropout, attn_mask, flashmask);
   // reference mha_fwd: "return_softmax is only supported when p_dropout > 0.0" (flash_api.cpp:276-279)
@@ -113,6 +129,9 @@ bool fwd_impl(const void* q, const void* k, const void* v, const int32_t* cu_q, 
   fa::FwdParams p;
   std::memset(&p, 0, sizeof(p));
   p.s = make_shape(b, h, hk, sq, sk, d, scale, causal, cu_q, cu_k, padded, p_dropout, seed, offset);
+  set_mask(p.s, attn_mask, mask_dims, unscale);
+  if (return_softmax && attn_mask != nullptr)
+    throw std::runtime_error("return_softmax with attn_mask is not supported by the MI355X build");
   if (return_softmax) {
     FA_CHECK(softmax_ptr != nullptr && sq_r >= sq && sk_r >= sk);
     p.p_out = softmax_ptr;
@@ -143,7 +162,8 @@ bool bwd_impl(const void* dout, const void* q, const void* k, const void* v, con
               int o_head, int q_batch, int k_batch, int v_batch, int o_batch, int dq_row,
               int dk_row, int dv_row, int dq_head, int dk_head, int dv_head, int do_row,
               int do_head, int dq_batch, int dk_batch, int dv_batch, int do_batch, bool padded,
-              bool gqa_reduce, void* rng_state, uint64_t seed, uint64_t offset) {
+              bool gqa_reduce, void* rng_state, uint64_t seed, uint64_t offset,
+              const int64_t* mask_dims = nullptr, float unscale = 1.f) {
   FA_BEGIN
   check_common(b, h, hk, d, d_r, p_dropout, attn_mask, flashmask);
   FA_CHECK(dout && q && k && v && out && softmax_d && lse && dq && dk && dv);
@@ -152,6 +172,7 @@ bool bwd_impl(const void* dout, const void* q, const void* k, const void* v, con
   fa::BwdParams p;
   std::memset(&p, 0, sizeof(p));
   p.s = make_shape(b, h, hk, sq, sk, d, scale, causal, cu_q, cu_k, padded, p_dropout, seed, offset);
+  set_mask(p.s, attn_mask, mask_dims, unscale);
   p.s.lse_pitch = sq;
   if (p.s.dropout && rng_state != nullptr) {   // reference capi flash_attn.cu:943-947
     const uint64_t st[2] = {seed, offset};
@@ -209,7 +230,6 @@ bool flash_attn_fwd(const void* const q, const void* const k, const void* const 
                     const int q_head_stride, const int k_head_stride, const int v_head_stride,
                     const int o_row_stride, const int o_head_stride, const int q_batch_stride,
                     const int k_batch_stride, const int v_batch_stride, const int o_batch_stride) {
-  (void)softmax_unscale; (void)mask_dims;
   (void)flashmask_dims; (void)flashmask_upend_ptr; (void)flashmask_downend_ptr;
   (void)flashmask_upstart_ptr; (void)flashmask_maxmin_ptr;
   return fwd_impl(q, k, v, nullptr, nullptr, rng_state, out, softmax_ptr, softmax_lse_ptr,
@@ -219,7 +239,7 @@ bool flash_attn_fwd(const void* const q, const void* const k, const void* const 
                   stream, seed, offset, attn_mask, flashmask_downstart_ptr, q_row_stride,
                   k_row_stride, v_row_stride, q_head_stride, k_head_stride, v_head_stride,
                   o_row_stride, o_head_stride, q_batch_stride, k_batch_stride, v_batch_stride,
-                  o_batch_stride, false);
+                  o_batch_stride, false, mask_dims, softmax_unscale);
 }
 
 bool flash_attn_varlen_fwd(const void* const q, const void* const k, const void* const v,
@@ -240,7 +260,6 @@ bool flash_attn_varlen_fwd(const void* const q, const void* const k, const void*
                            const int o_head_stride, const int q_batch_stride,
                            const int k_batch_stride, const int v_batch_stride,
                            const int o_batch_stride, bool varlen_padded_input) {
-  (void)softmax_unscale; (void)mask_dims;
   if (cu_seqlens_q == nullptr || cu_seqlens_k == nullptr) {
     set_error("flash_attn_varlen_fwd: cu_seqlens_q / cu_seqlens_k must not be null");
     return false;
@@ -252,7 +271,8 @@ bool flash_attn_varlen_fwd(const void* const q, const void* const k, const void*
                   return_softmax, is_bf16, stream, seed, offset, attn_mask, nullptr, q_row_stride,
                   k_row_stride, v_row_stride, q_head_stride, k_head_stride, v_head_stride,
                   o_row_stride, o_head_stride, q_batch_stride, k_batch_stride, v_batch_stride,
-                  o_batch_stride, varlen_padded_input);
+                  o_batch_stride, varlen_padded_input, static_cast<const int64_t*>(mask_dims),
+                  softmax_unscale);
 }
 
 #define FA_BWD_ARGS                                                                               \
@@ -279,8 +299,8 @@ bool flash_attn_varlen_fwd(const void* const q, const void* const k, const void*
       const int do_batch_stride
 
 #define FA_BWD_CALL(GQA)                                                                          \
-  (void)seqlen_k_rounded; (void)softmax_unscale; (void)num_splits;                                \
-  (void)mask_dims; (void)flashmask_dims; (void)flashmask_upend_ptr;                                \
+  (void)seqlen_k_rounded; (void)num_splits;                                                       \
+  (void)flashmask_dims; (void)flashmask_upend_ptr;                                                 \
   (void)flashmask_downend_ptr; (void)flashmask_upstart_ptr; (void)flashmask_maxmin_ptr;            \
   return bwd_impl(dout, q, k, v, out, softmax_d, softmax_lse, nullptr, nullptr, dq, dk, dv,        \
                   dq_accum, batch_size, seqlen_q, seqlen_k, seqlen_q_rounded, num_heads,           \
@@ -290,7 +310,8 @@ bool flash_attn_varlen_fwd(const void* const q, const void* const k, const void*
                   o_head_stride, q_batch_stride, k_batch_stride, v_batch_stride, o_batch_stride,   \
                   dq_row_stride, dk_row_stride, dv_row_stride, dq_head_stride, dk_head_stride,     \
                   dv_head_stride, do_row_stride, do_head_stride, dq_batch_stride, dk_batch_stride, \
-                  dv_batch_stride, do_batch_stride, false, GQA, rng_state, seed, offset)
+                  dv_batch_stride, do_batch_stride, false, GQA, rng_state, seed, offset,         \
+                  mask_dims, softmax_unscale)
 
 bool flash_attn_bwd(FA_BWD_ARGS) { FA_BWD_CALL(false); }
 bool flash_attn_bwd_gqa(FA_BWD_ARGS) { FA_BWD_CALL(true); }
@@ -317,7 +338,7 @@ bool flash_attn_bwd_gqa(FA_BWD_ARGS) { FA_BWD_CALL(true); }
       const int dv_batch_stride, const int do_batch_stride, const bool varlen_padded_input
 
 #define FA_VARLEN_BWD_CALL(GQA)                                                                   \
-  (void)seqlen_k_rounded; (void)softmax_unscale; (void)num_splits; (void)mask_dims;               \
+  (void)seqlen_k_rounded; (void)num_splits;                                                       \
   if (cu_seqlens_q == nullptr || cu_seqlens_k == nullptr) {                                        \
     set_error("flash_attn_varlen_bwd: cu_seqlens_q / cu_seqlens_k must not be null");             \
     return false;                                                                                  \
@@ -331,7 +352,7 @@ bool flash_attn_bwd_gqa(FA_BWD_ARGS) { FA_BWD_CALL(true); }
                   dq_row_stride, dk_row_stride, dv_row_stride, dq_head_stride, dk_head_stride,     \
                   dv_head_stride, do_row_stride, do_head_stride, dq_batch_stride, dk_batch_stride, \
                   dv_batch_stride, do_batch_stride, varlen_padded_input, GQA, rng_state, seed,     \
-                  offset)
+                  offset, mask_dims, softmax_unscale)
 
 bool flash_attn_varlen_bwd(FA_VARLEN_BWD_ARGS) { FA_VARLEN_BWD_CALL(false); }
 bool flash_attn_varlen_bwd_gqa(FA_VARLEN_BWD_ARGS) { FA_VARLEN_BWD_CALL(true); }

@@ -296,6 +296,16 @@ __device__ inline void xcd_order(int L, int nbh, int nblk, int& bh, int& blk) {
   }
 }
 
+// Row `q` of the dense additive mask for (batch, head), or nullptr when there is no mask / q is out
+// of range (AttnShape::mask; reference row_offset_mask, flash_fwd_kernel.h:640-643, with the query
+// index taken modulo mask_sq per row).
+template <typename Shape>
+__device__ inline const unsigned short* mask_row_ptr(const Shape& s, int bidb, int head, int q) {
+  if (s.mask == nullptr) return nullptr;
+  const int64_t r = ((int64_t)bidb * s.mask_h + head % s.mask_h) * s.mask_sq + q % s.mask_sq;
+  return (const unsigned short*)s.mask + r * s.mask_row;
+}
+
 // Accumulator element g -> row offset inside a 32x32 tile for lane half h.
 __device__ __host__ constexpr inline int acc_row(int g, int h) { return (g & 3) + 8 * (g >> 2) + 4 * h; }
 

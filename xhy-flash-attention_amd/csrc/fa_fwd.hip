@@ -139,8 +139,8 @@ __global__ void __launch_bounds__(FwdTile<D>::NW * 64, FwdTile<D>::MINB) fwd_ker
 
   const int n_end = CAUSAL ? min(sk, m0 + BM) : sk;
   const int nblk = n_end > 0 ? (n_end + BN - 1) / BN : 0;
-  // tiles [0, nfast) need no mask for any row of the workgroup
-  const int nfast = min(nblk, (CAUSAL ? min(sk, m0 + 1) : sk) / BN);
+  // tiles [0, nfast) need no mask for any row of the workgroup (none at all with a dense mask)
+  const int nfast = s.mask ? 0 : min(nblk, (CAUSAL ? min(sk, m0 + 1) : sk) / BN);
 
   // ---- LDS-DMA of K/V tiles: per-lane byte offsets of this wave's 1-KiB pieces ----
   // piece pc covers rows 16*(pc % (BN/16)) .. +15 of panel pc / (BN/16); lane l writes
@@ -397,12 +397,14 @@ __global__ void __launch_bounds__(FwdTile<D>::NW * 64, FwdTile<D>::MINB) fwd_ker
     if (active) {
       f32x16_t st[NT];
       qk(kslot(nb), st);
+      const u16* mrow = mask_row_ptr(s, bidb, head, qi < sq ? qi : 0);
 #pragma unroll
       for (int t = 0; t < NT; ++t)
 #pragma unroll
         for (int g = 0; g < 16; ++g) {
           const int key = n0 + t * 32 + acc_row(g, hh);
           if (key >= sk || (CAUSAL && key > qi)) st[t][g] = kNegInf;
+          else if (mrow != nullptr) st[t][g] += E::to_f32(mrow[key]) * s.mask_unscale;
         }
       rescale(rowmax(st));
       i16x8_t pf[2 * NT];

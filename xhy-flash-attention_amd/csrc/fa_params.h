@@ -33,6 +33,14 @@ struct AttnShape {
   float p_keep;             // keep probability 1 - p_dropout
   float rp_dropout;         // 1 / p_keep
   uint64_t philox_seed, philox_offset;   // the reference's (seed, offset) pair (rng_state)
+  // Paddle dense additive mask (reference Flash_fwd_params attn_mask_ptr / mask_head_mod_size /
+  // mask_seq_q_mod_size / unscale_softmax, flash.h; applied in softmax.h:361-379): raw scores
+  // QK^T += mask[b][h % mask_h][q % mask_sq][k] * mask_unscale, in the input dtype, row stride
+  // mask_row (= seqlen_k).  nullptr: no mask.
+  const void* mask;
+  int mask_h, mask_sq;
+  int64_t mask_row;
+  float mask_unscale;
 };
 
 struct FwdParams {
