@@ -18,9 +18,14 @@
  *   - a call returns false on error and leaves a thread-local message readable
  *     through flash_attn_error();
  *   - head_size % 8 == 0, head_size <= 256, num_heads % num_heads_k == 0;
- *   - the Paddle dense-mask / FlashMask arguments are accepted for ABI
- *     compatibility but must be NULL (out of scope for this build: the call
- *     fails with a message otherwise);
+ *   - attn_mask (dense additive Paddle mask, input dtype) is supported in the
+ *     forward and backward entry points: raw scores QK^T get
+ *     attn_mask[b][h % mask_dims[1]][q % mask_dims[2]][k] * softmax_unscale
+ *     added before the softmax scale (reference flash_fwd_kernel.h:640-660,
+ *     softmax.h:361-379); mask_dims = {batch, head modulus, row modulus,
+ *     seqlen_k} (host int64[4], reference flash_attn.cu:623-624); not combined
+ *     with return_softmax.  The FlashMask column-range arguments must be NULL
+ *     (out of scope for this build: the call fails with a message otherwise);
  *   - backward: softmax_d (b, h, seqlen_q_rounded) fp32 is a caller-owned
  *     output (D = rowsum(dO * O)); dq_accum is caller-owned fp32 SCRATCH of at
  *     least batch * num_heads * seqlen_q_rounded floats (the reference's
