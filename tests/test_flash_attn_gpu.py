@@ -485,3 +485,29 @@ def test_fwd_deferred_max_forced(mode, causal, dtype):
     gp = torch.autograd.grad(out_pt, (qc, kc, vc), gc)
     for name, got, r, p in zip(("dq", "dk", "dv"), (dq, dk, dv), gr, gp):
         _assert_bound(name, got, r, p)
+
+
+# ------------------------------------------------------------------------------------------------
+# XCD-grouped work order (fa_common.h xcd_order_grouped): launches whose K/V stream exceeds the
+# 256 MiB Infinity Cache run a head-grouped order; the result must be bitwise the head-fastest one
+# (FLASH_ATTN_MI355X_NO_XCD_GROUP=1, read per launch, forces that order).
+# ------------------------------------------------------------------------------------------------
+def test_xcd_grouped_order_is_bitwise_head_fastest(monkeypatch):
+    from flash_attn import flash_attn_func
+
+    torch.manual_seed(0)
+    # K + V = 402 MB > 256 MiB: grouped order for the forward and dQ kernels
+    q = torch.randn(3, 16384, 32, 128, device=DEV, dtype=torch.bfloat16, requires_grad=True)
+    k = torch.randn(3, 16384, 16, 128, device=DEV, dtype=torch.bfloat16, requires_grad=True)
+    v = torch.randn(3, 16384, 16, 128, device=DEV, dtype=torch.bfloat16, requires_grad=True)
+    g = torch.randn_like(q)
+    res = {}
+    for flag in ("0", "1"):
+        monkeypatch.setenv("FLASH_ATTN_MI355X_NO_XCD_GROUP", flag)
+        out, lse, _ = flash_attn_func(q, k, v, causal=True, return_attn_probs=True)
+        dq, dk, dv = torch.autograd.grad(out, (q, k, v), g)
+        torch.cuda.synchronize()
+        res[flag] = (out, lse, dq, dk, dv)
+    for name, a, b in zip(("out", "lse", "dq", "dk", "dv"), res["0"], res["1"]):
+        assert torch.isfinite(a.float()).all(), name
+        assert torch.equal(a, b), name

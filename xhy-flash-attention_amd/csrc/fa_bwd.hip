@@ -490,9 +490,9 @@ __global__ void __launch_bounds__(DqTile<D>::NW * 64, DqTile<D>::MINB) bwd_dq_ke
   const int r = lane & 31, hh = lane >> 5;
   const LdsBases lb(lane);
   const int num_m = (s.seqlen_q + BM - 1) / BM;
-  // head-fastest, heaviest causal block first (as the forward; xcd_order measured 5% slower here)
-  const int bh = blockIdx.x % (s.b * s.h);
-  const int m_idx = blockIdx.x / (s.b * s.h);
+  // XCD-aware, heads grouped as in the forward (p.dq_head_group from launch_bwd)
+  int bh, m_idx;
+  xcd_order_grouped(blockIdx.x, s.b * s.h, num_m, p.dq_head_group, bh, m_idx);
   const int bidb = bh / s.h;
   const int head = bh - bidb * s.h;
   const int kvh = head / (s.h / s.hk);
@@ -730,6 +730,14 @@ void launch_bwd(const BwdParams& p_in, bool is_bf16, hipStream_t stream) {
       (int64_t)p_in.s.b * p_in.s.h * p_in.num_n_blocks > 0x7fffffff)
     throw std::runtime_error("flash_attn_bwd: problem too large for the grid");
   BwdParams p = p_in;
+  {
+    const int bm = p.s.d <= 128 ? DqTile<128>::BM : DqTile<256>::BM;
+    p.dq_head_group = xcd_head_group((long long)p.s.b * p.s.h, (p.s.seqlen_q + bm - 1) / bm,
+                                     4ll * p.s.b * p.s.seqlen_k * p.s.hk * p.s.d, p.s.causal);
+#ifdef FA_FWD_NOGROUP
+    p.dq_head_group = 0;
+#endif
+  }
   // softmax_scale == 0 (uniform attention) would make -LSE / scale infinite: a tiny positive scale
   // gives the same P to fp32 precision (P deviates from uniform by 1e-30 |S|) and dQ, dK ~ 1e-30.
   if (p.s.scale == 0.f) { p.s.scale = 1e-30f; p.s.scale_log2 = 1e-30f * kLog2e; }

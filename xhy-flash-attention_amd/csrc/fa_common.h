@@ -20,6 +20,7 @@
 
 #include <hip/hip_runtime.h>
 #include <stdint.h>
+#include <stdlib.h>
 
 #include <type_traits>
 
@@ -304,6 +305,49 @@ __device__ inline const unsigned short* mask_row_ptr(const Shape& s, int bidb, i
   if (s.mask == nullptr) return nullptr;
   const int64_t r = ((int64_t)bidb * s.mask_h + head % s.mask_h) * s.mask_sq + q % s.mask_sq;
   return (const unsigned short*)s.mask + r * s.mask_row;
+}
+
+// The same with heads taken hp at a time: the XCD of group j walks groups of hp of its heads, and
+// inside a group block-major / head-minor (block 0 -- the heaviest causal block -- of every head of
+// the group first).  hp = 1 is xcd_order.  A larger hp keeps fewer heads' streams in flight than
+// head-fastest order while bounding the causal tail: the last group's heaviest block starts after
+// (G-1)/G of the XCD's work, G = heads per XCD / hp (launchers pick hp, xcd_head_group()).
+// Requires nbh % 8 == 0 and (nbh / 8) % hp == 0; otherwise head-fastest order.
+__device__ inline void xcd_order_grouped(int L, int nbh, int nblk, int hp, int& bh, int& blk) {
+  if ((nbh & 7) == 0 && hp > 0 && ((nbh >> 3) % hp) == 0) {
+    const int i = L >> 3;
+    const int per_group = hp * nblk;
+    const int g = i / per_group;
+    const int r = i - g * per_group;
+    blk = r / hp;
+    const int hl = g * hp + (r - blk * hp);
+    bh = hl * 8 + (L & 7);
+  } else {
+    blk = L / nbh;
+    bh = L - blk * nbh;
+  }
+}
+
+// Heads per group for xcd_order_grouped on a causal grid of nbh heads x nblk blocks whose block b
+// costs ~(b + 1) units: the heaviest block (nblk units) must fit in 1/G of a CU's share of the work,
+// G <= nbh (nblk + 1) / (2 * 256 CUs); hp = the smallest divisor of nbh / 8 giving G within that.
+// Used only when the K/V (or Q/dO) stream of the launch is larger than the 256 MiB Infinity Cache
+// (stream_bytes): below that the cache absorbs the re-reads of head-fastest order, which then keeps
+// the better causal balance (measured at C3, 256 MiB of K/V: grouping -1.5%; at C5, 1 GiB: +16% fwd,
+// +14% dQ).  causal = false: every block costs the same, one head per group.
+inline int xcd_head_group(long long nbh, long long nblk, long long stream_bytes, bool causal) {
+  // test knob (read per launch): FLASH_ATTN_MI355X_NO_XCD_GROUP=1 -> head-fastest order
+  const char* e = std::getenv("FLASH_ATTN_MI355X_NO_XCD_GROUP");
+  const bool disabled = e != nullptr && e[0] == '1';
+  if (disabled || stream_bytes <= (256ll << 20)) return 0;
+  if (nbh % 8 != 0 || nbh <= 0 || nblk <= 0) return 0;
+  if (!causal) return 1;
+  const long long h8 = nbh / 8;
+  long long gmax = nbh * (nblk + 1) / 512;
+  if (gmax < 1) gmax = 1;
+  for (long long hp = 1; hp <= h8; ++hp)
+    if (h8 % hp == 0 && h8 / hp <= gmax) return (int)hp;
+  return (int)h8;
 }
 
 // Accumulator element g -> row offset inside a 32x32 tile for lane half h.

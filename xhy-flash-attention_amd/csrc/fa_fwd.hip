@@ -83,11 +83,11 @@ __global__ void __launch_bounds__(FwdTile<D>::NW * 64, FwdTile<D>::MINB) fwd_ker
   const int r = lane & 31, hh = lane >> 5;
   const LdsBases lb(lane);
 
-  // head-fastest, heaviest causal block first over the whole grid; with b * h a multiple of 8 every
-  // block of one head lands on the same XCD (L % 8).  Grouping a head's blocks in time as well
-  // (xcd_order, which the dK/dV kernel uses) measured 5% slower here: the causal tail grows.
-  const int bh = blockIdx.x % (s.b * s.h);
-  const int m_idx = blockIdx.x / (s.b * s.h);
+  // Work order: XCD-aware, heads grouped (xcd_order_grouped, p.head_group from launch_fwd): a few
+  // heads' query blocks run together on one XCD, heaviest first, sharing K/V through its L2; the
+  // group size bounds the causal tail (all heads of an XCD in sequence, xcd_order, measured -5%).
+  int bh, m_idx;
+  xcd_order_grouped(blockIdx.x, s.b * s.h, p.num_m_blocks, p.head_group, bh, m_idx);
   const int bidb = bh / s.h;
   const int head = bh - bidb * s.h;
   const int kvh = head / (s.h / s.hk);
@@ -528,8 +528,14 @@ void fwd_block_size(int d, int* block_m, int* block_n) {
   *block_n = d <= 128 ? FwdTile<128>::BN : FwdTile<256>::BN;
 }
 
-void launch_fwd(const FwdParams& p, bool is_bf16, hipStream_t stream) {
+void launch_fwd(const FwdParams& p_in, bool is_bf16, hipStream_t stream) {
+  FwdParams p = p_in;
   if (p.s.b <= 0 || p.s.h <= 0) return;
+  p.head_group = xcd_head_group((long long)p.s.b * p.s.h, p.num_m_blocks,
+                                 4ll * p.s.b * p.s.seqlen_k * p.s.hk * p.s.d, p.s.causal);   // K + V bytes
+#ifdef FA_FWD_NOGROUP
+  p.head_group = 0;
+#endif
   if (p.num_m_blocks <= 0) return;
   if ((int64_t)p.s.b * p.s.h * p.num_m_blocks > 0x7fffffff)
     throw std::runtime_error("flash_attn_fwd: batch * heads * query blocks too large for the grid");

@@ -54,6 +54,7 @@ struct FwdParams {
   int64_t v_batch, v_row, v_head;
   int64_t o_batch, o_row, o_head;
   int num_m_blocks;
+  int head_group;           // xcd_order_grouped heads per group (0: head-fastest order); launch_fwd
   void* p_out;              // return_softmax (dropout only): S_dmask (b, h, sq_rounded, sk_rounded)
   int p_rows, p_cols;       // sq_rounded, sk_rounded
 };
@@ -80,6 +81,7 @@ struct BwdParams {
   bool gqa_reduce;        // true: dk/dv have hk heads and the kernel sums the group in-register;
                           // false: dk/dv have h heads (reference "expanded" contract)
   int num_n_blocks;
+  int dq_head_group;        // dQ kernel: xcd_order_grouped heads per group (0: head-fastest)
 };
 
 // Host launchers (fa_fwd.hip / fa_bwd.hip).  Throw std::runtime_error on invalid configuration.
