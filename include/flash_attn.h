@@ -11,6 +11,7 @@
  *   flash_attn_bwd         <- reference csrc/capi/flash_attn.h:100-161
  *   flash_attn_varlen_bwd  <- reference csrc/capi/flash_attn.h:163-221
  *   flash_attn_error       <- reference csrc/capi/flash_attn.h:315
+ *   calc_reduced_attn_scores <- reference csrc/capi/flash_attn.h:223-247
  *
  * Conventions (reference csrc/capi/flash_attn.cu:29-96, 576-1105):
  *   - every buffer is a caller-owned device pointer; strides are in ELEMENTS;
@@ -268,6 +269,38 @@ bool flash_attn_varlen_bwd(const void * const dout,
                            const int dv_batch_stride,
                            const int do_batch_stride,
                            const bool varlen_padded_input);
+
+/* reference csrc/capi/flash_attn.h:223-247 (calc_reduced_attn_scores): for every (batch, head,
+ * key) the column sum over all queries of exp(softmax_scale * q.k - softmax_lse[q]) into
+ * reduced_scores (fp32, batch x num_heads x seqlen_k; written, so it needs no zeroing -- the
+ * reference atomically adds into a zeroed buffer), and with return_softmax the probabilities into
+ * softmax_ptr (fp32, batch x num_heads x seqlen_q x seqlen_k).  Non-causal, no mask (as the
+ * reference); MQA/GQA through num_heads_k.  num_splits and the o_* strides are accepted and unused. */
+bool calc_reduced_attn_scores(const void * const q,
+                              const void * const k,
+                              const void * const softmax_lse,
+                              void * const reduced_scores,
+                              void * const softmax_ptr,
+                              const int batch_size,
+                              const int seqlen_q,
+                              const int seqlen_k,
+                              const int num_heads,
+                              const int num_heads_k,
+                              const int head_size,
+                              const float softmax_scale,
+                              const bool return_softmax,
+                              const bool is_bf16,
+                              const int num_splits,
+                              hipStream_t stream,
+                              const int q_row_stride,
+                              const int k_row_stride,
+                              const int o_row_stride,
+                              const int q_head_stride,
+                              const int k_head_stride,
+                              const int o_head_stride,
+                              const int q_batch_stride,
+                              const int k_batch_stride,
+                              const int o_batch_stride);
 
 const char *flash_attn_error();
 

@@ -355,6 +355,38 @@ bool flash_attn_bwd_gqa(FA_BWD_ARGS) { FA_BWD_CALL(true); }
                   offset, mask_dims, softmax_unscale)
 
 bool flash_attn_varlen_bwd(FA_VARLEN_BWD_ARGS) { FA_VARLEN_BWD_CALL(false); }
+
+// reference csrc/capi/flash_attn.cu:1107-1201 (o_* strides are accepted and unused there too)
+bool calc_reduced_attn_scores(const void* const q, const void* const k, const void* const softmax_lse,
+                              void* const reduced_scores, void* const softmax_ptr, const int batch_size,
+                              const int seqlen_q, const int seqlen_k, const int num_heads,
+                              const int num_heads_k, const int head_size, const float softmax_scale,
+                              const bool return_softmax, const bool is_bf16, const int num_splits,
+                              hipStream_t stream, const int q_row_stride, const int k_row_stride,
+                              const int o_row_stride, const int q_head_stride, const int k_head_stride,
+                              const int o_head_stride, const int q_batch_stride, const int k_batch_stride,
+                              const int o_batch_stride) {
+  (void)num_splits; (void)o_row_stride; (void)o_head_stride; (void)o_batch_stride;
+  FA_BEGIN
+  check_common(batch_size, num_heads, num_heads_k, head_size, head_size, 0.f, nullptr, nullptr);
+  FA_CHECK(q && k && softmax_lse && reduced_scores);
+  FA_CHECK(seqlen_q > 0 && seqlen_k > 0);
+  if (return_softmax) FA_CHECK(softmax_ptr != nullptr);
+  fa::ReducedParams p;
+  std::memset(&p, 0, sizeof(p));
+  p.q = q; p.k = k;
+  p.lse = static_cast<const float*>(softmax_lse);
+  p.reduced = static_cast<float*>(reduced_scores);
+  p.p_out = return_softmax ? static_cast<float*>(softmax_ptr) : nullptr;
+  p.b = batch_size; p.h = num_heads; p.hk = num_heads_k;
+  p.sq = seqlen_q; p.sk = seqlen_k; p.d = head_size;
+  p.scale = softmax_scale;
+  p.q_batch = q_batch_stride; p.q_row = q_row_stride; p.q_head = q_head_stride;
+  p.k_batch = k_batch_stride; p.k_row = k_row_stride; p.k_head = k_head_stride;
+  fa::launch_reduced_scores(p, is_bf16, stream);
+  return true;
+  FA_END
+}
 bool flash_attn_varlen_bwd_gqa(FA_VARLEN_BWD_ARGS) { FA_VARLEN_BWD_CALL(true); }
 
 }  // extern "C"

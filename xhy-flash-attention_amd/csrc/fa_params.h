@@ -84,9 +84,23 @@ struct BwdParams {
   int dq_head_group;        // dQ kernel: xcd_order_grouped heads per group (0: head-fastest)
 };
 
+// calc_reduced_attn_scores (fa_reduced.hip; reference reduced_scores::Params,
+// calc_reduced_attn_scores_kernel.h:14-40): column sums of exp(scale q.k - LSE) per (b, h, key).
+struct ReducedParams {
+  const void* q; const void* k;
+  const float* lse;        // (b, h, sq) fp32
+  float* reduced;          // (b, h, sk) fp32, written (not accumulated)
+  float* p_out;            // optional (b, h, sq, sk) fp32 probabilities
+  int b, h, hk, sq, sk, d;
+  float scale;
+  int64_t q_batch, q_row, q_head;
+  int64_t k_batch, k_row, k_head;
+};
+
 // Host launchers (fa_fwd.hip / fa_bwd.hip).  Throw std::runtime_error on invalid configuration.
 void launch_fwd(const FwdParams& p, bool is_bf16, hipStream_t stream);
 void launch_bwd(const BwdParams& p, bool is_bf16, hipStream_t stream);
+void launch_reduced_scores(const ReducedParams& p, bool is_bf16, hipStream_t stream);
 
 // Tile sizes the launchers use for a given head dim (reported by _get_block_size in Python).
 void fwd_block_size(int d, int* block_m, int* block_n);
