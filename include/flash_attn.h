@@ -25,8 +25,18 @@
  *     added before the softmax scale (reference flash_fwd_kernel.h:640-660,
  *     softmax.h:361-379); mask_dims = {batch, head modulus, row modulus,
  *     seqlen_k} (host int64[4], reference flash_attn.cu:623-624); not combined
- *     with return_softmax.  The FlashMask column-range arguments must be NULL
- *     (out of scope for this build: the call fails with a message otherwise);
+ *     with return_softmax;
+ *   - FlashMask (flash_attn_fwd / flash_attn_bwd*, not varlen, reference
+ *     flash_attn.cu:204-209): active iff flashmask_downstart_ptr != NULL.
+ *     int32 row bounds of shape (batch, flashmask_dims[1], seqlen_k) each;
+ *     attention head h uses mask head h / (num_heads / flashmask_dims[1]).
+ *     Causal: key k is hidden from rows in [downstart[k], downend[k]) (downend
+ *     NULL: to the end).  Non-causal: rows in [downstart, downend) and
+ *     [upstart, upend) when upstart is given, else rows >= downstart or
+ *     < upend; upend is required (reference softmax.h:180-298).  Pass the same
+ *     pointers to the backward.  flashmask_maxmin_ptr (the reference's
+ *     tile-scan scratch) is accepted and not used.  Not combined with attn_mask
+ *     or return_softmax.  Rows that see no key give out = 0, LSE = +inf;
  *   - backward: softmax_d (b, h, seqlen_q_rounded) fp32 is a caller-owned
  *     output (D = rowsum(dO * O)); dq_accum is caller-owned fp32 SCRATCH of at
  *     least batch * num_heads * seqlen_q_rounded floats (the reference's

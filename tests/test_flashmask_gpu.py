@@ -1,0 +1,171 @@
+"""GPU parity of FlashMask column-range masks through the C ABI.
+
+The reference (csrc/capi/flash_attn.cu:204-209, 540, 795; softmax.h:180-298; flash_fwd_kernel.h:
+1055-1700; flash_bwd_kernel.h:1148-1700) removes (row, key) by per-key int32 row bounds; the rule is
+restated in oracle/flashmask_ref.py (parity unpinned against reference outputs: its tests hold no
+FlashMask fixtures).  Here the kernels' out / LSE / dq / dk / dv are checked against an fp32 torch
+attention with that keep matrix, under the reference's 2x rule; fully masked rows give out = 0,
+LSE = +inf and zero gradients, as the reference's Check_inf softmax does.
+"""
+import numpy as np
+import pytest
+import torch
+
+from oracle.attention_ref import check_within_bound
+from oracle.flashmask_ref import document_lts, flashmask_keep
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda"
+
+
+@pytest.fixture(scope="module", autouse=True)
+def _need_gpu():
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    import flash_attn_2_cuda  # noqa: F401
+
+
+def _ref(q, k, v, keep, scale, upcast=True):
+    """softmax(scale QK^T) V over kept (row, key) pairs; keep: (b, hm, sq, sk) bool on DEV."""
+    dt = q.dtype
+    if upcast:
+        q, k, v = q.float(), k.float(), v.float()
+    b, sq, h, d = q.shape
+    hk, hm = k.shape[2], keep.shape[1]
+    k = k.repeat_interleave(h // hk, dim=2)
+    v = v.repeat_interleave(h // hk, dim=2)
+    kp = keep[:, torch.arange(h, device=q.device) // (h // hm)]            # (b, h, sq, sk)
+    s = torch.einsum("bqhd,bkhd->bhqk", q, k) * scale
+    row_any = kp.any(-1, keepdim=True)
+    s = torch.where(row_any, s.masked_fill(~kp, float("-inf")), torch.zeros_like(s))
+    p = torch.softmax(s, dim=-1) * row_any
+    return torch.einsum("bhqk,bkhd->bqhd", p, v).to(dt)
+
+
+def _capi(q, k, v, dout, scale, causal, lts, lte=None, uts=None, ute=None):
+    import flash_attn_2_cuda as m
+
+    b, sq, h, d = q.shape
+    sk, hk = k.shape[1], k.shape[2]
+    out = torch.empty_like(q)
+    lse = torch.empty(b, h, sq, device=DEV, dtype=torch.float32)
+    rng = torch.empty(2, device=DEV, dtype=torch.int64)
+    dev = lambda a: None if a is None else torch.from_numpy(np.ascontiguousarray(a, np.int32)).to(DEV)  # noqa: E731
+    tl, te, us, ue = dev(lts), dev(lte), dev(uts), dev(ute)
+    dims = torch.tensor([b, lts.shape[1], sk, 1], dtype=torch.int64)
+    dims_p = dims.numpy().ctypes.data
+    P = m._ptr
+    Pn = lambda t: None if t is None else P(t)  # noqa: E731
+    maxmin = torch.empty(8 * b * lts.shape[1] * ((sk + 127) // 128 + 1), device=DEV, dtype=torch.int32)
+    fm = (Pn(tl), dims_p, Pn(ue), Pn(te), Pn(us), P(maxmin))
+    st = lambda t: (t.stride(1), t.stride(2), t.stride(0))  # noqa: E731 (row, head, batch)
+    (qr, qh, qb), (kr, kh, kb), (vr, vh, vb), (orr, oh, ob) = st(q), st(k), st(v), st(out)
+    sq_r, sk_r = (sq + 127) // 128 * 128, (sk + 127) // 128 * 128
+    bf16 = q.dtype == torch.bfloat16
+    ok = m._lib.flash_attn_fwd(P(q), P(k), P(v), P(rng), P(out), None, P(lse), b, sq, sk, sq_r, sk_r,
+                               h, hk, d, d, 0.0, scale, 1.0, causal, False, bf16,
+                               m._stream(q), 0, 0, None, None, *fm,
+                               qr, kr, vr, qh, kh, vh, orr, oh, qb, kb, vb, ob)
+    assert ok, m._lib.flash_attn_error()
+    dq, dk, dv = torch.empty_like(q), torch.empty_like(k), torch.empty_like(v)
+    softmax_d = torch.empty(b, h, sq_r, device=DEV)
+    (dqr, dqh, dqb), (dkr, dkh, dkb), (dvr, dvh, dvb), (dor, doh, dob) = st(dq), st(dk), st(dv), st(dout)
+    ok = m._lib.flash_attn_bwd_gqa(P(dout), P(q), P(k), P(v), P(out), P(softmax_d), P(lse), P(rng),
+                                   P(dq), P(dk), P(dv), None, b, sq, sk, sq_r, sk_r, h, hk, d, d,
+                                   0.0, scale, 1.0, causal, bf16, 1,
+                                   m._stream(q), 0, 0, None, None, *fm,
+                                   qr, kr, vr, qh, kh, vh, orr, oh, qb, kb, vb, ob,
+                                   dqr, dkr, dvr, dqh, dkh, dvh, dor, doh, dqb, dkb, dvb, dob)
+    assert ok, m._lib.flash_attn_error()
+    torch.cuda.synchronize()
+    return out, lse, dq, dk, dv
+
+
+def _bounds(mode, b, hm, sq, sk, rng):
+    draw = lambda lo=0: rng.integers(lo, sq + 1, size=(b, hm, sk)).astype(np.int32)  # noqa: E731
+    if mode == "doc":          # causal document mask, random document lengths per batch / head
+        lts = np.empty((b, hm, sk), np.int32)
+        for i in range(b):
+            for j in range(hm):
+                cuts = np.sort(rng.choice(np.arange(1, sq), size=3, replace=False))
+                lts[i, j] = document_lts(np.diff(np.concatenate([[0], cuts, [sq]])), sq)
+        return True, dict(lts=lts)
+    if mode == "causal_range":
+        lts = draw()
+        return True, dict(lts=lts, lte=np.minimum(lts + rng.integers(0, sq // 2, size=lts.shape), sq).astype(np.int32))
+    if mode == "causal_tail":  # rows >= sq/2 see no key at all: out 0, LSE +inf
+        return True, dict(lts=np.full((b, hm, sk), sq // 2, np.int32))
+    if mode == "bidir2":
+        return False, dict(lts=draw(), ute=draw() // 3)
+    lts = draw()
+    uts = draw()
+    return False, dict(lts=lts, lte=np.minimum(lts + sq // 4, sq).astype(np.int32), uts=uts,
+                       ute=np.minimum(uts + sq // 5, sq).astype(np.int32))
+
+
+@pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float16])
+@pytest.mark.parametrize("mode", ["doc", "causal_range", "causal_tail", "bidir2", "bidir4"])
+@pytest.mark.parametrize("d,sq,h,hk,hm", [(64, 300, 4, 2, 1), (128, 517, 4, 4, 2), (256, 190, 2, 1, 2)])
+def test_flashmask_fwd_bwd(d, sq, h, hk, hm, mode, dtype):
+    torch.manual_seed(0)
+    rng = np.random.default_rng(d + sq)
+    b, sk = 2, sq
+    q = torch.randn(b, sq, h, d, device=DEV, dtype=dtype)
+    k = torch.randn(b, sk, hk, d, device=DEV, dtype=dtype)
+    v = torch.randn(b, sk, hk, d, device=DEV, dtype=dtype)
+    dout = torch.randn(b, sq, h, d, device=DEV, dtype=dtype)
+    causal, bnd = _bounds(mode, b, hm, sq, sk, rng)
+    scale = d ** -0.5
+    out, lse, dq, dk, dv = _capi(q, k, v, dout, scale, causal, **bnd)
+
+    keep = torch.from_numpy(flashmask_keep(bnd["lts"], sq, causal, lte=bnd.get("lte"),
+                                           uts=bnd.get("uts"), ute=bnd.get("ute"))).to(DEV)
+    qc, kc, vc = (x.clone().requires_grad_() for x in (q, k, v))
+    ref = _ref(qc, kc, vc, keep, scale)
+    pt = _ref(qc, kc, vc, keep, scale, upcast=False)
+    ok, err, bound = check_within_bound(out, ref, pt)
+    assert ok, f"out: {err:.3e} > {bound:.3e}"
+    # LSE: finite rows against the fp32 logsumexp, fully masked rows +inf
+    kp = keep[:, torch.arange(h, device=DEV) // (h // hm)]
+    kf = k.float().repeat_interleave(h // hk, dim=2)
+    s = torch.einsum("bqhd,bkhd->bhqk", q.float(), kf) * scale
+    lse_ref = torch.logsumexp(s.masked_fill(~kp, float("-inf")), dim=-1)
+    dead = ~kp.any(-1)
+    assert torch.isinf(lse[dead]).all() and (lse[dead] > 0).all()
+    torch.testing.assert_close(lse[~dead], lse_ref[~dead], atol=2e-3, rtol=0)
+    if dead.any():
+        assert (out.permute(0, 2, 1, 3)[dead] == 0).all()
+    gr = torch.autograd.grad(ref, (qc, kc, vc), dout)
+    gp = torch.autograd.grad(pt, (qc, kc, vc), dout)
+    for name, got, r, p in zip(("dq", "dk", "dv"), (dq, dk, dv), gr, gp):
+        assert torch.isfinite(got).all(), name
+        ok, err, bound = check_within_bound(got, r, p, floor=1e-3)
+        assert ok, f"{name}: {err:.3e} > {bound:.3e}"
+
+
+def test_flashmask_argument_checks():
+    import flash_attn_2_cuda as m
+
+    q = torch.randn(1, 64, 4, 64, device=DEV, dtype=torch.float16)
+    lse = torch.empty(1, 4, 64, device=DEV)
+    out = torch.empty_like(q)
+    lts = torch.zeros(1, 1, 64, device=DEV, dtype=torch.int32)
+    st = (q.stride(1), q.stride(1), q.stride(1), q.stride(2), q.stride(2), q.stride(2), out.stride(1),
+          out.stride(2), q.stride(0), q.stride(0), q.stride(0), out.stride(0))
+    P = m._ptr
+
+    def call(causal, dims, upend, mask=None, mask_dims=None):
+        return m._lib.flash_attn_fwd(P(q), P(q), P(q), None, P(out), None, P(lse), 1, 64, 64, 128, 128,
+                                     4, 4, 64, 64, 0.0, 0.125, 8.0, causal, False, False, m._stream(q),
+                                     0, 0, mask, mask_dims, P(lts), dims.numpy().ctypes.data, upend,
+                                     None, None, None, *st)
+
+    assert not call(True, torch.tensor([1, 3, 64, 1]), None)         # 3 does not divide 4 heads
+    assert b"flashmask_dims" in m._lib.flash_attn_error()
+    assert not call(False, torch.tensor([1, 1, 64, 1]), None)        # non-causal needs upend
+    assert b"upend" in m._lib.flash_attn_error()
+    dm = torch.zeros(1, 1, 64, 64, device=DEV, dtype=torch.float16)
+    dm_dims = torch.tensor([1, 1, 64, 64], dtype=torch.int64)
+    assert not call(True, torch.tensor([1, 1, 64, 1]), None, P(dm), dm_dims.numpy().ctypes.data)
+    assert b"cannot be combined" in m._lib.flash_attn_error()
+    assert call(True, torch.tensor([1, 1, 64, 1]), None)

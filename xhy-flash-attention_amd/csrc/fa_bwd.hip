@@ -160,7 +160,9 @@ __global__ void __launch_bounds__(256) bwd_pre_kernel(const BwdParams p) {
 // Slice lifetimes: Q (+ LSE, D) is read in steps it and it+1 (3-deep ring, one slice of DMA in
 // flight), dO only in step it (2-deep ring), P(it) in steps it and it+1 (2 buffers).
 // Each wave needs one 32-key operand set and one D x 32 accumulator set (<= 256 registers).
-template <bool BF16, int D, bool CAUSAL, bool DROPOUT>
+// MASKED (dense additive mask and/or FlashMask present): every slice takes the per-element path; the
+// unmasked instantiations carry no mask code (as in fwd_kernel).
+template <bool BF16, int D, bool CAUSAL, bool DROPOUT, bool MASKED>
 __global__ void __launch_bounds__(DkdvTile<D>::NW * 64, 1) bwd_dkdv_kernel(const BwdParams p) {
   using E = Elt<BF16>;
   constexpr int NW = DkdvTile<D>::NW;
@@ -346,9 +348,14 @@ __global__ void __launch_bounds__(DkdvTile<D>::NW * 64, 1) bwd_dkdv_kernel(const
           float x;
           if constexpr (MASK) {
             const int q = q0 + 32 * qi + 8 * u + 4 * hh + j;
-            const bool out = key >= sk || q >= sq || (CAUSAL && key > q);
-            const u16* mrow = out ? nullptr : mask_row_ptr(s, bidb, h_begin + it_head, q);
-            const float add = mrow != nullptr ? E::to_f32(mrow[key]) * s.mask_unscale : 0.f;
+            bool out = key >= sk || q >= sq || (CAUSAL && key > q);
+            float add = 0.f;
+            if constexpr (MASKED) {
+              out = out || (s.fm_lts != nullptr &&
+                            fm_masked<CAUSAL>(s, fm_base(s, bidb, h_begin + it_head) + key, q));
+              const u16* mrow = out ? nullptr : mask_row_ptr(s, bidb, h_begin + it_head, q);
+              if (mrow != nullptr) add = E::to_f32(mrow[key]) * s.mask_unscale;
+            }
             x = out ? 0.f : fast_exp2((sp[qi][4 * u + j] + add) * c);
           } else {
             x = fast_exp2(sp[qi][4 * u + j] * c);
@@ -429,7 +436,7 @@ __global__ void __launch_bounds__(DkdvTile<D>::NW * 64, 1) bwd_dkdv_kernel(const
       }
     phase1(pwave ? qs : os, sp);                       // S' = Q K^T - LSE/scale  /  dP'' = D - dO V^T
     if (pwave) {
-      const bool fast = !s.mask && (q0 + BQ <= sq) && (n0 + BKN <= sk) && (!CAUSAL || q0 >= n0 + BKN - 1);
+      const bool fast = !MASKED && (q0 + BQ <= sq) && (n0 + BKN <= sk) && (!CAUSAL || q0 >= n0 + BKN - 1);
       if (fast) p_step(std::false_type{}, sp, q0, it_head, xw_of(it), fr);
       else p_step(std::true_type{}, sp, q0, it_head, xw_of(it), fr);
     }
@@ -467,7 +474,7 @@ __global__ void __launch_bounds__(DkdvTile<D>::NW * 64, 1) bwd_dkdv_kernel(const
 // ------------------------------------------------------------------------------------------------
 // 3. dQ  (forward-shaped: query on the lane, K/V streamed)
 // ------------------------------------------------------------------------------------------------
-template <bool BF16, int D, bool CAUSAL, bool DROPOUT>
+template <bool BF16, int D, bool CAUSAL, bool DROPOUT, bool MASKED>
 __global__ void __launch_bounds__(DqTile<D>::NW * 64, DqTile<D>::MINB) bwd_dq_kernel(const BwdParams p) {
   using E = Elt<BF16>;
   constexpr int NW = DqTile<D>::NW;
@@ -532,8 +539,9 @@ __global__ void __launch_bounds__(DqTile<D>::NW * 64, DqTile<D>::MINB) bwd_dq_ke
 
   const int n_end = CAUSAL ? min(sk, m0 + BM) : sk;
   const int nblk = n_end > 0 ? (n_end + BN - 1) / BN : 0;
-  const int nfast = s.mask ? 0 : min(nblk, (CAUSAL ? min(sk, m0 + 1) : sk) / BN);
-  const u16* mrow = mask_row_ptr(s, bidb, head, q_ok ? qi : 0);
+  const int nfast = MASKED ? 0 : min(nblk, (CAUSAL ? min(sk, m0 + 1) : sk) / BN);
+  const int64_t fmb = (MASKED && s.fm_lts) ? fm_base(s, bidb, head) : 0;
+  const u16* mrow = MASKED ? mask_row_ptr(s, bidb, head, q_ok ? qi : 0) : nullptr;
 
   int voff_k[PPW], voff_v[PPW];
 #pragma unroll
@@ -602,8 +610,12 @@ __global__ void __launch_bounds__(DqTile<D>::NW * 64, DqTile<D>::MINB) bwd_dq_ke
         float pv;
         if constexpr (MASK) {
           const int kk = n0 + t * 32 + acc_row(g, hh);
-          const bool out = kk >= sk || (CAUSAL && kk > qi);
-          const float add = (!out && mrow != nullptr) ? E::to_f32(mrow[kk]) * s.mask_unscale : 0.f;
+          bool out = kk >= sk || (CAUSAL && kk > qi);
+          float add = 0.f;
+          if constexpr (MASKED) {
+            out = out || (s.fm_lts != nullptr && fm_masked<CAUSAL>(s, fmb + kk, qi));
+            if (!out && mrow != nullptr) add = E::to_f32(mrow[kk]) * s.mask_unscale;
+          }
           pv = out ? 0.f : fast_exp2(fmaf(st[t][g] + add, c, -lse_l2));
         } else {
           pv = fast_exp2(fmaf(st[t][g], c, -lse_l2));
@@ -676,16 +688,23 @@ __global__ void __launch_bounds__(DqTile<D>::NW * 64, DqTile<D>::MINB) bwd_dq_ke
 template <bool BF16, int D, bool CAUSAL, bool DROPOUT>
 static void run_bwd(const BwdParams& p, hipStream_t stream) {
   const int nheads_grid = p.gqa_reduce ? p.s.hk : p.s.h;
+  const bool masked = p.s.mask != nullptr || p.s.fm_lts != nullptr;
   {
     dim3 grid(p.s.b * nheads_grid * p.num_n_blocks);   // 1-D, xcd_order
     prof_begin(kTimeBwdMain, stream);
-    hipLaunchKernelGGL((bwd_dkdv_kernel<BF16, D, CAUSAL, DROPOUT>), grid, dim3(DkdvTile<D>::NW * 64), 0, stream, p);
+    if (masked)
+      hipLaunchKernelGGL((bwd_dkdv_kernel<BF16, D, CAUSAL, DROPOUT, true>), grid, dim3(DkdvTile<D>::NW * 64), 0, stream, p);
+    else
+      hipLaunchKernelGGL((bwd_dkdv_kernel<BF16, D, CAUSAL, DROPOUT, false>), grid, dim3(DkdvTile<D>::NW * 64), 0, stream, p);
     prof_end(kTimeBwdMain, stream);
   }
   {
     dim3 grid(p.s.b * p.s.h * ((p.s.seqlen_q + DqTile<D>::BM - 1) / DqTile<D>::BM));
     prof_begin(kTimeBwdDq, stream);
-    hipLaunchKernelGGL((bwd_dq_kernel<BF16, D, CAUSAL, DROPOUT>), grid, dim3(DqTile<D>::NW * 64), 0, stream, p);
+    if (masked)
+      hipLaunchKernelGGL((bwd_dq_kernel<BF16, D, CAUSAL, DROPOUT, true>), grid, dim3(DqTile<D>::NW * 64), 0, stream, p);
+    else
+      hipLaunchKernelGGL((bwd_dq_kernel<BF16, D, CAUSAL, DROPOUT, false>), grid, dim3(DqTile<D>::NW * 64), 0, stream, p);
     prof_end(kTimeBwdDq, stream);
   }
 }

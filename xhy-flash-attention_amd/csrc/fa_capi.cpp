@@ -60,9 +60,19 @@ void check_device() {
   checked_dev = dev;
 }
 
+// FlashMask column-range mask arguments of the reference C ABI (capi/flash_attn.h:38-43); the
+// reference takes the FlashMask path iff downstart is non-null (flash_attn.cu:540, 795).
+struct FlashMaskArgs {
+  const void* downstart;        // LTStart
+  const int64_t* dims;          // dims[1] = heads of the mask (reference mask_head_mod_size)
+  const void* upend;            // UTEnd
+  const void* downend;          // LTEnd
+  const void* upstart;          // UTStart
+};
+
 void check_common(int batch_size, int num_heads, int num_heads_k, int head_size,
                   int head_size_rounded, float p_dropout, const void* attn_mask,
-                  const void* flashmask) {
+                  const FlashMaskArgs* flashmask) {
   check_device();
   FA_CHECK(batch_size > 0);
   FA_CHECK(num_heads > 0 && num_heads_k > 0);
@@ -70,8 +80,8 @@ void check_common(int batch_size, int num_heads, int num_heads_k, int head_size,
   FA_CHECK(head_size <= 256);
   FA_CHECK(num_heads % num_heads_k == 0);
   FA_CHECK(head_size_rounded >= head_size);
-  (void)attn_mask;
-  if (flashmask != nullptr) throw std::runtime_error("FlashMask is not supported by the MI355X build");
+  if (attn_mask != nullptr && flashmask != nullptr && flashmask->downstart != nullptr)
+    throw std::runtime_error("attn_mask and FlashMask cannot be combined");
   FA_CHECK(p_dropout >= 0.f && p_dropout < 1.f);
 }
 
@@ -111,12 +121,31 @@ void set_mask(fa::AttnShape& s, const void* attn_mask, const int64_t* mask_dims,
   s.mask_unscale = unscale;
 }
 
+// FlashMask (reference capi flash_attn.cu:204-209, mask.h, flash_fwd_kernel.h:1055-1700): int32
+// row bounds per key column, (batch, mask heads, seqlen_k) each, head index head / (h / mask_heads).
+// The reference's caller-provided maxmin scratch feeds its tile-skip scan; the MI355X kernels
+// classify tiles themselves and do not need it.
+void set_flashmask(fa::AttnShape& s, const FlashMaskArgs* fm) {
+  if (fm == nullptr || fm->downstart == nullptr) return;
+  if (fm->dims == nullptr || fm->dims[1] < 1 || s.h % fm->dims[1] != 0)
+    throw std::runtime_error("FlashMask: flashmask_dims[1] must divide num_heads");
+  if (!s.causal && fm->upend == nullptr)
+    throw std::runtime_error("FlashMask: non-causal attention needs flashmask_upend_ptr");
+  if (!s.causal && fm->upstart != nullptr && fm->downend == nullptr)
+    throw std::runtime_error("FlashMask: flashmask_upstart_ptr needs flashmask_downend_ptr");
+  s.fm_lts = static_cast<const int*>(fm->downstart);
+  s.fm_lte = static_cast<const int*>(fm->downend);
+  s.fm_uts = s.causal ? nullptr : static_cast<const int*>(fm->upstart);
+  s.fm_ute = s.causal ? nullptr : static_cast<const int*>(fm->upend);
+  s.fm_h = (int)fm->dims[1];
+}
+
 bool fwd_impl(const void* q, const void* k, const void* v, const int32_t* cu_q, const int32_t* cu_k,
               void* rng_state, void* out, void* softmax_ptr, void* lse, int b, int sq, int sk,
               int sq_r, int sk_r,
               int h, int hk, int d, int d_r, float p_dropout, float scale, bool causal,
               bool return_softmax, bool is_bf16, hipStream_t stream, uint64_t seed, uint64_t offset,
-              const void* attn_mask, const void* flashmask, int q_row, int k_row, int v_row,
+              const void* attn_mask, const FlashMaskArgs* flashmask, int q_row, int k_row, int v_row,
               int q_head, int k_head, int v_head, int o_row, int o_head, int q_batch, int k_batch,
               int v_batch, int o_batch, bool padded, const int64_t* mask_dims = nullptr,
               float unscale = 1.f) {
@@ -130,8 +159,9 @@ bool fwd_impl(const void* q, const void* k, const void* v, const int32_t* cu_q, 
   std::memset(&p, 0, sizeof(p));
   p.s = make_shape(b, h, hk, sq, sk, d, scale, causal, cu_q, cu_k, padded, p_dropout, seed, offset);
   set_mask(p.s, attn_mask, mask_dims, unscale);
-  if (return_softmax && attn_mask != nullptr)
-    throw std::runtime_error("return_softmax with attn_mask is not supported by the MI355X build");
+  set_flashmask(p.s, flashmask);
+  if (return_softmax && (attn_mask != nullptr || p.s.fm_lts != nullptr))
+    throw std::runtime_error("return_softmax with attn_mask / FlashMask is not supported by the MI355X build");
   if (return_softmax) {
     FA_CHECK(softmax_ptr != nullptr && sq_r >= sq && sk_r >= sk);
     p.p_out = softmax_ptr;
@@ -157,7 +187,7 @@ bool bwd_impl(const void* dout, const void* q, const void* k, const void* v, con
               const void* softmax_d, const void* lse, const int32_t* cu_q, const int32_t* cu_k,
               void* dq, void* dk, void* dv, void* dq_accum, int b, int sq, int sk, int sq_r,
               int h, int hk, int d, int d_r, float p_dropout, float scale, bool causal,
-              bool is_bf16, hipStream_t stream, const void* attn_mask, const void* flashmask,
+              bool is_bf16, hipStream_t stream, const void* attn_mask, const FlashMaskArgs* flashmask,
               int q_row, int k_row, int v_row, int q_head, int k_head, int v_head, int o_row,
               int o_head, int q_batch, int k_batch, int v_batch, int o_batch, int dq_row,
               int dk_row, int dv_row, int dq_head, int dk_head, int dv_head, int do_row,
@@ -173,6 +203,7 @@ bool bwd_impl(const void* dout, const void* q, const void* k, const void* v, con
   std::memset(&p, 0, sizeof(p));
   p.s = make_shape(b, h, hk, sq, sk, d, scale, causal, cu_q, cu_k, padded, p_dropout, seed, offset);
   set_mask(p.s, attn_mask, mask_dims, unscale);
+  set_flashmask(p.s, flashmask);
   p.s.lse_pitch = sq;
   if (p.s.dropout && rng_state != nullptr) {   // reference capi flash_attn.cu:943-947
     const uint64_t st[2] = {seed, offset};
@@ -230,13 +261,14 @@ bool flash_attn_fwd(const void* const q, const void* const k, const void* const 
                     const int q_head_stride, const int k_head_stride, const int v_head_stride,
                     const int o_row_stride, const int o_head_stride, const int q_batch_stride,
                     const int k_batch_stride, const int v_batch_stride, const int o_batch_stride) {
-  (void)flashmask_dims; (void)flashmask_upend_ptr; (void)flashmask_downend_ptr;
-  (void)flashmask_upstart_ptr; (void)flashmask_maxmin_ptr;
+  (void)flashmask_maxmin_ptr;
+  const FlashMaskArgs fm = {flashmask_downstart_ptr, flashmask_dims, flashmask_upend_ptr,
+                            flashmask_downend_ptr, flashmask_upstart_ptr};
   return fwd_impl(q, k, v, nullptr, nullptr, rng_state, out, softmax_ptr, softmax_lse_ptr,
                   batch_size, seqlen_q, seqlen_k, seqlen_q_rounded, seqlen_k_rounded,
                   num_heads, num_heads_k, head_size,
                   head_size_rounded, p_dropout, softmax_scale, is_causal, return_softmax, is_bf16,
-                  stream, seed, offset, attn_mask, flashmask_downstart_ptr, q_row_stride,
+                  stream, seed, offset, attn_mask, &fm, q_row_stride,
                   k_row_stride, v_row_stride, q_head_stride, k_head_stride, v_head_stride,
                   o_row_stride, o_head_stride, q_batch_stride, k_batch_stride, v_batch_stride,
                   o_batch_stride, false, mask_dims, softmax_unscale);
@@ -300,12 +332,13 @@ bool flash_attn_varlen_fwd(const void* const q, const void* const k, const void*
 
 #define FA_BWD_CALL(GQA)                                                                          \
   (void)seqlen_k_rounded; (void)num_splits;                                                       \
-  (void)flashmask_dims; (void)flashmask_upend_ptr;                                                 \
-  (void)flashmask_downend_ptr; (void)flashmask_upstart_ptr; (void)flashmask_maxmin_ptr;            \
+  (void)flashmask_maxmin_ptr;                                                                      \
+  const FlashMaskArgs fm = {flashmask_downstart_ptr, flashmask_dims, flashmask_upend_ptr,          \
+                            flashmask_downend_ptr, flashmask_upstart_ptr};                         \
   return bwd_impl(dout, q, k, v, out, softmax_d, softmax_lse, nullptr, nullptr, dq, dk, dv,        \
                   dq_accum, batch_size, seqlen_q, seqlen_k, seqlen_q_rounded, num_heads,           \
                   num_heads_k, head_size, head_size_rounded, p_dropout, softmax_scale, is_causal,  \
-                  is_bf16, stream, attn_mask, flashmask_downstart_ptr, q_row_stride, k_row_stride, \
+                  is_bf16, stream, attn_mask, &fm, q_row_stride, k_row_stride,                     \
                   v_row_stride, q_head_stride, k_head_stride, v_head_stride, o_row_stride,         \
                   o_head_stride, q_batch_stride, k_batch_stride, v_batch_stride, o_batch_stride,   \
                   dq_row_stride, dk_row_stride, dv_row_stride, dq_head_stride, dk_head_stride,     \

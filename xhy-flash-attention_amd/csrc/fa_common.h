@@ -307,6 +307,27 @@ __device__ inline const unsigned short* mask_row_ptr(const Shape& s, int bidb, i
   return (const unsigned short*)s.mask + r * s.mask_row;
 }
 
+// FlashMask: offset of the (batch, head) column-bound vectors (reference row_offset_sparse_mask,
+// flash_fwd_kernel.h:1109: (bidb * h_sparsemask + bidh / (h / h_sparsemask)) * seqlen_k).
+template <typename Shape>
+__device__ inline int64_t fm_base(const Shape& s, int bidb, int head) {
+  return ((int64_t)bidb * s.fm_h + head / (s.h / s.fm_h)) * s.seqlen_k;
+}
+// Whether FlashMask removes (row, key); `col` points at the key's bounds (fm_base + key).  Unsigned
+// compares as in the reference (softmax.h:180-298): apply_sparse_mask_causal(_withend) for causal,
+// apply_sparse_mask pairwise (LT and UT ranges) when upstart is given, else rows >= LTStart or
+// < UTEnd.  The causal (key > row) and key-bound parts stay with the caller.
+template <bool CAUSAL, typename Shape>
+__device__ inline bool fm_masked(const Shape& s, int64_t col, int row) {
+  const unsigned r = (unsigned)row;
+  const unsigned lts = (unsigned)s.fm_lts[col];
+  if (CAUSAL) return r >= lts && (s.fm_lte == nullptr || r < (unsigned)s.fm_lte[col]);
+  const unsigned ute = (unsigned)s.fm_ute[col];
+  if (s.fm_uts != nullptr)
+    return (r >= lts && r < (unsigned)s.fm_lte[col]) || (r >= (unsigned)s.fm_uts[col] && r < ute);
+  return r >= lts || r < ute;
+}
+
 // The same with heads taken hp at a time: the XCD of group j walks groups of hp of its heads, and
 // inside a group block-major / head-minor (block 0 -- the heaviest causal block -- of every head of
 // the group first).  hp = 1 is xcd_order.  A larger hp keeps fewer heads' streams in flight than

@@ -51,7 +51,9 @@ constexpr int kFwdBufs = 4;   // K ring depth: tiles nb, nb+1 read while nb+2, n
 constexpr float kFwdRescaleThr = 8.f;   // deferred-max threshold, log2 units (P <= 256)
 constexpr float kFwdSumThr = 256.f;     // fast-path guard on a lane's per-tile sum of P (= 2^8)
 
-template <bool BF16, int D, bool CAUSAL, bool DROPOUT>
+// MASKED: the dense additive mask and/or FlashMask are present; such a launch has no fast path (every
+// tile takes the per-element general path), and the unmasked instantiations carry no mask code.
+template <bool BF16, int D, bool CAUSAL, bool DROPOUT, bool MASKED>
 __global__ void __launch_bounds__(FwdTile<D>::NW * 64, FwdTile<D>::MINB) fwd_kernel(const FwdParams p) {
   using E = Elt<BF16>;
   constexpr int NW = FwdTile<D>::NW;
@@ -139,8 +141,9 @@ __global__ void __launch_bounds__(FwdTile<D>::NW * 64, FwdTile<D>::MINB) fwd_ker
 
   const int n_end = CAUSAL ? min(sk, m0 + BM) : sk;
   const int nblk = n_end > 0 ? (n_end + BN - 1) / BN : 0;
-  // tiles [0, nfast) need no mask for any row of the workgroup (none at all with a dense mask)
-  const int nfast = s.mask ? 0 : min(nblk, (CAUSAL ? min(sk, m0 + 1) : sk) / BN);
+  // tiles [0, nfast) need no mask for any row of the workgroup (none at all with a dense mask or
+  // FlashMask)
+  const int nfast = MASKED ? 0 : min(nblk, (CAUSAL ? min(sk, m0 + 1) : sk) / BN);
 
   // ---- LDS-DMA of K/V tiles: per-lane byte offsets of this wave's 1-KiB pieces ----
   // piece pc covers rows 16*(pc % (BN/16)) .. +15 of panel pc / (BN/16); lane l writes
@@ -340,7 +343,7 @@ __global__ void __launch_bounds__(FwdTile<D>::NW * 64, FwdTile<D>::MINB) fwd_ker
   lds_barrier();
 
   // ---- fast path: unmasked tiles, QK^T of the next tile overlapped with this tile's softmax ----
-  if (nfast > 0) {
+  if (!MASKED && nfast > 0) {
     f32x16_t sa[NT], sb[NT];
     qk(kslot(0), sa);
     rescale(rowmax(sa));   // first tile: running max from an explicit max pass
@@ -397,15 +400,26 @@ __global__ void __launch_bounds__(FwdTile<D>::NW * 64, FwdTile<D>::MINB) fwd_ker
     if (active) {
       f32x16_t st[NT];
       qk(kslot(nb), st);
-      const u16* mrow = mask_row_ptr(s, bidb, head, qi < sq ? qi : 0);
 #pragma unroll
       for (int t = 0; t < NT; ++t)
 #pragma unroll
         for (int g = 0; g < 16; ++g) {
           const int key = n0 + t * 32 + acc_row(g, hh);
           if (key >= sk || (CAUSAL && key > qi)) st[t][g] = kNegInf;
-          else if (mrow != nullptr) st[t][g] += E::to_f32(mrow[key]) * s.mask_unscale;
         }
+      if constexpr (MASKED) {
+        const u16* mrow = mask_row_ptr(s, bidb, head, qi < sq ? qi : 0);
+        const int64_t fmb = s.fm_lts ? fm_base(s, bidb, head) : 0;
+#pragma unroll
+        for (int t = 0; t < NT; ++t)
+#pragma unroll
+          for (int g = 0; g < 16; ++g) {
+            const int key = n0 + t * 32 + acc_row(g, hh);
+            if (key >= sk || (CAUSAL && key > qi)) continue;
+            if (s.fm_lts != nullptr && fm_masked<CAUSAL>(s, fmb + key, qi)) st[t][g] = kNegInf;
+            else if (mrow != nullptr) st[t][g] += E::to_f32(mrow[key]) * s.mask_unscale;
+          }
+      }
       rescale(rowmax(st));
       i16x8_t pf[2 * NT];
       softmax_pack(st, pf, n0);
@@ -494,7 +508,10 @@ template <bool BF16, int D, bool CAUSAL, bool DROPOUT>
 static void run_fwd(const FwdParams& p, hipStream_t stream) {
   dim3 grid(p.s.b * p.s.h * p.num_m_blocks);   // 1-D: heads fastest, heaviest query block first
   prof_begin(kTimeFwd, stream);
-  hipLaunchKernelGGL((fwd_kernel<BF16, D, CAUSAL, DROPOUT>), grid, dim3(FwdTile<D>::NW * 64), 0, stream, p);
+  if (p.s.mask != nullptr || p.s.fm_lts != nullptr)
+    hipLaunchKernelGGL((fwd_kernel<BF16, D, CAUSAL, DROPOUT, true>), grid, dim3(FwdTile<D>::NW * 64), 0, stream, p);
+  else
+    hipLaunchKernelGGL((fwd_kernel<BF16, D, CAUSAL, DROPOUT, false>), grid, dim3(FwdTile<D>::NW * 64), 0, stream, p);
   prof_end(kTimeFwd, stream);
 }
 

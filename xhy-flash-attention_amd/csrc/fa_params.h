@@ -41,6 +41,15 @@ struct AttnShape {
   int mask_h, mask_sq;
   int64_t mask_row;
   float mask_unscale;
+  // FlashMask column-range mask (reference Flash_fwd_params flashmask_*_ptr / h_sparsemask, flash.h;
+  // applied in softmax.h:180-298): per (batch, mask head, key) int32 row bounds; fm_lts == nullptr:
+  // none.  Causal: LT range [lts, lte) (lte nullptr = to the end).  Non-causal: [lts, lte) and
+  // [uts, ute) when uts is given, else rows >= lts or < ute.  See fm_masked (fa_common.h).
+  const int* fm_lts;
+  const int* fm_lte;
+  const int* fm_uts;
+  const int* fm_ute;
+  int fm_h;
 };
 
 struct FwdParams {
