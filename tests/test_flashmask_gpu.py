@@ -143,6 +143,48 @@ def test_flashmask_fwd_bwd(d, sq, h, hk, hm, mode, dtype):
         assert ok, f"{name}: {err:.3e} > {bound:.3e}"
 
 
+@pytest.mark.parametrize("mode", ["doc16", "band", "band4", "doc_end"])
+@pytest.mark.parametrize("d", [64, 128, 256])
+def test_flashmask_tile_skip(mode, d):
+    """Masks that hide whole tiles (the kernels skip them): many documents, a sliding band."""
+    torch.manual_seed(1)
+    rng = np.random.default_rng(7)
+    b, sq, h, hk, hm = 1, 2048 + 37, 2, 1, 1
+    q = torch.randn(b, sq, h, d, device=DEV, dtype=torch.bfloat16)
+    k = torch.randn(b, sq, hk, d, device=DEV, dtype=torch.bfloat16)
+    v = torch.randn(b, sq, hk, d, device=DEV, dtype=torch.bfloat16)
+    dout = torch.randn(b, sq, h, d, device=DEV, dtype=torch.bfloat16)
+    key = np.arange(sq)
+    if mode in ("doc16", "doc_end"):
+        cuts = np.sort(rng.choice(np.arange(1, sq), size=15, replace=False))
+        lts = document_lts(np.diff(np.concatenate([[0], cuts, [sq]])), sq)[None, None]
+        causal, bnd = True, dict(lts=lts)
+        if mode == "doc_end":   # LT range [doc end, doc end + 300): rows after that see the key again
+            bnd["lte"] = np.minimum(lts + 300, sq).astype(np.int32)
+    elif mode == "band":        # |q - k| <= 100
+        causal, bnd = False, dict(lts=(key + 101)[None, None].astype(np.int32),
+                                  ute=np.maximum(key - 100, 0)[None, None].astype(np.int32))
+    else:                       # two bands via the 4-bound form
+        causal, bnd = False, dict(lts=np.minimum(key + 101, sq)[None, None].astype(np.int32),
+                                  lte=np.full((1, 1, sq), sq, np.int32),
+                                  uts=np.zeros((1, 1, sq), np.int32),
+                                  ute=np.maximum(key - 100, 0)[None, None].astype(np.int32))
+    scale = d ** -0.5
+    out, lse, dq, dk, dv = _capi(q, k, v, dout, scale, causal, **bnd)
+    keep = torch.from_numpy(flashmask_keep(bnd["lts"], sq, causal, lte=bnd.get("lte"),
+                                           uts=bnd.get("uts"), ute=bnd.get("ute"))).to(DEV)
+    qc, kc, vc = (x.clone().requires_grad_() for x in (q, k, v))
+    ref = _ref(qc, kc, vc, keep, scale)
+    pt = _ref(qc, kc, vc, keep, scale, upcast=False)
+    ok, err, bound = check_within_bound(out, ref, pt)
+    assert ok, f"out: {err:.3e} > {bound:.3e}"
+    gr = torch.autograd.grad(ref, (qc, kc, vc), dout)
+    gp = torch.autograd.grad(pt, (qc, kc, vc), dout)
+    for name, got, r, p in zip(("dq", "dk", "dv"), (dq, dk, dv), gr, gp):
+        ok, err, bound = check_within_bound(got, r, p, floor=1e-3)
+        assert ok, f"{name}: {err:.3e} > {bound:.3e}"
+
+
 def test_flashmask_argument_checks():
     import flash_attn_2_cuda as m
 

@@ -245,9 +245,10 @@ __global__ void __launch_bounds__(DkdvTile<D>::NW * 64, 1) bwd_dkdv_kernel(const
   // slower at C3 than this order under xcd_order.)
   auto slice_head = [&](int it) { return it / ns; };
   auto slice_q0 = [&](int it) { return (m_first + it % ns) * BQ; };
-  auto issue = [&](int it) {
-    const int hq = h_begin + slice_head(it);
-    const int q0 = slice_q0(it);
+  // slice `sid` into ring position `it` (the same except when FlashMask skips slices)
+  auto issue = [&](int sid, int it) {
+    const int hq = h_begin + slice_head(sid);
+    const int q0 = slice_q0(sid);
     char* qdst = smem + (it % 3) * QSLOT;
     char* odst = smem + OBASE + (it & 1) * QTILE;
     const u16* Qp = (const u16*)p.q + geo.q_off + (int64_t)hq * p.q_head + (int64_t)q0 * p.q_row;
@@ -331,6 +332,11 @@ __global__ void __launch_bounds__(DkdvTile<D>::NW * 64, 1) bwd_dkdv_kernel(const
   char* const dscr = smem + XBASE + 2 * XBUF + kg * 1024;
   auto p_step = [&](auto MASKC, f32x16_t (&sp)[NQT], int q0, int it_head, char* xw, i16x8_t (&fr)[2 * NQT]) {
     constexpr bool MASK = decltype(MASKC)::value;
+    // FlashMask bounds of this lane's key for this slice's head, loaded once per slice
+    FmCol fc = {0u, 0xffffffffu, 0u, 0u};
+    const bool fm_on = MASK && MASKED && s.fm_lts != nullptr;
+    if constexpr (MASK && MASKED)
+      if (fm_on) fc = fm_load(s, fm_base(s, bidb, h_begin + it_head) + (key < sk ? key : 0));
 #pragma unroll
     for (int qi = 0; qi < NQT; ++qi) {
       unsigned rb[4];
@@ -351,8 +357,7 @@ __global__ void __launch_bounds__(DkdvTile<D>::NW * 64, 1) bwd_dkdv_kernel(const
             bool out = key >= sk || q >= sq || (CAUSAL && key > q);
             float add = 0.f;
             if constexpr (MASKED) {
-              out = out || (s.fm_lts != nullptr &&
-                            fm_masked<CAUSAL>(s, fm_base(s, bidb, h_begin + it_head) + key, q));
+              out = out || (fm_on && fm_hidden<CAUSAL>(fc, s.fm_uts != nullptr, q));
               const u16* mrow = out ? nullptr : mask_row_ptr(s, bidb, h_begin + it_head, q);
               if (mrow != nullptr) add = E::to_f32(mrow[key]) * s.mask_unscale;
             }
@@ -405,7 +410,30 @@ __global__ void __launch_bounds__(DkdvTile<D>::NW * 64, 1) bwd_dkdv_kernel(const
   // block and then feeds the matrix pipe, while the P wave's exp-heavy block can wait; measured at
   // C3: dS waves at prio 1 +9%, P waves at prio 1 +5%, versus none.
   if (!pwave) __builtin_amdgcn_s_setprio(1);
-  if (total > 0) issue(0);
+  // FlashMask slice skip: a slice is dead when the bounds hide every key of this workgroup from
+  // every row of the slice (fm_tile_dead per 64 keys); all waves walk the same live slices
+  auto slice_dead = [&](int sid) {
+    if constexpr (!MASKED) {
+      return false;
+    } else {
+      if (s.fm_lts == nullptr) return false;
+      const int q0 = slice_q0(sid);
+      const int64_t base = fm_base(s, bidb, h_begin + slice_head(sid));
+#pragma unroll
+      for (int k0 = 0; k0 < BKN; k0 += 64)
+        if (!fm_tile_dead<CAUSAL>(s, base, n0 + k0, min(64, BKN - k0), sk, q0, min(q0 + BQ, sq), lane))
+          return false;
+      return true;
+    }
+  };
+  auto next_live = [&](int sid) {
+    if (sid >= total) return total;
+    ++sid;
+    while (sid < total && slice_dead(sid)) ++sid;
+    return sid;
+  };
+  int sid = next_live(-1);
+  if (sid < total) issue(sid, 0);
   wait_vmem_all();   // K/V fragments and slice 0 (compiler-visible: no vmcnt waits inside the loop)
   lds_barrier();
 
@@ -414,10 +442,13 @@ __global__ void __launch_bounds__(DkdvTile<D>::NW * 64, 1) bwd_dkdv_kernel(const
   //   dS waves: dS''(it-1) from sp (VALU) | sp = dP''(it) (MFMA) |                 | dK'' += Q(it-1)^T dS''
   //   P waves:                            | sp = S(it)     (MFMA) | P(it) (VALU)    | dV   += dO(it)^T P
   f32x16_t sp[NQT];  // S of this slice (P waves) / dP'' of the previous slice (dS waves)
-  for (int it = 0; it < total; ++it) {
-    if (it + 1 < total) issue(it + 1);
-    const int q0 = slice_q0(it);
-    const int it_head = slice_head(it);   // query head of this slice within the group
+  int it = 0;   // ring position of slice sid (the same slice without a mask)
+  for (; MASKED ? sid < total : it < total; ++it) {
+    const int cur = MASKED ? sid : it;
+    const int nxt = MASKED ? next_live(sid) : it + 1;
+    if (nxt < total) issue(nxt, it + 1);
+    const int q0 = slice_q0(cur);
+    const int it_head = slice_head(cur);   // query head of this slice within the group
     const int qs = (it % 3) * QSLOT;
     const float* lt = (const float*)(smem + qs + QTILE);
     const int os = OBASE + (it & 1) * QTILE;
@@ -442,11 +473,13 @@ __global__ void __launch_bounds__(DkdvTile<D>::NW * 64, 1) bwd_dkdv_kernel(const
     }
     if (pwave || it > 0) phase2(pwave ? os : ((it + 2) % 3) * QSLOT, fr);   // dV^T / dK''^T
     wait_dma_keep_and_barrier(0);
+    if constexpr (MASKED) sid = nxt;
   }
-  if (!pwave && total > 0) {   // the last slice's dK update (no DMA after it: its Q is resident)
+  const int nlive = MASKED ? it : total;
+  if (!pwave && nlive > 0) {   // the last slice's dK update (no DMA after it: its Q is resident)
     i16x8_t fr[2 * NQT];
-    ds_step(sp, xw_of(total - 1), (const float*)(smem + ((total - 1) % 3) * QSLOT + QTILE) + 64, fr);
-    phase2(((total - 1) % 3) * QSLOT, fr);
+    ds_step(sp, xw_of(nlive - 1), (const float*)(smem + ((nlive - 1) % 3) * QSLOT + QTILE) + 64, fr);
+    phase2(((nlive - 1) % 3) * QSLOT, fr);
   }
 
   // ---- epilogue: dV = (dV^T)^T from the P waves, dK = -scale * (dK''^T)^T from the dS waves ----
@@ -549,9 +582,10 @@ __global__ void __launch_bounds__(DqTile<D>::NW * 64, DqTile<D>::MINB) bwd_dq_ke
     voff_k[j] = dma_voff<BN>(wave + j * NW, lane, p.k_row, dlim);
     voff_v[j] = dma_voff<BN>(wave + j * NW, lane, p.v_row, dlim);
   }
-  auto issue = [&](int nb) {
+  // K/V tile `nb` into ring position `pos` (the same except when FlashMask skips tiles)
+  auto issue_at = [&](int nb, int pos) {
     const int n0 = nb * BN;
-    char* dst = smem + (nb % kBwdBufs) * 2 * TILE;
+    char* dst = smem + (pos % kBwdBufs) * 2 * TILE;
     const buf_rsrc_t rk = make_rsrc(K + (int64_t)n0 * p.k_row, rec_bytes(sk - n0, p.k_row, 2));
     const buf_rsrc_t rv = make_rsrc(V + (int64_t)n0 * p.v_row, rec_bytes(sk - n0, p.v_row, 2));
 #pragma unroll
@@ -570,10 +604,10 @@ __global__ void __launch_bounds__(DqTile<D>::NW * 64, DqTile<D>::MINB) bwd_dq_ke
 #pragma unroll
     for (int g = 0; g < 16; ++g) dq[t][g] = 0.f;
 
-  auto tile = [&](auto MASKC, int nb) {
+  auto tile = [&](auto MASKC, int nb, int pos) {
     constexpr bool MASK = decltype(MASKC)::value;
     const int n0 = nb * BN;
-    const int kt = (nb % kBwdBufs) * 2 * TILE;
+    const int kt = (pos % kBwdBufs) * 2 * TILE;
     const TileAddr tk(lb, kt), tv(lb, kt + TILE);
     f32x16_t st[NT], pt[NT];
     static_for<0, NT>([&](auto T) {
@@ -651,19 +685,33 @@ __global__ void __launch_bounds__(DqTile<D>::NW * 64, DqTile<D>::MINB) bwd_dq_ke
   for (int j = 0; j < PPW; ++j)
     if (PIECES % NW == 0 || wave + j * NW < PIECES) ndma += 2;
 
-  if (nblk > 0) issue(0);
+  // FlashMask tile skip, as in fwd_kernel: all waves walk the same sequence of live tiles
+  auto next_live = [&](int nb) {
+    if (nb >= nblk) return nblk;
+    ++nb;
+    if constexpr (MASKED)
+      if (s.fm_lts != nullptr)
+        while (nb < nblk && fm_tile_dead<CAUSAL>(s, fmb, nb * BN, BN, sk, m0, min(m0 + BM, sq), lane)) ++nb;
+    return nb;
+  };
+  const int tq0 = next_live(-1), tq1 = next_live(tq0);
+  if (tq0 < nblk) issue_at(tq0, 0);
   wait_vmem_all();   // Q / dO fragments, LSE / D and tile 0 (compiler-visible)
-  if (nblk > 1) issue(1);
+  if (tq1 < nblk) issue_at(tq1, 1);
   lds_barrier();
   for (int nb = 0; nb < nfast; ++nb) {
-    if (nb + 2 < nblk) issue(nb + 2);
-    tile(std::false_type{}, nb);
+    if (nb + 2 < nblk) issue_at(nb + 2, nb + 2);
+    tile(std::false_type{}, nb, nb);
     wait_dma_keep_and_barrier(nb + 2 < nblk ? ndma : 0);
   }
-  for (int nb = nfast; nb < nblk; ++nb) {
-    if (nb + 2 < nblk) issue(nb + 2);
-    if ((wq0 < sq) && (!CAUSAL || nb * BN <= wq0 + 31)) tile(std::true_type{}, nb);
-    wait_dma_keep_and_barrier(nb + 2 < nblk ? ndma : 0);
+  // ring position pos holds tile nb; a1 is the next live tile (already in flight)
+  int nb = MASKED ? tq0 : nfast, a1 = MASKED ? tq1 : nfast + 1;
+  for (int pos = nfast; nb < nblk; ++pos) {
+    const int a2 = next_live(a1);
+    if (a2 < nblk) issue_at(a2, pos + 2);
+    if ((wq0 < sq) && (!CAUSAL || nb * BN <= wq0 + 31)) tile(std::true_type{}, nb, pos);
+    wait_dma_keep_and_barrier(a2 < nblk ? ndma : 0);
+    nb = a1; a1 = a2;
   }
 
   if (q_ok) {

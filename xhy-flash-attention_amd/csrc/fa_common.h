@@ -313,19 +313,62 @@ template <typename Shape>
 __device__ inline int64_t fm_base(const Shape& s, int bidb, int head) {
   return ((int64_t)bidb * s.fm_h + head / (s.h / s.fm_h)) * s.seqlen_k;
 }
-// Whether FlashMask removes (row, key); `col` points at the key's bounds (fm_base + key).  Unsigned
-// compares as in the reference (softmax.h:180-298): apply_sparse_mask_causal(_withend) for causal,
-// apply_sparse_mask pairwise (LT and UT ranges) when upstart is given, else rows >= LTStart or
-// < UTEnd.  The causal (key > row) and key-bound parts stay with the caller.
+// The bounds of one key column (absent vectors: neutral values) and whether they hide `row`.
+// Unsigned compares as in the reference (softmax.h:180-298): apply_sparse_mask_causal(_withend) for
+// causal (LTEnd absent = to the end), apply_sparse_mask pairwise (LT and UT ranges) when upstart is
+// given, else rows >= LTStart or < UTEnd.  The causal (key > row) and key-bound parts stay with the
+// caller.
+struct FmCol {
+  unsigned lts, lte, uts, ute;
+};
+template <typename Shape>
+__device__ inline FmCol fm_load(const Shape& s, int64_t col) {
+  FmCol c;
+  c.lts = (unsigned)s.fm_lts[col];
+  c.lte = s.fm_lte ? (unsigned)s.fm_lte[col] : 0xffffffffu;
+  c.uts = s.fm_uts ? (unsigned)s.fm_uts[col] : 0u;
+  c.ute = s.fm_ute ? (unsigned)s.fm_ute[col] : 0u;
+  return c;
+}
+template <bool CAUSAL>
+__device__ inline bool fm_hidden(const FmCol& c, bool pairwise, int row) {
+  const unsigned r = (unsigned)row;
+  if (CAUSAL) return r >= c.lts && r < c.lte;
+  if (pairwise) return (r >= c.lts && r < c.lte) || (r >= c.uts && r < c.ute);
+  return r >= c.lts || r < c.ute;
+}
+// Whether FlashMask removes (row, key); `col` = fm_base + key.
 template <bool CAUSAL, typename Shape>
 __device__ inline bool fm_masked(const Shape& s, int64_t col, int row) {
-  const unsigned r = (unsigned)row;
-  const unsigned lts = (unsigned)s.fm_lts[col];
-  if (CAUSAL) return r >= lts && (s.fm_lte == nullptr || r < (unsigned)s.fm_lte[col]);
-  const unsigned ute = (unsigned)s.fm_ute[col];
-  if (s.fm_uts != nullptr)
-    return (r >= lts && r < (unsigned)s.fm_lte[col]) || (r >= (unsigned)s.fm_uts[col] && r < ute);
-  return r >= lts || r < ute;
+  return fm_hidden<CAUSAL>(fm_load(s, col), s.fm_uts != nullptr, row);
+}
+// Whether the bounds hide every key of [n0, n0 + nk) (keys >= sk count as hidden) from every row of
+// [r0, r1): the reference's per-block max/min test (mask.h:4-126 scan, flash_fwd_kernel.h:1305-
+// 1308), one key per lane (nk <= 64) and a wave reduction instead of a separate scan kernel.
+// Conservative (a mixed block counts as live); the result is wave-uniform.
+template <bool CAUSAL, typename Shape>
+__device__ inline bool fm_tile_dead(const Shape& s, int64_t base, int n0, int nk, int sk, int r0, int r1,
+                                    int lane) {
+  const int key = n0 + lane;
+  const bool ok = lane < nk && key < sk;   // other lanes: neutral values
+  const int64_t col = base + (ok ? key : 0);
+  unsigned lts = ok ? (unsigned)s.fm_lts[col] : 0u;
+  unsigned lte = (ok && s.fm_lte) ? (unsigned)s.fm_lte[col] : 0xffffffffu;
+  unsigned uts = (ok && s.fm_uts) ? (unsigned)s.fm_uts[col] : 0u;
+  unsigned ute = (ok && s.fm_ute) ? (unsigned)s.fm_ute[col] : 0xffffffffu;
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) {
+    lts = max(lts, (unsigned)__shfl_xor((int)lts, off));
+    lte = min(lte, (unsigned)__shfl_xor((int)lte, off));
+    uts = max(uts, (unsigned)__shfl_xor((int)uts, off));
+    ute = min(ute, (unsigned)__shfl_xor((int)ute, off));
+  }
+  const unsigned a = (unsigned)r0, e = (unsigned)r1;
+  bool dead;
+  if (CAUSAL) dead = a >= lts && e <= lte;
+  else if (s.fm_uts != nullptr) dead = (a >= lts && e <= lte) || (a >= uts && e <= ute);
+  else dead = a >= lts || e <= ute;
+  return __builtin_amdgcn_readfirstlane((int)dead) != 0;
 }
 
 // The same with heads taken hp at a time: the XCD of group j walks groups of hp of its heads, and

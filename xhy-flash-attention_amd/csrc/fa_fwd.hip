@@ -159,10 +159,11 @@ __global__ void __launch_bounds__(FwdTile<D>::NW * 64, FwdTile<D>::MINB) fwd_ker
     voff_k[j] = ok ? (int)(((int64_t)row * p.k_row + col) * 2) : 0x7ffffff0;
     voff_v[j] = ok ? (int)(((int64_t)row * p.v_row + col) * 2) : 0x7ffffff0;
   }
-  auto issue = [&](int nb) {
+  // DMA of K/V tile `nb` into ring position `pos` (the same except when FlashMask skips tiles)
+  auto issue_at = [&](int nb, int pos) {
     const int n0 = nb * BN;
-    char* kdst = smem + kslot(nb);
-    char* vdst = smem + vslot(nb);
+    char* kdst = smem + kslot(pos);
+    char* vdst = smem + vslot(pos);
     const int64_t kb = (int64_t)(sk - n0) * p.k_row * 2, vb = (int64_t)(sk - n0) * p.v_row * 2;
     const int krec = (int)(kb > 0x7fffffff ? 0x7fffffff : kb);
     const int vrec = (int)(vb > 0x7fffffff ? 0x7fffffff : vb);
@@ -176,6 +177,24 @@ __global__ void __launch_bounds__(FwdTile<D>::NW * 64, FwdTile<D>::MINB) fwd_ker
         dma16(rv, vdst + pc * 1024, voff_v[j]);
       }
     }
+  };
+  auto issue = [&](int nb) { issue_at(nb, nb); };
+
+  // FlashMask tile skip: a tile is dead when the bounds hide every key of it from every row
+  // [m0, min(m0 + BM, sq)) of the workgroup (fm_tile_dead).  Every wave reduces the same bounds, so
+  // all waves walk the same sequence of live tiles; dead tiles are neither loaded nor computed.
+  const int64_t fmb = (MASKED && s.fm_lts) ? fm_base(s, bidb, head) : 0;
+  auto fm_dead = [&](int nb) {
+    return fm_tile_dead<CAUSAL>(s, fmb, nb * BN, BN, sk, m0, min(m0 + BM, sq), lane);
+  };
+  // next live tile after nb (nblk when none)
+  auto next_live = [&](int nb) {
+    if (nb >= nblk) return nblk;
+    ++nb;
+    if constexpr (MASKED)
+      if (s.fm_lts != nullptr)
+        while (nb < nblk && fm_dead(nb)) ++nb;
+    return nb;
   };
   // DMA operations one issue() leaves outstanding in this wave.  Step nb reads tiles nb (V) and
   // nb+1 (K, software-pipelined QK^T) and issues nb+3; it ends waiting for nb+2 only, so nb+3
@@ -336,10 +355,12 @@ __global__ void __launch_bounds__(FwdTile<D>::NW * 64, FwdTile<D>::MINB) fwd_ker
   };
 
   if (wave >= NW / 2) __builtin_amdgcn_s_setprio(1);   // younger half: static priority (T5 static form)
-  if (nblk > 0) issue(0);
-  if (nblk > 1) issue(1);
+  // tiles at ring positions 0, 1, 2 (0, 1, 2 unless FlashMask skips tiles)
+  const int tq0 = next_live(-1), tq1 = next_live(tq0), tq2 = next_live(tq1);
+  if (tq0 < nblk) issue_at(tq0, 0);
+  if (tq1 < nblk) issue_at(tq1, 1);
   wait_vmem_all();   // Q fragments, tiles 0 and 1 (compiler-visible: no vmcnt waits inside the loops)
-  if (nblk > 2) issue(2);
+  if (tq2 < nblk) issue_at(tq2, 2);
   lds_barrier();
 
   // ---- fast path: unmasked tiles, QK^T of the next tile overlapped with this tile's softmax ----
@@ -393,13 +414,16 @@ __global__ void __launch_bounds__(FwdTile<D>::NW * 64, FwdTile<D>::MINB) fwd_ker
   }
 
   // ---- general path: causal diagonal / ragged tiles, per-element masks ----
-  for (int nb = nfast; nb < nblk; ++nb) {
+  // ring position pos holds tile nb; a1, a2 are the next two live tiles (already in flight)
+  int nb = MASKED ? tq0 : nfast, a1 = MASKED ? tq1 : nfast + 1, a2 = MASKED ? tq2 : nfast + 2;
+  for (int pos = nfast; nb < nblk; ++pos) {
     const int n0 = nb * BN;
-    if (nb + 3 < nblk) issue(nb + 3);
+    const int a3 = next_live(a2);
+    if (a3 < nblk) issue_at(a3, pos + 3);
     const bool active = (wq0 < sq) && (!CAUSAL || n0 <= wq0 + 31);
     if (active) {
       f32x16_t st[NT];
-      qk(kslot(nb), st);
+      qk(kslot(pos), st);
 #pragma unroll
       for (int t = 0; t < NT; ++t)
 #pragma unroll
@@ -409,7 +433,6 @@ __global__ void __launch_bounds__(FwdTile<D>::NW * 64, FwdTile<D>::MINB) fwd_ker
         }
       if constexpr (MASKED) {
         const u16* mrow = mask_row_ptr(s, bidb, head, qi < sq ? qi : 0);
-        const int64_t fmb = s.fm_lts ? fm_base(s, bidb, head) : 0;
 #pragma unroll
         for (int t = 0; t < NT; ++t)
 #pragma unroll
@@ -423,9 +446,10 @@ __global__ void __launch_bounds__(FwdTile<D>::NW * 64, FwdTile<D>::MINB) fwd_ker
       rescale(rowmax(st));
       i16x8_t pf[2 * NT];
       softmax_pack(st, pf, n0);
-      pv(vslot(nb), pf);
+      pv(vslot(pos), pf);
     }
-    tile_sync(nb + 3 < nblk);
+    tile_sync(a3 < nblk);
+    nb = a1; a1 = a2; a2 = a3;
   }
 
   // ---- epilogue ----
