@@ -380,6 +380,23 @@ bool flash_attn_varlen_bwd_gqa(const void * const dout, const void * const q,
                                const int dv_batch_stride, const int do_batch_stride,
                                const bool varlen_padded_input);
 
+/* Rotary position embedding of the attention modules; replaces the reference's torch extension
+ * op rotary_emb.apply_rotary (csrc/rotary/rotary.cpp:16-37, rotary_cuda.cu:9-45) as used by
+ * flash_attn/layers/rotary.py:35-196.  x, out: (batch, seqlen, num_heads, >= rotary_dim) with
+ * ELEMENT strides and a contiguous last dim (out may alias x); cos, sin: (seqlen, rotary_dim / 2)
+ * with row stride cos_row_stride, input dtype.  For each pair (x1, x2) -- the two halves of the
+ * first rotary_dim columns, or (even, odd) columns when interleaved -- writes
+ * x1 cos - x2 sin, x1 sin + x2 cos (conj: with -sin, the backward), fp32 arithmetic.  Columns
+ * past rotary_dim are not written. */
+bool flash_attn_rotary_apply(const void * const x, void * const out, const void * const cos,
+                             const void * const sin, const int batch_size, const int seqlen,
+                             const int num_heads, const int rotary_dim,
+                             const int64_t x_batch_stride, const int64_t x_row_stride,
+                             const int64_t x_head_stride, const int64_t out_batch_stride,
+                             const int64_t out_row_stride, const int64_t out_head_stride,
+                             const int64_t cos_row_stride, const bool interleaved, const bool conj,
+                             const bool is_bf16, hipStream_t stream);
+
 /* Tile sizes (block_m x block_n) of the forward / backward launchers for head_size. */
 void flash_attn_block_size(int head_size, int is_backward, int * block_m, int * block_n);
 

@@ -121,7 +121,11 @@ def test_mha_module_surface_on_cpu():
     FlashCrossAttention()
     m = MHA(128, 4, num_heads_kv=2)
     assert m.Wqkv.out_features == 32 * (4 + 2 * 2)
-    with pytest.raises(NotImplementedError, match="rotary_emb_dim"):
-        MHA(128, 4, rotary_emb_dim=16)
+    with pytest.raises(NotImplementedError, match="fused_bias_fc"):
+        MHA(128, 4, fused_bias_fc=True)
+    r = MHA(128, 4, rotary_emb_dim=16, rotary_emb_interleaved=True)
+    assert r.rotary_emb.dim == 16 and r.rotary_emb.interleaved
+    with pytest.raises(AssertionError):
+        MHA(128, 4, cross_attn=True, rotary_emb_dim=16)
     with pytest.raises(AssertionError):
         FlashSelfAttention()(torch.randn(1, 8, 3, 2, 64))

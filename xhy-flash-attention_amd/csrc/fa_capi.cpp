@@ -422,4 +422,31 @@ bool calc_reduced_attn_scores(const void* const q, const void* const k, const vo
 }
 bool flash_attn_varlen_bwd_gqa(FA_VARLEN_BWD_ARGS) { FA_VARLEN_BWD_CALL(true); }
 
+// reference csrc/rotary/rotary.cpp:16-37 (apply_rotary on the x1 / x2 halves, conj for the
+// backward); here on the whole (b, seqlen, h, d) view, rotary_dim leading columns.
+bool flash_attn_rotary_apply(const void* const x, void* const out, const void* const cos,
+                             const void* const sin, const int batch_size, const int seqlen,
+                             const int num_heads, const int rotary_dim, const int64_t x_batch_stride,
+                             const int64_t x_row_stride, const int64_t x_head_stride,
+                             const int64_t out_batch_stride, const int64_t out_row_stride,
+                             const int64_t out_head_stride, const int64_t cos_row_stride,
+                             const bool interleaved, const bool conj, const bool is_bf16,
+                             hipStream_t stream) {
+  FA_BEGIN
+  check_device();
+  FA_CHECK(x && out && cos && sin);
+  FA_CHECK(batch_size >= 0 && seqlen >= 0 && num_heads >= 0);
+  FA_CHECK(rotary_dim > 0 && rotary_dim % 2 == 0);
+  fa::RotaryParams p;
+  std::memset(&p, 0, sizeof(p));
+  p.x = x; p.out = out; p.cos = cos; p.sin = sin;
+  p.b = batch_size; p.seqlen = seqlen; p.h = num_heads; p.rotary_dim = rotary_dim;
+  p.x_batch = x_batch_stride; p.x_row = x_row_stride; p.x_head = x_head_stride;
+  p.o_batch = out_batch_stride; p.o_row = out_row_stride; p.o_head = out_head_stride;
+  p.cs_row = cos_row_stride;
+  fa::launch_rotary(p, interleaved, conj, is_bf16, stream);
+  return true;
+  FA_END
+}
+
 }  // extern "C"

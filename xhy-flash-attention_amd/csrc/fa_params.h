@@ -106,10 +106,25 @@ struct ReducedParams {
   int64_t k_batch, k_row, k_head;
 };
 
+// Rotary embedding (fa_rotary.hip; reference csrc/rotary): x, out (b, seqlen, h, >= rotary_dim)
+// with element strides and a contiguous last dim; cos / sin (seqlen, rotary_dim / 2), row stride
+// cs_row, in the input dtype.
+struct RotaryParams {
+  const void* x;
+  void* out;
+  const void* cos;
+  const void* sin;
+  int b, seqlen, h, rotary_dim;
+  int64_t x_batch, x_row, x_head;
+  int64_t o_batch, o_row, o_head;
+  int64_t cs_row;
+};
+
 // Host launchers (fa_fwd.hip / fa_bwd.hip).  Throw std::runtime_error on invalid configuration.
 void launch_fwd(const FwdParams& p, bool is_bf16, hipStream_t stream);
 void launch_bwd(const BwdParams& p, bool is_bf16, hipStream_t stream);
 void launch_reduced_scores(const ReducedParams& p, bool is_bf16, hipStream_t stream);
+void launch_rotary(const RotaryParams& p, bool interleaved, bool conj, bool is_bf16, hipStream_t stream);
 
 // Tile sizes the launchers use for a given head dim (reported by _get_block_size in Python).
 void fwd_block_size(int d, int* block_m, int* block_n);

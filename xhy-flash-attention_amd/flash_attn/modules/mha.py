@@ -6,9 +6,10 @@ Drop-in for the attention-core classes of the reference's ``flash_attn/modules/m
   * ``FlashCrossAttention`` (reference ``:87-142``)  -- q plus packed kv, fixed-length or varlen;
   * ``MHA``                 (reference ``:343-561``) -- the projection wrapper, restricted to what
     sits on this path: fused Wqkv (or Wq + Wkv for cross attention), MQA / GQA through
-    ``num_heads_kv``, causal / dropout / softmax_scale, and the output projection.  The reference's
-    rotary embedding, tensor-parallel linears, fused dense and KV-cache inference are out of scope
-    (SURVEY.md §8 marks the callers' own subsystems outside the hot path); asking for them raises.
+    ``num_heads_kv``, rotary embedding (``flash_attn.layers.rotary``, HIP kernel), causal /
+    dropout / softmax_scale, and the output projection.  The reference's tensor-parallel linears,
+    fused dense and KV-cache inference are out of scope (SURVEY.md §8 marks the callers' own
+    subsystems outside the hot path); asking for them raises.
 
 Same constructor arguments, forward signatures, shape conventions and dropout semantics
 (``self.drop.p`` while training, 0 in eval) as the reference.  Everything runs through
@@ -85,9 +86,10 @@ class FlashCrossAttention(nn.Module):
 class MHA(nn.Module):
     """Multi-head attention block: Wqkv -> FlashSelfAttention / FlashCrossAttention -> out_proj.
 
-    Constructor arguments follow the reference (mha.py:347-448, forward :449-561); the ones that select subsystems
-    outside this build (rotary_emb_dim > 0, fused_bias_fc, dwconv, return_residual, process_group,
-    use_flash_attn=False) are accepted only at their neutral value.
+    Constructor arguments follow the reference (mha.py:347-448, forward :449-561); rotary_emb_dim > 0
+    applies flash_attn.layers.rotary.RotaryEmbedding (HIP kernel) to q and k as the reference does.
+    The ones that select subsystems outside this build (fused_bias_fc, dwconv, return_residual,
+    process_group, use_flash_attn=False) are accepted only at their neutral value.
     """
 
     def __init__(self, embed_dim, num_heads, num_heads_kv=None, cross_attn=False, qkv_proj_bias=True,
@@ -96,7 +98,7 @@ class MHA(nn.Module):
                  rotary_emb_interleaved=False, fused_bias_fc=False, use_flash_attn=True,
                  return_residual=False, checkpointing=False, device=None, dtype=None):
         super().__init__()
-        for name, val, neutral in (("dwconv", dwconv, False), ("rotary_emb_dim", rotary_emb_dim, 0),
+        for name, val, neutral in (("dwconv", dwconv, False),
                                    ("fused_bias_fc", fused_bias_fc, False),
                                    ("use_flash_attn", use_flash_attn, True),
                                    ("return_residual", return_residual, False)):
@@ -113,6 +115,13 @@ class MHA(nn.Module):
         assert self.num_heads % self.num_heads_kv == 0, "num_heads must be divisible by num_heads_kv"
         assert self.embed_dim % num_heads == 0, "embed_dim must be divisible by num_heads"
         self.head_dim = self.embed_dim // num_heads
+        self.rotary_emb_dim = rotary_emb_dim
+        if rotary_emb_dim > 0:   # reference mha.py:379-384
+            assert not cross_attn, "MHA with rotary embedding does not support cross-attention yet"
+            from flash_attn.layers.rotary import RotaryEmbedding
+            self.rotary_emb = RotaryEmbedding(rotary_emb_dim, base=rotary_emb_base,
+                                              scale_base=rotary_emb_scale_base,
+                                              interleaved=rotary_emb_interleaved, device=device)
         qkv_dim = self.head_dim * (self.num_heads + 2 * self.num_heads_kv)
         kv_dim = 2 * self.head_dim * self.num_heads_kv
         if not self.cross_attn:
@@ -141,15 +150,21 @@ class MHA(nn.Module):
             out = self.forward(x_unpad, cu_seqlens=cu, max_seqlen=max_s)
             return pad_input(out, indices, b, s)
         h, hk, d = self.num_heads, self.num_heads_kv, self.head_dim
+        if self.rotary_emb_dim > 0 and cu_seqlens is not None:
+            raise NotImplementedError("MHA: rotary embedding with varlen / key_padding_mask input")
         if not self.cross_attn:
             qkv = self.Wqkv(x)
             lead = qkv.shape[:-1]
             if hk == h:
                 qkv = qkv.view(*lead, 3, h, d)
+                if self.rotary_emb_dim > 0:   # reference mha.py:499-500
+                    qkv = self.rotary_emb(qkv)
                 context = self.inner_attn(qkv, cu_seqlens=cu_seqlens, max_seqlen=max_seqlen)
             else:
                 q = qkv[..., : h * d].reshape(*lead, h, d)
                 kv = qkv[..., h * d:].reshape(*lead, 2, hk, d)
+                if self.rotary_emb_dim > 0:   # reference mha.py:544-545
+                    q, kv = self.rotary_emb(q, kv)
                 if cu_seqlens is not None:
                     context = self.inner_cross_attn(q, kv, cu_seqlens=cu_seqlens, max_seqlen=max_seqlen,
                                                     cu_seqlens_k=cu_seqlens, max_seqlen_k=max_seqlen)
