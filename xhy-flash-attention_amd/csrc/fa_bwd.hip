@@ -812,16 +812,7 @@ void launch_bwd(const BwdParams& p_in, bool is_bf16, hipStream_t stream) {
   void* ws = nullptr;
   p.lse_s = p.dq_accum;
   if (p.lse_s == nullptr) {
-    static bool pool_kept = false;
-    if (!pool_kept) {   // keep freed blocks in the device pool across synchronisations
-      int dev = 0;
-      hipMemPool_t pool;
-      if (hipGetDevice(&dev) == hipSuccess && hipDeviceGetDefaultMemPool(&pool, dev) == hipSuccess) {
-        uint64_t thr = UINT64_MAX;
-        (void)hipMemPoolSetAttribute(pool, hipMemPoolAttrReleaseThreshold, &thr);
-      }
-      pool_kept = true;
-    }
+    keep_pool_memory();
     const size_t bytes = (size_t)p.s.b * p.s.h * p.seqlen_q_rounded * sizeof(float);
     if (hipMallocAsync(&ws, bytes, stream) != hipSuccess)
       throw std::runtime_error("flash_attn_bwd: hipMallocAsync of the LSE scratch failed");

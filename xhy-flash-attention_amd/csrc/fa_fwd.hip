@@ -28,6 +28,7 @@
 //   * Heaviest causal query blocks are dispatched first (1-D grid, head-fastest) to shorten the tail.
 //   * Epilogue: v_permlane32_swap pairs column groups so each lane stores 16 bytes of its O row.
 //   * Waves 4-7 (the younger half of the workgroup) run at s_setprio 1 for the whole kernel.
+#include <algorithm>
 #include <stdexcept>
 #include <string>
 
@@ -53,7 +54,9 @@ constexpr float kFwdSumThr = 256.f;     // fast-path guard on a lane's per-tile 
 
 // MASKED: the dense additive mask and/or FlashMask are present; such a launch has no fast path (every
 // tile takes the per-element general path), and the unmasked instantiations carry no mask code.
-template <bool BF16, int D, bool CAUSAL, bool DROPOUT, bool MASKED>
+// SPLIT (non-causal, unmasked, no dropout, fixed-length; launch_fwd decides): blockIdx.y selects a
+// key range, treated as an attention of its own, and the epilogue writes fp32 partials.
+template <bool BF16, int D, bool CAUSAL, bool DROPOUT, bool MASKED, bool SPLIT = false>
 __global__ void __launch_bounds__(FwdTile<D>::NW * 64, FwdTile<D>::MINB) fwd_kernel(const FwdParams p) {
   using E = Elt<BF16>;
   constexpr int NW = FwdTile<D>::NW;
@@ -115,6 +118,13 @@ __global__ void __launch_bounds__(FwdTile<D>::NW * 64, FwdTile<D>::MINB) fwd_ker
   }
   const int m0 = m_block * BM;
   if (m0 >= sq) return;
+  if constexpr (SPLIT) {   // this workgroup's key range
+    static_assert(!CAUSAL && !DROPOUT && !MASKED, "split-KV is for plain non-causal launches");
+    const int n0s = blockIdx.y * p.split_tiles * BN;
+    k_off += (int64_t)n0s * p.k_row;
+    v_off += (int64_t)n0s * p.v_row;
+    sk = max(0, min(sk - n0s, p.split_tiles * BN));
+  }
 
   typedef unsigned short u16;
   const u16* __restrict__ Q = (const u16*)p.q + q_off + (int64_t)head * p.q_head;
@@ -457,6 +467,27 @@ __global__ void __launch_bounds__(FwdTile<D>::NW * 64, FwdTile<D>::MINB) fwd_ker
   const bool bad = (l_tot == 0.f) || (l_tot != l_tot);
   const float inv = bad ? 1.f : fast_rcp(l_tot) * (DROPOUT ? s.rp_dropout : 1.f);
   const float lse = bad ? __builtin_huge_valf() : m_run * s.scale + __logf(l_tot);
+  if constexpr (SPLIT) {
+    // fp32 partial O_i = O / l and LSE_i (-inf for an empty range, NaN propagates) for the combine
+    if (qi < sq) {
+      const int64_t prow = ((int64_t)blockIdx.y * s.b * s.h + bh) * s.seqlen_q + qi;
+      float* arow = p.o_acc + prow * p.acc_d;
+      const float iv = l_tot == 0.f ? 0.f : fast_rcp(l_tot);
+#pragma unroll
+      for (int dt = 0; dt < NP; ++dt)
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+          const int col = dt * 32 + 8 * u + 4 * hh;
+          if (col < dlim) {
+            const f32x4_t w = {o[dt][4 * u] * iv, o[dt][4 * u + 1] * iv, o[dt][4 * u + 2] * iv,
+                               o[dt][4 * u + 3] * iv};
+            *(f32x4_t*)(arow + col) = w;
+          }
+        }
+      if (hh == 0) p.lse_acc[prow] = l_tot == 0.f ? -__builtin_huge_valf() : m_run * s.scale + __logf(l_tot);
+    }
+    return;
+  }
   {
     // 16-byte stores: v_permlane32_swap pairs column groups (u, u+1) so that lane half 0 holds
     // columns 8u..8u+7 and half 1 columns 8u+8..8u+15 of its row (T21)
@@ -528,10 +559,66 @@ __global__ void __launch_bounds__(256) dmask_kernel(const FwdParams p) {
   *out = (u16)(E::pack2(val, 0.f) & 0xffff);
 }
 
+// Split-KV combine: one wave per (b, h, query row).  LSE = log sum_i exp(LSE_i), O = sum_i
+// exp(LSE_i - LSE) O_i (the reference's combine_attn_seqk_parallel in FA2's split-KV path, done
+// here without its shared-memory transpose: split i's weight is broadcast from lane i).
+template <bool BF16>
+__global__ void __launch_bounds__(256) splitkv_combine_kernel(const FwdParams p) {
+  using E = Elt<BF16>;
+  typedef unsigned short u16;
+  const int lane = threadIdx.x & 63;
+  const int64_t row = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);   // (b * h) * seqlen_q + q
+  const int64_t nrows = (int64_t)p.s.b * p.s.h * p.s.seqlen_q;
+  if (row >= nrows) return;
+  const int q = (int)(row % p.s.seqlen_q);
+  const int bh = (int)(row / p.s.seqlen_q);
+  const int bidb = bh / p.s.h, head = bh - bidb * p.s.h;
+  const int64_t split_stride = nrows;
+  float li = lane < p.n_split ? p.lse_acc[lane * split_stride + row] : -__builtin_huge_valf();
+  float mx = li;
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) mx = fmaxf(mx, __shfl_xor(mx, off));
+  const bool empty = mx == -__builtin_huge_valf();
+  float w = empty ? 0.f : __expf(li - mx);
+  float sum = w;
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) sum += __shfl_xor(sum, off);
+  const float lse = empty ? __builtin_huge_valf() : mx + __logf(sum);
+  w = empty ? 0.f : w / sum;
+  float acc[4] = {0.f, 0.f, 0.f, 0.f};
+  for (int i = 0; i < p.n_split; ++i) {
+    const float wi = __shfl(w, i);
+    const float* src = p.o_acc + (i * split_stride + row) * p.acc_d;
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {
+      const int col = lane + 64 * c;
+      if (col < p.s.d && wi != 0.f) acc[c] += wi * src[col];
+    }
+  }
+  u16* orow = (u16*)p.o + (int64_t)bidb * p.o_batch + (int64_t)head * p.o_head + (int64_t)q * p.o_row;
+#pragma unroll
+  for (int c = 0; c < 4; ++c) {
+    const int col = lane + 64 * c;
+    if (col < p.s.d) orow[col] = (u16)(E::pack2(acc[c], 0.f) & 0xffffu);
+  }
+  if (lane == 0) p.lse[(int64_t)bh * p.s.lse_pitch + q] = lse;
+}
+
 template <bool BF16, int D, bool CAUSAL, bool DROPOUT>
 static void run_fwd(const FwdParams& p, hipStream_t stream) {
   dim3 grid(p.s.b * p.s.h * p.num_m_blocks);   // 1-D: heads fastest, heaviest query block first
   prof_begin(kTimeFwd, stream);
+  if constexpr (!CAUSAL && !DROPOUT) {
+    if (p.n_split > 1) {
+      hipLaunchKernelGGL((fwd_kernel<BF16, D, false, false, false, true>), dim3(grid.x, p.n_split),
+                         dim3(FwdTile<D>::NW * 64), 0, stream, p);
+      const int64_t rows = (int64_t)p.s.b * p.s.h * p.s.seqlen_q;
+      hipLaunchKernelGGL((splitkv_combine_kernel<BF16>), dim3((unsigned)((rows + 3) / 4)), dim3(256), 0,
+                         stream, p);
+      prof_end(kTimeFwd, stream);
+      return;
+    }
+  }
   if (p.s.mask != nullptr || p.s.fm_lts != nullptr)
     hipLaunchKernelGGL((fwd_kernel<BF16, D, CAUSAL, DROPOUT, true>), grid, dim3(FwdTile<D>::NW * 64), 0, stream, p);
   else
@@ -580,9 +667,42 @@ void launch_fwd(const FwdParams& p_in, bool is_bf16, hipStream_t stream) {
   if (p.num_m_blocks <= 0) return;
   if ((int64_t)p.s.b * p.s.h * p.num_m_blocks > 0x7fffffff)
     throw std::runtime_error("flash_attn_fwd: batch * heads * query blocks too large for the grid");
+  // Split-KV for decode-shaped calls (FA2's num_splits heuristic, flash_api.cpp): with fewer
+  // workgroups than CUs, split the keys so that about two workgroups per CU stream K/V, each split
+  // at least 4 tiles; plain non-causal fixed-length launches only.  FLASH_ATTN_MI355X_NO_SPLITKV=1
+  // disables it (tests compare both paths).
+  void* ws = nullptr;
+  p.n_split = 1;
+  {
+    int bm, bn;
+    fwd_block_size(p.s.d, &bm, &bn);
+    const long long wgs = (long long)p.s.b * p.s.h * p.num_m_blocks;
+    const int nblk = (p.s.seqlen_k + bn - 1) / bn;
+    const char* env = getenv("FLASH_ATTN_MI355X_NO_SPLITKV");
+    const bool plain = !p.s.causal && !p.s.dropout && p.s.mask == nullptr && p.s.fm_lts == nullptr &&
+                       p.p_out == nullptr && p.s.cu_seqlens_q == nullptr && p.s.cu_seqlens_k == nullptr;
+    if (plain && !(env && env[0] == '1') && wgs < 256 && nblk >= 8) {
+      int ns = (int)std::min<long long>(64, std::min<long long>((512 + wgs - 1) / wgs, nblk / 4));
+      if (ns >= 2) {
+        p.split_tiles = (nblk + ns - 1) / ns;
+        p.n_split = (nblk + p.split_tiles - 1) / p.split_tiles;
+      }
+    }
+    if (p.n_split > 1) {
+      p.acc_d = (p.s.d + 31) / 32 * 32;
+      const size_t rows = (size_t)p.n_split * p.s.b * p.s.h * p.s.seqlen_q;
+      const size_t bytes = rows * p.acc_d * sizeof(float) + rows * sizeof(float);
+      keep_pool_memory();
+      if (hipMallocAsync(&ws, bytes, stream) != hipSuccess)
+        throw std::runtime_error("flash_attn_fwd: hipMallocAsync of the split-KV scratch failed");
+      p.o_acc = static_cast<float*>(ws);
+      p.lse_acc = p.o_acc + rows * p.acc_d;
+    }
+  }
   if (p.p_out != nullptr && (p.p_rows > 65535 * 4 || p.s.b * p.s.h > 65535))
     throw std::runtime_error("flash_attn_fwd: return_softmax grid too large");
   if (is_bf16) dispatch_fwd<true>(p, stream); else dispatch_fwd<false>(p, stream);
+  if (ws != nullptr) (void)hipFreeAsync(ws, stream);
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) throw std::runtime_error(std::string("flash_attn_fwd launch: ") + hipGetErrorString(e));
 }

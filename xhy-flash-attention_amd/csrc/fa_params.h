@@ -66,6 +66,12 @@ struct FwdParams {
   int head_group;           // xcd_order_grouped heads per group (0: head-fastest order); launch_fwd
   void* p_out;              // return_softmax (dropout only): S_dmask (b, h, sq_rounded, sk_rounded)
   int p_rows, p_cols;       // sq_rounded, sk_rounded
+  // split-KV (launch_fwd decides; decode-shaped calls): workgroup (., split) covers key tiles
+  // [split * split_tiles, +split_tiles) and writes fp32 O_i / LSE_i partials, merged by a combine
+  // kernel.  o_acc: (n_split, b, h, seqlen_q, acc_d), lse_acc: (n_split, b, h, seqlen_q).
+  int n_split, split_tiles, acc_d;
+  float* o_acc;
+  float* lse_acc;
 };
 
 struct BwdParams {
