@@ -59,3 +59,24 @@ def test_splitkv_forward(sq, sk, h, hk, d, dtype, monkeypatch):
     for name, got, rr, pp in zip("qkv", grads, rg, pg):
         ok, err, bound = check_within_bound(got, rr, pp, floor=1e-3)
         assert ok, (name, err, bound)
+
+
+@pytest.mark.parametrize("d", [64, 128])
+def test_gqa_packing_without_split(d, monkeypatch):
+    """Many sequences (no split) with grouped heads: the packed launch alone (n_split = 1)."""
+    from flash_attn.flash_attn_interface import _flash_attn_forward
+
+    torch.manual_seed(0)
+    b, sq, sk, h, hk = 160, 2, 700, 8, 2
+    q = torch.randn(b, sq, h, d, device=DEV, dtype=torch.bfloat16)
+    k = torch.randn(b, sk, hk, d, device=DEV, dtype=torch.bfloat16)
+    v = torch.randn(b, sk, hk, d, device=DEV, dtype=torch.bfloat16)
+    out, _, _, _, _, lse, _, _ = _flash_attn_forward(q, k, v, 0.0, d ** -0.5, False, False)
+    ref, _ = attention_ref(q, k, v)
+    pt, _ = attention_ref(q, k, v, upcast=False, reorder_ops=True)
+    ok, err, bound = check_within_bound(out, ref, pt)
+    assert ok, (err, bound)
+    monkeypatch.setenv("FLASH_ATTN_MI355X_NO_SPLITKV", "1")
+    out1, _, _, _, _, lse1, _, _ = _flash_attn_forward(q, k, v, 0.0, d ** -0.5, False, False)
+    torch.testing.assert_close(lse, lse1, atol=2e-5, rtol=0)
+    torch.testing.assert_close(out.float(), out1.float(), atol=2 ** -7, rtol=2 ** -7)

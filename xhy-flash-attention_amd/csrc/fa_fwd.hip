@@ -127,7 +127,8 @@ __global__ void __launch_bounds__(FwdTile<D>::NW * 64, FwdTile<D>::MINB) fwd_ker
   }
 
   typedef unsigned short u16;
-  const u16* __restrict__ Q = (const u16*)p.q + q_off + (int64_t)head * p.q_head;
+  const int G = SPLIT ? p.pack_g : 1;   // packed query heads per row group (split-KV path)
+  const u16* __restrict__ Q = (const u16*)p.q + q_off + (int64_t)head * G * p.q_head;
   const u16* __restrict__ K = (const u16*)p.k + k_off + (int64_t)kvh * p.k_head;
   const u16* __restrict__ V = (const u16*)p.v + v_off + (int64_t)kvh * p.v_head;
   u16* __restrict__ O = (u16*)p.o + o_off + (int64_t)head * p.o_head;
@@ -141,7 +142,8 @@ __global__ void __launch_bounds__(FwdTile<D>::NW * 64, FwdTile<D>::MINB) fwd_ker
   i16x8_t qf[KS];
   {
     const bool ok = qi < sq;
-    const u16* qrow = Q + (int64_t)(ok ? qi : 0) * p.q_row;
+    const u16* qrow = SPLIT ? Q + (int64_t)(ok ? qi / G : 0) * p.q_row + (int64_t)(ok ? qi % G : 0) * p.q_head
+                            : Q + (int64_t)(ok ? qi : 0) * p.q_row;
 #pragma unroll
     for (int ks = 0; ks < KS; ++ks) {
       const int d0 = 16 * ks + 8 * hh;
@@ -570,9 +572,11 @@ __global__ void __launch_bounds__(256) splitkv_combine_kernel(const FwdParams p)
   const int64_t row = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);   // (b * h) * seqlen_q + q
   const int64_t nrows = (int64_t)p.s.b * p.s.h * p.s.seqlen_q;
   if (row >= nrows) return;
-  const int q = (int)(row % p.s.seqlen_q);
+  const int qi = (int)(row % p.s.seqlen_q);   // packed row (query qi / G, head qi % G of the group)
   const int bh = (int)(row / p.s.seqlen_q);
-  const int bidb = bh / p.s.h, head = bh - bidb * p.s.h;
+  const int G = p.pack_g;
+  const int bidb = bh / p.s.h, kvh = bh - bidb * p.s.h;
+  const int q = qi / G, head = kvh * G + qi % G;
   const int64_t split_stride = nrows;
   float li = lane < p.n_split ? p.lse_acc[lane * split_stride + row] : -__builtin_huge_valf();
   float mx = li;
@@ -601,7 +605,7 @@ __global__ void __launch_bounds__(256) splitkv_combine_kernel(const FwdParams p)
     const int col = lane + 64 * c;
     if (col < p.s.d) orow[col] = (u16)(E::pack2(acc[c], 0.f) & 0xffffu);
   }
-  if (lane == 0) p.lse[(int64_t)bh * p.s.lse_pitch + q] = lse;
+  if (lane == 0) p.lse[((int64_t)bidb * p.s.h * G + head) * p.s.lse_pitch + q] = lse;
 }
 
 template <bool BF16, int D, bool CAUSAL, bool DROPOUT>
@@ -609,7 +613,7 @@ static void run_fwd(const FwdParams& p, hipStream_t stream) {
   dim3 grid(p.s.b * p.s.h * p.num_m_blocks);   // 1-D: heads fastest, heaviest query block first
   prof_begin(kTimeFwd, stream);
   if constexpr (!CAUSAL && !DROPOUT) {
-    if (p.n_split > 1) {
+    if (p.n_split > 0) {
       hipLaunchKernelGGL((fwd_kernel<BF16, D, false, false, false, true>), dim3(grid.x, p.n_split),
                          dim3(FwdTile<D>::NW * 64), 0, stream, p);
       const int64_t rows = (int64_t)p.s.b * p.s.h * p.s.seqlen_q;
@@ -671,24 +675,38 @@ void launch_fwd(const FwdParams& p_in, bool is_bf16, hipStream_t stream) {
   // workgroups than CUs, split the keys so that about two workgroups per CU stream K/V, each split
   // at least 4 tiles; plain non-causal fixed-length launches only.  FLASH_ATTN_MI355X_NO_SPLITKV=1
   // disables it (tests compare both paths).
+  // GQA packing on top (decode with grouped heads): the query heads of a kv head are packed as
+  // extra rows when seqlen_q * group fits one query block, so K/V are streamed once per kv head.
   void* ws = nullptr;
-  p.n_split = 1;
+  p.n_split = 0;   // 0: the ordinary launch
+  p.pack_g = 1;
   {
     int bm, bn;
     fwd_block_size(p.s.d, &bm, &bn);
-    const long long wgs = (long long)p.s.b * p.s.h * p.num_m_blocks;
     const int nblk = (p.s.seqlen_k + bn - 1) / bn;
     const char* env = getenv("FLASH_ATTN_MI355X_NO_SPLITKV");
     const bool plain = !p.s.causal && !p.s.dropout && p.s.mask == nullptr && p.s.fm_lts == nullptr &&
                        p.p_out == nullptr && p.s.cu_seqlens_q == nullptr && p.s.cu_seqlens_k == nullptr;
-    if (plain && !(env && env[0] == '1') && wgs < 256 && nblk >= 8) {
-      int ns = (int)std::min<long long>(64, std::min<long long>((512 + wgs - 1) / wgs, nblk / 4));
-      if (ns >= 2) {
+    const int G = p.s.h / p.s.hk;
+    const bool pack = plain && G > 1 && (long long)p.s.seqlen_q * G <= bm;
+    const long long wgs = pack ? (long long)p.s.b * p.s.hk : (long long)p.s.b * p.s.h * p.num_m_blocks;
+    if (plain && !(env && env[0] == '1') && nblk > 0 && (pack || (wgs < 256 && nblk >= 8))) {
+      int ns = 1;
+      if (wgs < 256 && nblk >= 8)
+        ns = (int)std::min<long long>(64, std::min<long long>((512 + wgs - 1) / wgs, nblk / 4));
+      if (ns >= 2 || pack) {
         p.split_tiles = (nblk + ns - 1) / ns;
         p.n_split = (nblk + p.split_tiles - 1) / p.split_tiles;
+        if (pack) {
+          p.pack_g = G;
+          p.s.h = p.s.hk;
+          p.s.seqlen_q *= G;
+          p.num_m_blocks = 1;
+        }
+        p.head_group = 0;
       }
     }
-    if (p.n_split > 1) {
+    if (p.n_split > 0) {
       p.acc_d = (p.s.d + 31) / 32 * 32;
       const size_t rows = (size_t)p.n_split * p.s.b * p.s.h * p.s.seqlen_q;
       const size_t bytes = rows * p.acc_d * sizeof(float) + rows * sizeof(float);

@@ -72,6 +72,9 @@ struct FwdParams {
   int n_split, split_tiles, acc_d;
   float* o_acc;
   float* lse_acc;
+  // GQA packing on the split-KV path: the pack_g query heads of a kv head become pack_g rows per
+  // query (s.h = kv heads, s.seqlen_q = seqlen_q * pack_g), so K/V stream once per kv head.  1: off.
+  int pack_g;
 };
 
 struct BwdParams {
