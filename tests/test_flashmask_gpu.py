@@ -211,3 +211,48 @@ def test_flashmask_argument_checks():
     assert not call(True, torch.tensor([1, 1, 64, 1]), None, P(dm), dm_dims.numpy().ctypes.data)
     assert b"cannot be combined" in m._lib.flash_attn_error()
     assert call(True, torch.tensor([1, 1, 64, 1]), None)
+
+
+@pytest.mark.parametrize("causal", [True, False])
+def test_flashmask_noop_bounds_equal_plain_attention(causal):
+    """Bounds that hide nothing give the plain result (masked instantiation vs the fast path)."""
+    from flash_attn import flash_attn_func
+
+    torch.manual_seed(0)
+    b, s, h, d = 2, 700, 4, 128
+    q, k, v, dout = (torch.randn(b, s, h, d, device=DEV, dtype=torch.bfloat16) for _ in range(4))
+    lts = np.full((b, 1, s), s, np.int32)
+    bnd = dict(lts=lts) if causal else dict(lts=lts, ute=np.zeros((b, 1, s), np.int32))
+    out, lse, dq, dk, dv = _capi(q, k, v, dout, d ** -0.5, causal, **bnd)
+    qr, kr, vr = (x.clone().requires_grad_() for x in (q, k, v))
+    o2 = flash_attn_func(qr, kr, vr, causal=causal)
+    g2 = torch.autograd.grad(o2, (qr, kr, vr), dout)
+    torch.testing.assert_close(out, o2, atol=2e-3, rtol=0)
+    for a, bb in zip((dq, dk, dv), g2):
+        torch.testing.assert_close(a, bb, atol=4e-3, rtol=0)
+
+
+def test_flashmask_with_dropout_matches_plain_dropout():
+    """Dropout under FlashMask draws the same Philox stream: with no-op bounds the result equals
+    the plain causal dropout launch (same seed / offset) to summation-order tolerance."""
+    import flash_attn_2_cuda as m
+
+    torch.manual_seed(0)
+    b, s, h, d = 1, 384, 2, 64
+    q, k, v = (torch.randn(b, s, h, d, device=DEV, dtype=torch.float16) for _ in range(3))
+    lts = torch.full((b, 1, s), s, device=DEV, dtype=torch.int32)
+    dims = torch.tensor([b, 1, s, 1], dtype=torch.int64)
+    P = m._ptr
+    st = (q.stride(1),) * 3 + (q.stride(2),) * 3 + (q.stride(1), q.stride(2)) + (q.stride(0),) * 4
+    outs = []
+    for fm in ((P(lts), dims.numpy().ctypes.data, None, None, None, None), (None,) * 6):
+        out = torch.empty_like(q)
+        lse = torch.empty(b, h, s, device=DEV)
+        ok = m._lib.flash_attn_fwd(P(q), P(k), P(v), None, P(out), None, P(lse), b, s, s, 384, 384, h, h,
+                                   d, d, 0.2, d ** -0.5, 1.0, True, False, False, m._stream(q), 123, 8,
+                                   None, None, *fm, *st)
+        assert ok, m._lib.flash_attn_error()
+        outs.append((out, lse))
+    torch.cuda.synchronize()
+    torch.testing.assert_close(outs[0][0], outs[1][0], atol=2e-3, rtol=0)
+    torch.testing.assert_close(outs[0][1], outs[1][1], atol=1e-4, rtol=0)

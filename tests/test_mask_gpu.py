@@ -153,3 +153,35 @@ def test_flashmask_and_bad_mask_dims_rejected():
                                64, 64, 0.0, 0.125, 8.0, False, False, False, m._stream(q), 0, 0,
                                P(mask), dims.numpy().ctypes.data, None, None, None, None, None, None, *st)
     assert not ok and b"mask_dims" in m._lib.flash_attn_error()
+
+
+def test_dense_mask_with_dropout_matches_plain_dropout():
+    """Dropout in the masked instantiation draws the same Philox stream as the plain launch: a zero
+    mask gives the plain dropout result (same seed / offset) to summation-order tolerance."""
+    import flash_attn_2_cuda as m
+
+    torch.manual_seed(0)
+    b, s, h, d = 1, 300, 2, 128
+    q, k, v = (torch.randn(b, s, h, d, device=DEV, dtype=torch.bfloat16) for _ in range(3))
+    mask = torch.zeros(b, 1, s, s, device=DEV, dtype=torch.bfloat16)
+    dims = torch.tensor([b, 1, s, s], dtype=torch.int64)
+    P = m._ptr
+    st = (q.stride(1),) * 3 + (q.stride(2),) * 3 + (q.stride(1), q.stride(2)) + (q.stride(0),) * 4
+    outs = []
+    for mk in ((P(mask), dims.numpy().ctypes.data), (None, None)):
+        out = torch.empty_like(q)
+        lse = torch.empty(b, h, s, device=DEV)
+        ok = m._lib.flash_attn_fwd(P(q), P(k), P(v), None, P(out), None, P(lse), b, s, s, 384, 384, h, h,
+                                   d, d, 0.3, d ** -0.5, 1.0, True, False, True, m._stream(q), 7, 4,
+                                   *mk, *([None] * 6), *st)
+        assert ok, m._lib.flash_attn_error()
+        outs.append((out, lse))
+    torch.cuda.synchronize()
+    torch.testing.assert_close(outs[0][0], outs[1][0], atol=4e-3, rtol=0)
+    torch.testing.assert_close(outs[0][1], outs[1][1], atol=1e-4, rtol=0)
+    # known defect: the non-causal masked dropout kernels at head_dim > 64 are refused (DESIGN.md)
+    out = torch.empty_like(q)
+    ok = m._lib.flash_attn_fwd(P(q), P(k), P(v), None, P(out), None, P(lse), b, s, s, 384, 384, h, h,
+                               d, d, 0.3, d ** -0.5, 1.0, False, False, True, m._stream(q), 7, 4,
+                               P(mask), dims.numpy().ctypes.data, *([None] * 6), *st)
+    assert not ok and b"not supported" in m._lib.flash_attn_error()
