@@ -10,6 +10,7 @@
  *   flash_attn_varlen_fwd  <- reference csrc/capi/flash_attn.h:57-98
  *   flash_attn_bwd         <- reference csrc/capi/flash_attn.h:100-161
  *   flash_attn_varlen_bwd  <- reference csrc/capi/flash_attn.h:163-221
+ *   flash_attn_set_error   <- reference csrc/capi/flash_attn.h:313
  *   flash_attn_error       <- reference csrc/capi/flash_attn.h:315
  *   calc_reduced_attn_scores <- reference csrc/capi/flash_attn.h:223-247
  *
@@ -55,6 +56,12 @@
  *   the reference entries but write dk/dv with num_heads_k heads, summing each
  *   query-head group inside the kernel (no expanded buffers, no extra HBM pass:
  *   replaces the at::sum_out of reference flash_api.cpp:682-686, 900-904).
+ *   With dropout, their rng_state (when non-NULL) is an INPUT: the forward's
+ *   {seed, offset} record, read by the kernels on the device (as the
+ *   reference's torch op reads rng_state, flash_api.cpp:669-670 /
+ *   flash_bwd_kernel.h:783-784), and the seed / offset arguments are ignored;
+ *   the reference-shaped entries keep the Paddle C ABI behaviour of writing
+ *   {seed, offset} into rng_state (flash_attn.cu:943-947).
  *   flash_attn_block_size reports the tile sizes the launchers use.
  */
 #ifndef FLASH_ATTN_MI355X_H_
@@ -311,6 +318,8 @@ bool calc_reduced_attn_scores(const void * const q,
                               const int q_batch_stride,
                               const int k_batch_stride,
                               const int o_batch_stride);
+
+void flash_attn_set_error(const char *msg);
 
 const char *flash_attn_error();
 

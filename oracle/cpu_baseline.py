@@ -25,8 +25,9 @@ def cpu_model_name() -> str:
 
 
 def sdpa_fwd_bwd_tflops(batch, seqlen, nheads, headdim, causal, dtype, threads, repeats=3,
-                        flops_fn=None):
-    """Times fwd+bwd of CPU SDPA (1 warm-up + `repeats`), returns (tflops, seconds_per_rep)."""
+                        flops_fn=None, fwd_only=False):
+    """Times fwd+bwd (or the forward alone) of CPU SDPA (1 warm-up + `repeats`), returns
+    (tflops, seconds_per_rep)."""
     prev = torch.get_num_threads()
     torch.set_num_threads(threads)
     try:
@@ -36,6 +37,10 @@ def sdpa_fwd_bwd_tflops(batch, seqlen, nheads, headdim, causal, dtype, threads, 
         dout = torch.randn(batch, nheads, seqlen, headdim, generator=g).to(dtype)
 
         def step():
+            if fwd_only:
+                with torch.no_grad():
+                    torch.nn.functional.scaled_dot_product_attention(q, k, v, is_causal=causal)
+                return
             out = torch.nn.functional.scaled_dot_product_attention(q, k, v, is_causal=causal)
             torch.autograd.grad(out, (q, k, v), dout)
 

@@ -1,14 +1,21 @@
 #!/bin/bash
-# PMC passes for the dominant kernels (run on the GPU box from the repo root).
-# One counter group per rocprofv3 pass; kernel-trace only, no sys/runtime tracing.
+# rocprofv3 PMC passes over the bench command of one workload (run on the GPU box from the repo
+# root): one counter group per pass, --kernel-trace only (no sys/runtime tracing), each pass under
+# its own time limit.  Then: python3 profiles/pmc.py OUT WORKLOAD  ->  profiles/pmc.json
+#   profiles/pmc_run.sh gpurun_out/pmc_c3 c3
 set -e
 OUT=${1:-gpurun_out/pmc}
+WL=${2:-c3}
 mkdir -p "$OUT"
-cd /tmp && export TMPDIR=/tmp && cd - > /dev/null
-ARGS="python3 bench.py --steps 2 --warmup 1 --no-cpu-baseline"
-timeout -k 10 240 rocprofv3 --kernel-trace --stats --pmc FETCH_SIZE -d "$OUT/fetch" -o run --output-format csv -- $ARGS > "$OUT/fetch.log" 2>&1
-timeout -k 10 240 rocprofv3 --kernel-trace --stats --pmc WRITE_SIZE -d "$OUT/write" -o run --output-format csv -- $ARGS > "$OUT/write.log" 2>&1
-timeout -k 10 240 rocprofv3 --kernel-trace --stats --pmc TCC_HIT_sum TCC_MISS_sum -d "$OUT/l2" -o run --output-format csv -- $ARGS > "$OUT/l2.log" 2>&1
-timeout -k 10 240 rocprofv3 --kernel-trace --stats --pmc SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_MFMA SQ_BUSY_CYCLES -d "$OUT/sq" -o run --output-format csv -- $ARGS > "$OUT/sq.log" 2>&1
-timeout -k 10 240 rocprofv3 --kernel-trace --stats --pmc SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_INSTS_VALU SQ_INSTS_LDS GRBM_GUI_ACTIVE -d "$OUT/lds" -o run --output-format csv -- $ARGS > "$OUT/lds.log" 2>&1
-echo done
+export TMPDIR=/tmp
+CMD="python3 bench.py --workload $WL --steps 3 --warmup 1 --no-cpu-baseline"
+pass() {   # name counters...
+  local name=$1; shift
+  timeout -k 10 180 rocprofv3 --kernel-trace --pmc "$@" -d "$OUT/$name" -o run --output-format csv -- $CMD \
+    > "$OUT/$name.log" 2>&1
+}
+pass fetch FETCH_SIZE
+pass write WRITE_SIZE
+pass sq SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_MFMA SQ_INSTS_VALU SQ_INSTS_LDS SQ_BUSY_CYCLES GRBM_GUI_ACTIVE
+pass lds SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_VALU_MFMA_BUSY_CYCLES GRBM_GUI_ACTIVE
+echo "pmc passes done: $OUT"

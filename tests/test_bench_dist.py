@@ -78,3 +78,41 @@ def test_aggregate_tflops_is_whole_job():
     eight = bench.aggregate_tflops(f, 10, 8, 0.055)
     assert eight == pytest.approx(8 * one)
     assert bench.flops_fwd(4, 8192, 16, 128, True) == pytest.approx(1.0995e12, rel=1e-4)
+
+
+@pytest.mark.timeout(300)
+def test_bench_gpus_flag_launches_ranks():
+    """`bench.py --gpus 2` without torch.distributed.run starts the two rank processes itself and
+    reports n_gpus from the initialised process group (gloo, harness-only dry run)."""
+    import json
+    import subprocess
+
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--dry-run",
+                        "--no-cpu-baseline", "--steps", "3", "--warmup", "1"],
+                       capture_output=True, text=True, env=env, timeout=240)
+    assert r.returncode == 0, r.stderr[-2000:]
+    lines = [json.loads(x) for x in r.stdout.splitlines() if x.startswith("{")]
+    assert len(lines) == 1 and lines[0]["n_gpus"] == 2 and lines[0]["steps"] == 3
+
+
+@pytest.mark.timeout(120)
+def test_bench_world_mismatch_is_an_error():
+    """A process group whose size differs from --gpus is refused (no silent 1-GPU timing)."""
+    import subprocess
+
+    env = dict(os.environ, WORLD_SIZE="1", RANK="0", LOCAL_RANK="0")
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--dry-run"],
+                       capture_output=True, text=True, env=env, timeout=100)
+    assert r.returncode != 0 and "--gpus 2" in r.stderr
+
+
+def test_c4_seqlens_recipe():
+    sys.path.insert(0, ROOT)
+    import bench
+
+    lens = bench.c4_seqlens()
+    assert sum(lens) == 65536
+    assert all(512 <= s <= 4096 for s in lens[:-1]) and 1 <= lens[-1] <= 4096
+    assert lens == bench.c4_seqlens()          # seeded, reproducible
+    assert 20 <= len(lens) <= 40

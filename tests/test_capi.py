@@ -26,8 +26,20 @@ def declared_functions():
 def test_header_declares_reference_entry_points():
     names = declared_functions()
     for ref_name in ("flash_attn_fwd", "flash_attn_varlen_fwd", "flash_attn_bwd",
-                     "flash_attn_varlen_bwd", "flash_attn_error"):
+                     "flash_attn_varlen_bwd", "flash_attn_set_error", "flash_attn_error"):
         assert ref_name in names
+
+
+def test_set_error_round_trip():
+    """flash_attn_set_error / flash_attn_error (reference capi/flash_attn.h:313-315): the message is
+    copied into the thread-local slot; NULL or empty gives "unknown error"."""
+    lib = ctypes.CDLL(LIB)
+    lib.flash_attn_set_error.argtypes = [ctypes.c_char_p]
+    lib.flash_attn_error.restype = ctypes.c_char_p
+    lib.flash_attn_set_error(b"caller message")
+    assert lib.flash_attn_error() == b"caller message"
+    lib.flash_attn_set_error(None)
+    assert lib.flash_attn_error() == b"unknown error"
 
 
 def test_library_exports_every_declared_symbol():

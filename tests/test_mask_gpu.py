@@ -27,8 +27,10 @@ def _need_gpu():
     import flash_attn_2_cuda  # noqa: F401
 
 
-def _mask_ref(q, k, v, mask, unscale, scale, causal, upcast=True):
-    """out (b, sq, h, d) of softmax(scale * (QK^T + M * unscale)) V with the kernel's indexing."""
+def _mask_ref(q, k, v, mask, unscale, scale, causal, upcast=True, keep=None, p=0.0):
+    """out (b, sq, h, d) of softmax(scale * (QK^T + M * unscale)) V with the kernel's indexing;
+    with a keep mask (b, h, sq, sk) the probabilities are dropped and scaled by 1 / (1 - p) as in
+    attention_ref (reference tests/test_flash_attn.py:150-156)."""
     dt = q.dtype
     if upcast:
         q, k, v, mask = q.float(), k.float(), v.float(), mask.float()
@@ -45,11 +47,13 @@ def _mask_ref(q, k, v, mask, unscale, scale, causal, upcast=True):
     if causal:
         s = s.masked_fill(torch.triu(torch.ones(sq, k.shape[1], dtype=torch.bool, device=q.device), 1),
                           float("-inf"))
-    p = torch.softmax(s, dim=-1)
-    return torch.einsum("bhqk,bkhd->bqhd", p, v).to(dt)
+    pr = torch.softmax(s, dim=-1)
+    if keep is not None:
+        pr = pr.masked_fill(~keep.to(pr.device), 0.0) / (1.0 - p)
+    return torch.einsum("bhqk,bkhd->bqhd", pr, v).to(dt)
 
 
-def _capi_fwd_bwd(q, k, v, mask, unscale, scale, causal, dout):
+def _capi_fwd_bwd(q, k, v, mask, unscale, scale, causal, dout, p=0.0, seed=0, offset=0):
     import flash_attn_2_cuda as m
 
     b, sq, h, d = q.shape
@@ -65,8 +69,8 @@ def _capi_fwd_bwd(q, k, v, mask, unscale, scale, causal, dout):
     P = m._ptr
     bf16 = q.dtype == torch.bfloat16
     ok = m._lib.flash_attn_fwd(P(q), P(k), P(v), P(rng), P(out), None, P(lse), b, sq, sk, sq_r, sk_r,
-                               h, hk, d, d, 0.0, scale, unscale, causal, False, bf16,
-                               m._stream(q), 0, 0, P(mask), dims_p, None, None, None, None, None, None,
+                               h, hk, d, d, p, scale, unscale, causal, False, bf16,
+                               m._stream(q), seed, offset, P(mask), dims_p, None, None, None, None, None, None,
                                qr, kr, vr, qh, kh, vh, orr, oh, qb, kb, vb, ob)
     assert ok, m._lib.flash_attn_error()
     dq, dk, dv = torch.empty_like(q), torch.empty_like(k), torch.empty_like(v)
@@ -74,8 +78,8 @@ def _capi_fwd_bwd(q, k, v, mask, unscale, scale, causal, dout):
     (dqr, dqh, dqb), (dkr, dkh, dkb), (dvr, dvh, dvb), (dor, doh, dob) = st(dq), st(dk), st(dv), st(dout)
     ok = m._lib.flash_attn_bwd_gqa(P(dout), P(q), P(k), P(v), P(out), P(softmax_d), P(lse), P(rng),
                                    P(dq), P(dk), P(dv), None, b, sq, sk, sq_r, sk_r, h, hk, d, d,
-                                   0.0, scale, unscale, causal, bf16, 1,
-                                   m._stream(q), 0, 0, P(mask), dims_p, None, None, None, None, None,
+                                   p, scale, unscale, causal, bf16, 1,
+                                   m._stream(q), seed, offset, P(mask), dims_p, None, None, None, None, None,
                                    None, qr, kr, vr, qh, kh, vh, orr, oh, qb, kb, vb, ob,
                                    dqr, dkr, dvr, dqh, dkh, dvh, dor, doh, dqb, dkb, dvb, dob)
     assert ok, m._lib.flash_attn_error()
@@ -155,33 +159,64 @@ def test_flashmask_and_bad_mask_dims_rejected():
     assert not ok and b"mask_dims" in m._lib.flash_attn_error()
 
 
-def test_dense_mask_with_dropout_matches_plain_dropout():
+@pytest.mark.parametrize("causal", [False, True])
+@pytest.mark.parametrize("d", [32, 64, 96, 128, 256])
+def test_dense_mask_with_dropout_matches_plain_dropout(d, causal):
     """Dropout in the masked instantiation draws the same Philox stream as the plain launch: a zero
-    mask gives the plain dropout result (same seed / offset) to summation-order tolerance."""
-    import flash_attn_2_cuda as m
+    mask gives the plain dropout result (same seed / offset) to summation-order tolerance, forward
+    and backward.  (Round 1 refused non-causal d > 64 here: an LDS-DMA hazard, DESIGN.md.)"""
+    from flash_attn import flash_attn_func
 
     torch.manual_seed(0)
-    b, s, h, d = 1, 300, 2, 128
-    q, k, v = (torch.randn(b, s, h, d, device=DEV, dtype=torch.bfloat16) for _ in range(3))
+    b, s, h = 1, 300, 2
+    q, k, v, dout = (torch.randn(b, s, h, d, device=DEV, dtype=torch.bfloat16) for _ in range(4))
     mask = torch.zeros(b, 1, s, s, device=DEV, dtype=torch.bfloat16)
-    dims = torch.tensor([b, 1, s, s], dtype=torch.int64)
-    P = m._ptr
-    st = (q.stride(1),) * 3 + (q.stride(2),) * 3 + (q.stride(1), q.stride(2)) + (q.stride(0),) * 4
-    outs = []
-    for mk in ((P(mask), dims.numpy().ctypes.data), (None, None)):
-        out = torch.empty_like(q)
-        lse = torch.empty(b, h, s, device=DEV)
-        ok = m._lib.flash_attn_fwd(P(q), P(k), P(v), None, P(out), None, P(lse), b, s, s, 384, 384, h, h,
-                                   d, d, 0.3, d ** -0.5, 1.0, True, False, True, m._stream(q), 7, 4,
-                                   *mk, *([None] * 6), *st)
-        assert ok, m._lib.flash_attn_error()
-        outs.append((out, lse))
-    torch.cuda.synchronize()
-    torch.testing.assert_close(outs[0][0], outs[1][0], atol=4e-3, rtol=0)
-    torch.testing.assert_close(outs[0][1], outs[1][1], atol=1e-4, rtol=0)
-    # known defect: the non-causal masked dropout kernels at head_dim > 64 are refused (DESIGN.md)
-    out = torch.empty_like(q)
-    ok = m._lib.flash_attn_fwd(P(q), P(k), P(v), None, P(out), None, P(lse), b, s, s, 384, 384, h, h,
-                               d, d, 0.3, d ** -0.5, 1.0, False, False, True, m._stream(q), 7, 4,
-                               P(mask), dims.numpy().ctypes.data, *([None] * 6), *st)
-    assert not ok and b"not supported" in m._lib.flash_attn_error()
+    seed, offset = 7, 4
+    out, dq, dk, dv = _capi_fwd_bwd(q, k, v, mask, 1.0, d ** -0.5, causal, dout, 0.3, seed, offset)
+    qr, kr, vr = (x.clone().requires_grad_() for x in (q, k, v))
+    cuda_gen = torch.cuda.default_generators[torch.cuda.current_device()]
+    state = cuda_gen.get_state()
+    cuda_gen.manual_seed(seed)
+    cuda_gen.set_offset(offset)
+    o2 = flash_attn_func(qr, kr, vr, 0.3, causal=causal)
+    cuda_gen.set_state(state)
+    g2 = torch.autograd.grad(o2, (qr, kr, vr), dout)
+    assert torch.isfinite(out).all()
+    torch.testing.assert_close(out, o2, atol=4e-3, rtol=0)
+    for a, bb in zip((dq, dk, dv), g2):
+        torch.testing.assert_close(a, bb, atol=8e-3, rtol=0)
+
+
+@pytest.mark.parametrize("dtype", [torch.float16, torch.bfloat16])
+@pytest.mark.parametrize("causal", [False, True])
+@pytest.mark.parametrize("d,sq,sk,h,hk", [(64, 200, 333, 4, 2), (96, 257, 190, 2, 2), (128, 513, 300, 4, 4),
+                                          (256, 130, 97, 2, 1)])
+def test_dense_mask_with_dropout_vs_oracle(d, sq, sk, h, hk, causal, dtype):
+    """Dense mask + dropout against the restatement with the oracle's keep mask (the reference's
+    densemask forward / backward with Is_dropout, flash_fwd_kernel.h:585-1052)."""
+    import numpy as np
+
+    from oracle.dropout_ref import dropout_keep_mask
+
+    torch.manual_seed(0)
+    b, p, seed, offset = 2, 0.17, 1234, 64
+    q = torch.randn(b, sq, h, d, device=DEV, dtype=dtype)
+    k = torch.randn(b, sk, hk, d, device=DEV, dtype=dtype)
+    v = torch.randn(b, sk, hk, d, device=DEV, dtype=dtype)
+    dout = torch.randn(b, sq, h, d, device=DEV, dtype=dtype)
+    mask = torch.randn(b, h, sq, sk, device=DEV) * 2.0
+    mask = mask.masked_fill(torch.rand(b, h, sq, sk, device=DEV) < 0.2, -3000.0).to(dtype)
+    scale = d ** -0.5
+    out, dq, dk, dv = _capi_fwd_bwd(q, k, v, mask, 1.0 / scale, scale, causal, dout, p, seed, offset)
+    keep = torch.from_numpy(np.stack([np.stack([dropout_keep_mask(seed, offset, bi, hi, h, sq, sk, p)
+                                                for hi in range(h)]) for bi in range(b)])).to(DEV)
+    qc, kc, vc = (x.clone().requires_grad_() for x in (q, k, v))
+    ref = _mask_ref(qc, kc, vc, mask, 1.0 / scale, scale, causal, keep=keep, p=p)
+    pt = _mask_ref(qc, kc, vc, mask, 1.0 / scale, scale, causal, upcast=False, keep=keep, p=p)
+    ok, err, bound = check_within_bound(out, ref, pt)
+    assert ok, f"out: {err:.3e} > {bound:.3e}"
+    gr = torch.autograd.grad(ref, (qc, kc, vc), dout)
+    gp = torch.autograd.grad(pt, (qc, kc, vc), dout)
+    for name, got, r, pp in zip(("dq", "dk", "dv"), (dq, dk, dv), gr, gp):
+        ok, err, bound = check_within_bound(got, r, pp, floor=1e-3)
+        assert ok, f"{name}: {err:.3e} > {bound:.3e}"

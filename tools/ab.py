@@ -53,13 +53,13 @@ def read_times(lib):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("libs", nargs="+")
-    ap.add_argument("--workload", default="c3", choices=sorted(WORKLOADS))
+    ap.add_argument("--workload", default="c3", choices=[w for w in sorted(WORKLOADS) if WORKLOADS[w][0]])
     ap.add_argument("--rounds", type=int, default=5)
     ap.add_argument("--iters", type=int, default=10)
     ap.add_argument("--bwd", action="store_true")
     args = ap.parse_args()
 
-    b, s, h, hk, d, dt, causal = WORKLOADS[args.workload]
+    b, s, h, hk, d, dt, causal, _kind = WORKLOADS[args.workload]
     dtype = torch.bfloat16 if dt == "bf16" else torch.float16
     g = torch.Generator(device="cuda").manual_seed(1234)
     q = torch.randn(b, s, h, d, device="cuda", dtype=dtype, generator=g)

@@ -186,6 +186,7 @@ __global__ void __launch_bounds__(DkdvTile<D>::NW * 64, 1) bwd_dkdv_kernel(const
   __shared__ __attribute__((aligned(16))) char smem[XBASE + 2 * XBUF + (DROPOUT ? NKG * 1024 : 0)];
 
   const AttnShape s = p.s;
+  const uint64_t pseed = DROPOUT ? philox_seed_of(s) : 0, poff = DROPOUT ? philox_offset_of(s) : 0;
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = wave_uniform(tid >> 6);
   const bool pwave = wave < NKG;
@@ -341,8 +342,8 @@ __global__ void __launch_bounds__(DkdvTile<D>::NW * 64, 1) bwd_dkdv_kernel(const
     for (int qi = 0; qi < NQT; ++qi) {
       unsigned rb[4];
       if constexpr (DROPOUT) {
-        const uint64_t doff = s.philox_offset + (uint64_t)(bidb * s.h + h_begin + it_head) * 32;
-        dropout_block_bytes<true>(dscr, s.philox_seed, doff, q0 + 32 * qi, kw0, lane);
+        const uint64_t doff = poff + (uint64_t)(bidb * s.h + h_begin + it_head) * 32;
+        dropout_block_bytes<true>(dscr, pseed, doff, q0 + 32 * qi, kw0, lane);
 #pragma unroll
         for (int u = 0; u < 4; ++u) rb[u] = dropout_group_bytes(dscr, r, hh, u);
       }
@@ -525,6 +526,7 @@ __global__ void __launch_bounds__(DqTile<D>::NW * 64, DqTile<D>::MINB) bwd_dq_ke
   __shared__ __attribute__((aligned(16))) char smem[kBwdBufs * 2 * TILE + (DROPOUT ? NW * 1024 : 0)];
 
   const AttnShape s = p.s;
+  const uint64_t pseed = DROPOUT ? philox_seed_of(s) : 0, poff = DROPOUT ? philox_offset_of(s) : 0;
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = wave_uniform(tid >> 6);
   const int r = lane & 31, hh = lane >> 5;
@@ -634,8 +636,8 @@ __global__ void __launch_bounds__(DqTile<D>::NW * 64, DqTile<D>::MINB) bwd_dq_ke
       unsigned rb[4];
       if constexpr (DROPOUT) {
         char* dscr = smem + kBwdBufs * 2 * TILE + wave * 1024;
-        const uint64_t doff = s.philox_offset + (uint64_t)bhi * 32;
-        dropout_block_bytes<false>(dscr, s.philox_seed, doff, wq0, n0 + 32 * t, lane);
+        const uint64_t doff = poff + (uint64_t)bhi * 32;
+        dropout_block_bytes<false>(dscr, pseed, doff, wq0, n0 + 32 * t, lane);
 #pragma unroll
         for (int u = 0; u < 4; ++u) rb[u] = dropout_group_bytes(dscr, r, hh, u);
       }

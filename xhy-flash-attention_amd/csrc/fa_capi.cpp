@@ -72,7 +72,7 @@ struct FlashMaskArgs {
 
 void check_common(int batch_size, int num_heads, int num_heads_k, int head_size,
                   int head_size_rounded, float p_dropout, const void* attn_mask,
-                  const FlashMaskArgs* flashmask, bool causal = true) {
+                  const FlashMaskArgs* flashmask) {
   check_device();
   FA_CHECK(batch_size > 0);
   FA_CHECK(num_heads > 0 && num_heads_k > 0);
@@ -82,12 +82,6 @@ void check_common(int batch_size, int num_heads, int num_heads_k, int head_size,
   FA_CHECK(head_size_rounded >= head_size);
   if (attn_mask != nullptr && flashmask != nullptr && flashmask->downstart != nullptr)
     throw std::runtime_error("attn_mask and FlashMask cannot be combined");
-  const bool any_mask = attn_mask != nullptr || (flashmask != nullptr && flashmask->downstart != nullptr);
-  // Known defect of this build (DESIGN.md "Known issues"): the masked non-causal dropout kernels for
-  // head_dim > 64 return wrong values, so that combination is refused rather than computed.
-  if (any_mask && p_dropout > 0.f && !causal && head_size > 64)
-    throw std::runtime_error("attn_mask / FlashMask with dropout, non-causal and head_dim > 64 is not "
-                             "supported by the MI355X build");
   FA_CHECK(p_dropout >= 0.f && p_dropout < 1.f);
 }
 
@@ -156,7 +150,7 @@ bool fwd_impl(const void* q, const void* k, const void* v, const int32_t* cu_q, 
               int v_batch, int o_batch, bool padded, const int64_t* mask_dims = nullptr,
               float unscale = 1.f) {
   FA_BEGIN
-  check_common(b, h, hk, d, d_r, p_dropout, attn_mask, flashmask, causal);
+  check_common(b, h, hk, d, d_r, p_dropout, attn_mask, flashmask);
   // reference mha_fwd: "return_softmax is only supported when p_dropout > 0.0" (flash_api.cpp:276-279)
   if (return_softmax && !(p_dropout > 0.f))
     throw std::runtime_error("return_softmax is only supported when p_dropout > 0.0");
@@ -201,7 +195,7 @@ bool bwd_impl(const void* dout, const void* q, const void* k, const void* v, con
               bool gqa_reduce, void* rng_state, uint64_t seed, uint64_t offset,
               const int64_t* mask_dims = nullptr, float unscale = 1.f) {
   FA_BEGIN
-  check_common(b, h, hk, d, d_r, p_dropout, attn_mask, flashmask, causal);
+  check_common(b, h, hk, d, d_r, p_dropout, attn_mask, flashmask);
   FA_CHECK(dout && q && k && v && out && softmax_d && lse && dq && dk && dv);
   FA_CHECK(d_r % 32 == 0);
   FA_CHECK(sq_r >= sq);
@@ -211,10 +205,18 @@ bool bwd_impl(const void* dout, const void* q, const void* k, const void* v, con
   set_mask(p.s, attn_mask, mask_dims, unscale);
   set_flashmask(p.s, flashmask);
   p.s.lse_pitch = sq;
-  if (p.s.dropout && rng_state != nullptr) {   // reference capi flash_attn.cu:943-947
-    const uint64_t st[2] = {seed, offset};
-    if (hipMemcpyAsync(rng_state, st, sizeof(st), hipMemcpyHostToDevice, stream) != hipSuccess)
-      throw std::runtime_error("flash_attn_bwd: rng_state copy failed");
+  if (p.s.dropout && rng_state != nullptr) {
+    if (gqa_reduce) {
+      // MI355X entry points (*_bwd_gqa): rng_state is the forward's record and the kernels read
+      // (seed, offset) from it on the device, as the reference's torch op does with rng_state
+      // (flash_api.cpp:669-670, flash_bwd_kernel.h:783-784); seed / offset are ignored.
+      p.s.philox_dev = static_cast<const uint64_t*>(rng_state);
+    } else {
+      // reference capi flash_attn.cu:943-947: {seed, offset} is written into rng_state
+      const uint64_t st[2] = {seed, offset};
+      if (hipMemcpyAsync(rng_state, st, sizeof(st), hipMemcpyHostToDevice, stream) != hipSuccess)
+        throw std::runtime_error("flash_attn_bwd: rng_state copy failed");
+    }
   }  // softmax_lse is (b, h, seqlen_q) as written by the forward
   p.q = q; p.k = k; p.v = v; p.o = out; p.dout = dout;
   p.dq = dq; p.dk = dk; p.dv = dv;
@@ -244,6 +246,8 @@ bool bwd_impl(const void* dout, const void* q, const void* k, const void* v, con
 
 extern "C" {
 
+// reference csrc/capi/flash_attn.h:313-315 (flash_attn.cu:47-60)
+void flash_attn_set_error(const char* msg) { set_error(msg); }
 const char* flash_attn_error() { return g_err.get(); }
 
 void flash_attn_block_size(int head_size, int is_backward, int* block_m, int* block_n) {

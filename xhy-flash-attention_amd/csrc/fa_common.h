@@ -222,15 +222,24 @@ __device__ inline buf_rsrc_t make_rsrc(const void* base, int bytes) {
 // `s_waitcnt vmcnt(0)` before them -- which waits for the tile just issued two steps ahead and
 // exposes its whole latency every iteration.  The kernels order DMA and LDS reads themselves
 // (counted vmcnt + barrier per ring step), so the compiler must not see these stores.
+//
+// The asm opens with `s_nop 4` (five wait states) because the compiler's hazard recognizer does not
+// look inside inline asm.  Two hazards apply to this instruction: M0 written by SALU -> LDS-DMA (one
+// wait state) and "VALU writes an SGPR -> VMEM reads that SGPR" (five wait states).  The second one
+// bites when SGPR pressure makes the compiler reload the descriptor from an SGPR spill lane
+// (v_readlane_b32) right before the asm: with `s_nop 0` the DMA then read a stale descriptor word
+// and filled the K tile with wrong bytes (the masked non-causal dropout forward at d = 128 returned
+// a wrong LSE and NaN outputs; the d = 32 / 96 spill-heavy instantiations had the same pattern).
+// tests/test_isa_hazards.py checks the built code object for this hazard.
 __device__ inline unsigned lds_addr(const char* p) {
   return wave_uniform((int)(unsigned)(size_t)(__attribute__((address_space(3))) const char*)p);
 }
 __device__ inline void dma16(buf_rsrc_t rsrc, char* lds_dst, int voffset) {
-  asm volatile("s_nop 0\n\tbuffer_load_dwordx4 %1, %2, 0 offen lds"
+  asm volatile("s_nop 4\n\tbuffer_load_dwordx4 %1, %2, 0 offen lds"
                :: "{m0}"(lds_addr(lds_dst)), "v"(voffset), "s"(rsrc) : "memory");
 }
 __device__ inline void dma4(buf_rsrc_t rsrc, char* lds_dst, int voffset) {
-  asm volatile("s_nop 0\n\tbuffer_load_dword %1, %2, 0 offen lds"
+  asm volatile("s_nop 4\n\tbuffer_load_dword %1, %2, 0 offen lds"
                :: "{m0}"(lds_addr(lds_dst)), "v"(voffset), "s"(rsrc) : "memory");
 }
 __device__ inline void wait_dma_and_barrier() {

@@ -45,6 +45,17 @@ __device__ inline u32x4_t philox(uint64_t seed, uint64_t subsequence, uint64_t o
   return r;
 }
 
+// (seed, offset) of the stream: the device rng_state when the launcher passes one (AttnShape::
+// philox_dev, backward), else the host values.  Read once per workgroup (scalar loads).
+template <typename Shape>
+__device__ inline uint64_t philox_seed_of(const Shape& s) {
+  return s.philox_dev != nullptr ? s.philox_dev[0] : s.philox_seed;
+}
+template <typename Shape>
+__device__ inline uint64_t philox_offset_of(const Shape& s) {
+  return s.philox_dev != nullptr ? s.philox_dev[1] : s.philox_offset;
+}
+
 // This wave's 32 x 32 block of dropout bytes -- rows row0 .. row0+31 (queries), columns col0 ..
 // col0+31 (keys), both multiples of 32 and relative to the sequence -- into the wave's 1-KiB LDS
 // scratch `buf`, laid out [row][col] (TRANS = false) or [col][row] (TRANS = true).

@@ -33,6 +33,10 @@ struct AttnShape {
   float p_keep;             // keep probability 1 - p_dropout
   float rp_dropout;         // 1 / p_keep
   uint64_t philox_seed, philox_offset;   // the reference's (seed, offset) pair (rng_state)
+  // backward only: when set, the kernels read (seed, offset) from this device buffer (the rng_state
+  // the forward recorded), as the reference's kernels read params.rng_state[0..1]
+  // (flash_bwd_kernel.h:783-784) -- no host round trip
+  const uint64_t* philox_dev;
   // Paddle dense additive mask (reference Flash_fwd_params attn_mask_ptr / mask_head_mod_size /
   // mask_seq_q_mod_size / unscale_softmax, flash.h; applied in softmax.h:361-379): raw scores
   // QK^T += mask[b][h % mask_h][q % mask_sq][k] * mask_unscale, in the input dtype, row stride

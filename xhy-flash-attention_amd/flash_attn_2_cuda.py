@@ -139,13 +139,15 @@ def _seed_offset(p_dropout, gen, device, counter_offset):
     return int(seed) & (2 ** 64 - 1), int(offset)
 
 
-def _rng_seed_offset(p_dropout, rng_state):
-    """(seed, offset) the forward recorded in rng_state (int64[2]); read back to the host, which
-    synchronises -- only on the dropout path."""
-    if not p_dropout > 0.0 or rng_state is None:
-        return 0, 0
-    seed, offset = (int(x) & (2 ** 64 - 1) for x in rng_state.cpu().tolist())
-    return seed, offset
+def _bwd_rng(p_dropout, rng_state, gen, device, counter_offset):
+    """(rng_state pointer, seed, offset) for the backward.  With the forward's rng_state the kernels
+    read (seed, offset) from it on the device (the *_bwd_gqa entries; reference mha_bwd
+    flash_api.cpp:669-670 and flash_bwd_kernel.h:783-784): no host round trip, capturable.  Without
+    one, dropout draws from the generator as the reference does (flash_api.cpp:671-677)."""
+    if not p_dropout > 0.0 or rng_state is not None:
+        return _ptr(rng_state), 0, 0
+    seed, offset = _seed_offset(p_dropout, gen, device, counter_offset)
+    return None, seed, offset
 
 
 # --------------------------------------------------------------------------------------------------
@@ -349,16 +351,19 @@ def bwd(dout, q, k, v, out, softmax_lse, dq_, dk_, dv_, p_dropout, softmax_scale
         # scratch for the kernels' -LSE/scale rows (the reference allocates (b, h, sq_r, d_r) here for
         # its fp32 atomic dQ accumulator; the MI355X backward needs only (b, h, sq_r))
         dq_accum = torch.empty((batch_size, num_heads, seqlen_q_rounded), dtype=torch.float32, device=q.device)
-        fn = _lib.flash_attn_bwd if num_heads == num_heads_k else _lib.flash_attn_bwd_gqa
+        # the *_gqa entry: dk/dv with num_heads_k heads (== the reference's result after its
+        # sum_out), rng_state read on the device
+        rng_p, seed, offset = _bwd_rng(p_dropout, rng_state, gen_, q.device, batch_size * num_heads * 32)
         st = [_strides(x, 4) for x in (qk, kk, vk, ok_, dq, dk, dv, dok)]
         (qb, qr, qh), (kb, kr, kh), (vb, vr, vh), (ob, orr, oh) = st[:4]
         (dqb, dqr, dqh), (dkb, dkr, dkh), (dvb, dvr, dvh), (dob, dor, doh) = st[4:]
-        ok = fn(_ptr(dok), _ptr(qk), _ptr(kk), _ptr(vk), _ptr(ok_), _ptr(softmax_d),
-                _ptr(softmax_lse), _ptr(rng_state), _ptr(dq), _ptr(dk), _ptr(dv), _ptr(dq_accum),
+        ok = _lib.flash_attn_bwd_gqa(
+                _ptr(dok), _ptr(qk), _ptr(kk), _ptr(vk), _ptr(ok_), _ptr(softmax_d),
+                _ptr(softmax_lse), rng_p, _ptr(dq), _ptr(dk), _ptr(dv), _ptr(dq_accum),
                 batch_size, seqlen_q, seqlen_k, seqlen_q_rounded, seqlen_k_rounded,
                 num_heads, num_heads_k, head_size, head_size_rounded,
                 float(p_dropout), float(softmax_scale), 1.0, bool(is_causal),
-                q.dtype == torch.bfloat16, 0, _stream(q), *_rng_seed_offset(p_dropout, rng_state),
+                q.dtype == torch.bfloat16, 0, _stream(q), seed, offset,
                 None, None, None, None, None, None, None, None,
                 qr, kr, vr, qh, kh, vh, orr, oh, qb, kb, vb, ob,
                 dqr, dkr, dvr, dqh, dkh, dvh, dor, doh, dqb, dkb, dvb, dob)
@@ -409,17 +414,18 @@ def varlen_bwd(dout, q, k, v, out, softmax_lse, dq_, dk_, dv_, cu_seqlens_q, cu_
         dq_accum = torch.empty((batch_size, num_heads, seqlen_q_rounded), dtype=torch.float32, device=q.device)
         if zero_tensors:
             dq.zero_(); dk.zero_(); dv.zero_(); softmax_d.zero_()
-        fn = _lib.flash_attn_varlen_bwd if num_heads == num_heads_k else _lib.flash_attn_varlen_bwd_gqa
+        rng_p, seed, offset = _bwd_rng(p_dropout, rng_state, gen_, q.device, batch_size * num_heads * 32)
         st = [_strides(x, 3) for x in (qk, kk, vk, ok_, dq, dk, dv, dok)]
         (_, qr, qh), (_, kr, kh), (_, vr, vh), (_, orr, oh) = st[:4]
         (_, dqr, dqh), (_, dkr, dkh), (_, dvr, dvh), (_, dor, doh) = st[4:]
-        ok = fn(_ptr(dok), _ptr(qk), _ptr(kk), _ptr(vk), _ptr(ok_), _ptr(softmax_d),
-                _ptr(softmax_lse), _ptr(cu_seqlens_q), _ptr(cu_seqlens_k), _ptr(rng_state),
+        ok = _lib.flash_attn_varlen_bwd_gqa(
+                _ptr(dok), _ptr(qk), _ptr(kk), _ptr(vk), _ptr(ok_), _ptr(softmax_d),
+                _ptr(softmax_lse), _ptr(cu_seqlens_q), _ptr(cu_seqlens_k), rng_p,
                 _ptr(dq), _ptr(dk), _ptr(dv), _ptr(dq_accum), batch_size, int(max_seqlen_q),
                 int(max_seqlen_k), seqlen_q_rounded, seqlen_k_rounded, num_heads, num_heads_k,
                 head_size, head_size_rounded, float(p_dropout), float(softmax_scale), 1.0,
                 bool(is_causal), q.dtype == torch.bfloat16, 0, _stream(q),
-                *_rng_seed_offset(p_dropout, rng_state), None, None,
+                seed, offset, None, None,
                 qr, kr, vr, qh, kh, vh, orr, oh, 0, 0, 0, 0,
                 dqr, dkr, dvr, dqh, dkh, dvh, dor, doh, 0, 0, 0, 0, False)
         if not ok:
