@@ -1,0 +1,108 @@
+"""GPU parity at the BASELINE.json configs' full sizes (C4, C5), through the public API.
+
+The reference's acceptance rule (tests/test_flash_attn.py:420-427, 630-639): max|x - ref| <= 2 x
+max|x_pt - ref|, ref = attention_ref in fp32, pt = attention_ref in the input dtype with
+reorder_ops.  Attention is independent per (sequence, head) -- per (batch, kv-head group) for
+GQA -- so the oracle is evaluated slice by slice on the same device, which is exactly the full-call
+reference restricted to that slice:
+  * C4 (configs[3]): flash_attn_varlen_qkvpacked_func, bf16, total 65536 tokens, cu_seqlens from
+    the SURVEY 8(d) recipe (bench.c4_seqlens), h = 32, d = 128, causal; EVERY sequence and head:
+    out, dqkv, and the per-batch-padded LSE (B, 32, max_seqlen) against the fp64 logsumexp.
+  * C5 (configs[4]): flash_attn_func, fp16, b = 8 per GPU, s = 32768, h = 32, hk = 8, causal; two
+    (batch, kv-head) groups: out / dq per query head, dk / dv summed over the group, LSE; every
+    output finite everywhere.
+"""
+import os
+import sys
+
+import pytest
+import torch
+
+from oracle.attention_ref import attention_lse_ref, attention_ref, check_within_bound
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda"
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+@pytest.fixture(scope="module", autouse=True)
+def _need_gpu():
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    import flash_attn_2_cuda  # noqa: F401
+
+
+def _ref_grads(q, k, v, dout, causal, upcast, reorder):
+    qr, kr, vr = (x.detach().clone().requires_grad_() for x in (q, k, v))
+    out, _ = attention_ref(qr, kr, vr, causal=causal, upcast=upcast, reorder_ops=reorder)
+    grads = torch.autograd.grad(out, (qr, kr, vr), dout)
+    return out.detach(), grads
+
+
+def _check(name, got, ref, pt, floor=0.0):
+    ok, err, bound = check_within_bound(got.float(), ref.float(), pt.float(), floor=floor)
+    assert ok, f"{name}: max|err| {err:.3e} > bound {bound:.3e}"
+
+
+def test_c4_varlen_qkvpacked_full_size():
+    sys.path.insert(0, ROOT)
+    import bench
+    from flash_attn import flash_attn_varlen_qkvpacked_func
+
+    torch.manual_seed(0)
+    lens = bench.c4_seqlens()
+    total, h, d = sum(lens), 32, 128
+    assert total == 65536
+    cu = torch.tensor([0] + lens, dtype=torch.int64).cumsum(0).to(torch.int32).to(DEV)
+    max_s = max(lens)
+    qkv = torch.randn(total, 3, h, d, device=DEV, dtype=torch.bfloat16, requires_grad=True)
+    out, lse, _ = flash_attn_varlen_qkvpacked_func(qkv, cu, max_s, causal=True, return_attn_probs=True)
+    assert out.shape == (total, h, d) and lse.shape == (len(lens), h, max_s)
+    dout = torch.randn_like(out)
+    (dqkv,) = torch.autograd.grad(out, (qkv,), dout)
+    assert torch.isfinite(out).all() and torch.isfinite(dqkv).all()
+    for i, s in enumerate(lens):
+        a, e = int(cu[i]), int(cu[i + 1])
+        q, k, v = (qkv.detach()[a:e, j].unsqueeze(0) for j in range(3))
+        g = dout[a:e].unsqueeze(0)
+        ref, gr = _ref_grads(q, k, v, g, True, True, False)
+        pt, gp = _ref_grads(q, k, v, g, True, False, True)
+        _check(f"seq {i} (s={s}) out", out[a:e].unsqueeze(0), ref, pt)
+        for j, name in enumerate(("dq", "dk", "dv")):
+            _check(f"seq {i} (s={s}) {name}", dqkv[a:e, j].unsqueeze(0), gr[j], gp[j])
+        lse_ref = attention_lse_ref(q, k, causal=True)[0]
+        torch.testing.assert_close(lse[i, :, :s], lse_ref, atol=2e-3, rtol=1e-4)
+
+
+def test_c5_gqa_long_context_full_size():
+    from flash_attn import flash_attn_func
+
+    torch.manual_seed(0)
+    b, s, h, hk, d = 8, 32768, 32, 8, 128
+    dt = torch.float16
+    q = torch.randn(b, s, h, d, device=DEV, dtype=dt, requires_grad=True)
+    k = torch.randn(b, s, hk, d, device=DEV, dtype=dt, requires_grad=True)
+    v = torch.randn(b, s, hk, d, device=DEV, dtype=dt, requires_grad=True)
+    out, lse, _ = flash_attn_func(q, k, v, causal=True, return_attn_probs=True)
+    dout = torch.randn_like(out)
+    dq, dk, dv = torch.autograd.grad(out, (q, k, v), dout)
+    for t in (out, lse, dq, dk, dv):
+        assert torch.isfinite(t).all()
+    grp = h // hk
+    for bi, kvh in ((0, 0), (b - 1, hk - 1)):
+        kk, vv = (x.detach()[bi:bi + 1, :, kvh:kvh + 1] for x in (k, v))
+        dk_ref = dk_pt = dv_ref = dv_pt = 0
+        for hi in range(kvh * grp, (kvh + 1) * grp):
+            qq = q.detach()[bi:bi + 1, :, hi:hi + 1]
+            g = dout[bi:bi + 1, :, hi:hi + 1]
+            ref, gr = _ref_grads(qq, kk, vv, g, True, True, False)
+            pt, gp = _ref_grads(qq, kk, vv, g, True, False, True)
+            _check(f"(b {bi}, h {hi}) out", out[bi:bi + 1, :, hi:hi + 1], ref, pt)
+            _check(f"(b {bi}, h {hi}) dq", dq[bi:bi + 1, :, hi:hi + 1], gr[0], gp[0])
+            dk_ref, dv_ref = dk_ref + gr[1].float(), dv_ref + gr[2].float()
+            dk_pt, dv_pt = dk_pt + gp[1].float(), dv_pt + gp[2].float()
+            lse_ref = attention_lse_ref(qq, kk, causal=True)[0, 0]
+            torch.testing.assert_close(lse[bi, hi], lse_ref, atol=2e-3, rtol=1e-4)
+            del ref, gr, pt, gp
+        _check(f"(b {bi}, kv {kvh}) dk", dk[bi:bi + 1, :, kvh:kvh + 1], dk_ref, dk_pt)
+        _check(f"(b {bi}, kv {kvh}) dv", dv[bi:bi + 1, :, kvh:kvh + 1], dv_ref, dv_pt)

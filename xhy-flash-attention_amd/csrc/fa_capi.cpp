@@ -160,8 +160,6 @@ bool fwd_impl(const void* q, const void* k, const void* v, const int32_t* cu_q, 
   p.s = make_shape(b, h, hk, sq, sk, d, scale, causal, cu_q, cu_k, padded, p_dropout, seed, offset);
   set_mask(p.s, attn_mask, mask_dims, unscale);
   set_flashmask(p.s, flashmask);
-  if (return_softmax && (attn_mask != nullptr || p.s.fm_lts != nullptr))
-    throw std::runtime_error("return_softmax with attn_mask / FlashMask is not supported by the MI355X build");
   if (return_softmax) {
     FA_CHECK(softmax_ptr != nullptr && sq_r >= sq && sk_r >= sk);
     p.p_out = softmax_ptr;

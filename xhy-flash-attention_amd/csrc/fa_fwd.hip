@@ -515,8 +515,10 @@ __global__ void __launch_bounds__(FwdTile<D>::NW * 64, FwdTile<D>::MINB) fwd_ker
 }
 
 // return_softmax (test-only, reference flash_api.cpp:276-279): S_dmask[b][h][i][j] =
-// exp(scale * q_i . k_j - LSE_i), negated where dropout drops the element, 0 where masked or padded.
-// A plain fp32 dot product per element: it runs only for the reference's dropout tests.
+// exp(scale * (q_i . k_j + mask_ij * unscale) - LSE_i), negated where dropout drops the element, 0
+// where causal / FlashMask hides it or it is padding (the reference writes P in its dense-mask and
+// FlashMask kernels too, flash_fwd_kernel.h:880-887, 1513-1520).  A plain fp32 dot product per
+// element: it runs only for the reference's dropout tests.
 template <bool BF16>
 __global__ void __launch_bounds__(256) dmask_kernel(const FwdParams p) {
   using E = Elt<BF16>;
@@ -541,11 +543,18 @@ __global__ void __launch_bounds__(256) dmask_kernel(const FwdParams p) {
     if (!s.varlen_padded_input) k_off = (int64_t)c0 * p.k_row;
   }
   float val = 0.f;
-  if (row < sq && col < sk && !(s.causal && col > row)) {
+  bool live = row < sq && col < sk && !(s.causal && col > row);
+  if (live && s.fm_lts != nullptr) {
+    const int64_t c = fm_base(s, bidb, head) + col;
+    live = !(s.causal ? fm_masked<true>(s, c, row) : fm_masked<false>(s, c, row));
+  }
+  if (live) {
     const u16* qr = (const u16*)p.q + q_off + (int64_t)head * p.q_head + (int64_t)row * p.q_row;
     const u16* kr = (const u16*)p.k + k_off + (int64_t)kvh * p.k_head + (int64_t)col * p.k_row;
     float acc = 0.f;
     for (int d = 0; d < s.d; ++d) acc += E::to_f32(qr[d]) * E::to_f32(kr[d]);
+    const u16* mrow = mask_row_ptr(s, bidb, head, row);
+    if (mrow != nullptr) acc += E::to_f32(mrow[col]) * s.mask_unscale;
     const float lse = p.lse[((int64_t)bidb * s.h + head) * s.lse_pitch + row];
     val = __expf(acc * s.scale - lse);
     // the reference's byte for (row, col), computed directly (one Philox call per element)
