@@ -331,7 +331,9 @@ __global__ void __launch_bounds__(DkdvTile<D>::NW * 64, 1) bwd_dkdv_kernel(const
   // apply_dropout<encode_dropout_in_sign_bit=true>, flash_bwd_kernel.h:848-857) and the packed
   // operand of dV^T carries P o Z (zeros where dropped).
   char* const dscr = smem + XBASE + 2 * XBUF + kg * 1024;
-  auto p_step = [&](auto MASKC, f32x16_t (&sp)[NQT], int q0, int it_head, char* xw, i16x8_t (&fr)[2 * NQT]) {
+  // (sp is read only: a write-back would make the scores' register set differ between the roles at
+  // the join after the P step, which costs 32 copies per step)
+  auto p_step = [&](auto MASKC, const f32x16_t (&sp)[NQT], int q0, int it_head, char* xw, i16x8_t (&fr)[2 * NQT]) {
     constexpr bool MASK = decltype(MASKC)::value;
     // FlashMask bounds of this lane's key for this slice's head, loaded once per slice
     FmCol fc = {0u, 0xffffffffu, 0u, 0u};
@@ -340,6 +342,7 @@ __global__ void __launch_bounds__(DkdvTile<D>::NW * 64, 1) bwd_dkdv_kernel(const
       if (fm_on) fc = fm_load(s, fm_base(s, bidb, h_begin + it_head) + (key < sk ? key : 0));
 #pragma unroll
     for (int qi = 0; qi < NQT; ++qi) {
+      f32x16_t pk;   // P (dropout: P o Z), the B operand of dV^T
       unsigned rb[4];
       if constexpr (DROPOUT) {
         const uint64_t doff = poff + (uint64_t)(bidb * s.h + h_begin + it_head) * 32;
@@ -355,30 +358,35 @@ __global__ void __launch_bounds__(DkdvTile<D>::NW * 64, 1) bwd_dkdv_kernel(const
           float x;
           if constexpr (MASK) {
             const int q = q0 + 32 * qi + 8 * u + 4 * hh + j;
-            bool out = key >= sk || q >= sq || (CAUSAL && key > q);
-            float add = 0.f;
+            // non-short-circuit ORs and exp2(-inf) = 0: selects, no per-lane branches
+            bool out = (key >= sk) | (q >= sq) | (CAUSAL && key > q);
+            float sc = sp[qi][4 * u + j];
             if constexpr (MASKED) {
               out = out || (fm_on && fm_hidden<CAUSAL>(fc, s.fm_uts != nullptr, q));
               const u16* mrow = out ? nullptr : mask_row_ptr(s, bidb, h_begin + it_head, q);
-              if (mrow != nullptr) add = E::to_f32(mrow[key]) * s.mask_unscale;
+              if (mrow != nullptr) sc += E::to_f32(mrow[key]) * s.mask_unscale;
             }
-            x = out ? 0.f : fast_exp2((sp[qi][4 * u + j] + add) * c);
+            x = fast_exp2(out ? kNegInf : sc * c);
           } else {
+#ifdef FA_ABL_NOEXP
+            x = sp[qi][4 * u + j] * c;   // ablation (wrong results): no exp
+#else
             x = fast_exp2(sp[qi][4 * u + j] * c);
+#endif
           }
           if constexpr (DROPOUT) {
             const bool keep = dropout_keep(rb[u], j, s.keep_u8);
             pv[j] = keep ? x : -x;
-            sp[qi][4 * u + j] = keep ? x : 0.f;
+            pk[4 * u + j] = keep ? x : 0.f;
           } else {
             pv[j] = x;
-            sp[qi][4 * u + j] = x;
+            pk[4 * u + j] = x;
           }
         }
         *(f32x4_t*)(xw + qi * XTILE + u * 1024) = pv;
       }
-      fr[2 * qi] = pack_frag<BF16>(sp[qi], 0);
-      fr[2 * qi + 1] = pack_frag<BF16>(sp[qi], 1);
+      fr[2 * qi] = pack_frag<BF16>(pk, 0);
+      fr[2 * qi + 1] = pack_frag<BF16>(pk, 1);
     }
   };
   // dS'' = P o dP'' of the slice whose P tiles are at `xw`, packed to `fr`
@@ -390,7 +398,12 @@ __global__ void __launch_bounds__(DkdvTile<D>::NW * 64, 1) bwd_dkdv_kernel(const
       f32x16_t x;
 #pragma unroll
       for (int u = 0; u < 4; ++u) {
+#ifdef FA_ABL_NOPREAD
+        const f32x4_t pv = {0.5f, 0.5f, 0.5f, 0.5f};   // ablation (wrong results): no P exchange read
+        (void)xw;
+#else
         const f32x4_t pv = *(const f32x4_t*)(xw + qi * XTILE + u * 1024);
+#endif
         if constexpr (DROPOUT) {
           const f32x4_t dv = *(const f32x4_t*)(dl + 32 * qi + 8 * u + 4 * hh);
 #pragma unroll
@@ -447,7 +460,9 @@ __global__ void __launch_bounds__(DkdvTile<D>::NW * 64, 1) bwd_dkdv_kernel(const
   for (; MASKED ? sid < total : it < total; ++it) {
     const int cur = MASKED ? sid : it;
     const int nxt = MASKED ? next_live(sid) : it + 1;
+#ifndef FA_ABL_NODMA
     if (nxt < total) issue(nxt, it + 1);
+#endif
     const int q0 = slice_q0(cur);
     const int it_head = slice_head(cur);   // query head of this slice within the group
     const int qs = (it % 3) * QSLOT;
@@ -466,14 +481,26 @@ __global__ void __launch_bounds__(DkdvTile<D>::NW * 64, 1) bwd_dkdv_kernel(const
 #pragma unroll
         for (int j = 0; j < 4; ++j) sp[qi][4 * u + j] = iv[j];
       }
+#ifndef FA_ABL_NOPH1
     phase1(pwave ? qs : os, sp);                       // S' = Q K^T - LSE/scale  /  dP'' = D - dO V^T
+#endif
     if (pwave) {
       const bool fast = !MASKED && (q0 + BQ <= sq) && (n0 + BKN <= sk) && (!CAUSAL || q0 >= n0 + BKN - 1);
       if (fast) p_step(std::false_type{}, sp, q0, it_head, xw_of(it), fr);
       else p_step(std::true_type{}, sp, q0, it_head, xw_of(it), fr);
     }
+#ifndef FA_ABL_NOPH2
     if (pwave || it > 0) phase2(pwave ? os : ((it + 2) % 3) * QSLOT, fr);   // dV^T / dK''^T
+#else
+    if (pwave || it > 0) acc[0] = E::mfma(fr[0], fr[1], acc[0]);   // keep fr live
+#endif
+#if defined(FA_ABL_NODMAWAIT)
+    lds_barrier();   // ablation (wrong results): DMA never waited for
+#elif defined(FA_ABL_NOBARRIER)
+    wait_vmcnt(0);   // ablation (wrong results): no workgroup barrier
+#else
     wait_dma_keep_and_barrier(0);
+#endif
     if constexpr (MASKED) sid = nxt;
   }
   const int nlive = MASKED ? it : total;
@@ -646,13 +673,14 @@ __global__ void __launch_bounds__(DqTile<D>::NW * 64, DqTile<D>::MINB) bwd_dq_ke
         float pv;
         if constexpr (MASK) {
           const int kk = n0 + t * 32 + acc_row(g, hh);
-          bool out = kk >= sk || (CAUSAL && kk > qi);
-          float add = 0.f;
+          // non-short-circuit OR and exp2(-inf) = 0: selects, no per-lane branches
+          bool out = (kk >= sk) | (CAUSAL && kk > qi);
+          float sc = st[t][g];
           if constexpr (MASKED) {
             out = out || (s.fm_lts != nullptr && fm_masked<CAUSAL>(s, fmb + kk, qi));
-            if (!out && mrow != nullptr) add = E::to_f32(mrow[kk]) * s.mask_unscale;
+            if (!out && mrow != nullptr) sc += E::to_f32(mrow[kk]) * s.mask_unscale;
           }
-          pv = out ? 0.f : fast_exp2(fmaf(st[t][g] + add, c, -lse_l2));
+          pv = fast_exp2(out ? kNegInf : fmaf(sc, c, -lse_l2));
         } else {
           pv = fast_exp2(fmaf(st[t][g], c, -lse_l2));
         }

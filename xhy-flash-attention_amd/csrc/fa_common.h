@@ -32,6 +32,7 @@ typedef __attribute__((ext_vector_type(8))) _Float16 f16x8_t;
 typedef __attribute__((ext_vector_type(2))) _Float16 f16x2_t;
 typedef __attribute__((ext_vector_type(16))) float f32x16_t;
 typedef __attribute__((ext_vector_type(4))) float f32x4_t;
+typedef __attribute__((ext_vector_type(2))) float f32x2_t;
 typedef __attribute__((ext_vector_type(4))) short i16x4_t;
 typedef __attribute__((ext_vector_type(8))) short i16x8_t;
 typedef __attribute__((ext_vector_type(4))) unsigned u32x4_t;
@@ -55,9 +56,12 @@ template <> struct Elt<true> {
   // v_cvt_pk_bf16_f32 (RNE, NaN-preserving).  Kept compiler-visible on purpose: an asm convert is
   // opaque to the hazard recognizer, which then omits the wait states between an MFMA and a
   // following VALU write of that MFMA's source registers (observed: corrupted dQ operands).
+  // The pair goes through ONE vector fptrunc (__builtin_convertvector): two scalar casts plus a
+  // build_vector were lowered in some kernels to cvt(lo, 0), cvt(lo, hi), v_bfi / v_perm -- twice the
+  // VALU of the single v_cvt_pk_bf16_f32 (seen in the dK/dV kernel's P packing).
   __device__ static inline unsigned pack2(float lo, float hi) {
-    bf16x2_t v = {(__bf16)lo, (__bf16)hi};
-    return __builtin_bit_cast(unsigned, v);
+    const f32x2_t v = {lo, hi};
+    return __builtin_bit_cast(unsigned, __builtin_convertvector(v, bf16x2_t));
   }
   __device__ static inline float to_f32(unsigned short x) {
     return __builtin_bit_cast(float, (unsigned)x << 16);
@@ -70,8 +74,8 @@ template <> struct Elt<false> {
                                                   __builtin_bit_cast(f16x8_t, b), c, 0, 0, 0);
   }
   __device__ static inline unsigned pack2(float lo, float hi) {   // v_cvt_pk_f16_f32 (RNE)
-    f16x2_t v = {(_Float16)lo, (_Float16)hi};
-    return __builtin_bit_cast(unsigned, v);
+    const f32x2_t v = {lo, hi};
+    return __builtin_bit_cast(unsigned, __builtin_convertvector(v, f16x2_t));
   }
   __device__ static inline float to_f32(unsigned short x) {
     return (float)__builtin_bit_cast(_Float16, x);
