@@ -49,8 +49,6 @@ template <int D> struct FwdTile {
   static constexpr int MINB = D <= 128 ? 2 : 1;   // __launch_bounds__ blocks per CU (register budget)
 };
 constexpr int kFwdBufs = 4;   // K ring depth: tiles nb, nb+1 read while nb+2, nb+3 land
-constexpr float kFwdRescaleThr = 8.f;   // deferred-max threshold, log2 units (P <= 256)
-constexpr float kFwdSumThr = 256.f;     // fast-path guard on a lane's per-tile sum of P (= 2^8)
 
 // MASKED: the dense additive mask and/or FlashMask are present; such a launch has no fast path (every
 // tile takes the per-element general path), and the unmasked instantiations carry no mask code.
@@ -621,6 +619,13 @@ template <bool BF16, int D, bool CAUSAL, bool DROPOUT>
 static void run_fwd(const FwdParams& p, hipStream_t stream) {
   dim3 grid(p.s.b * p.s.h * p.num_m_blocks);   // 1-D: heads fastest, heaviest query block first
   prof_begin(kTimeFwd, stream);
+  if constexpr (!DROPOUT && (D == 64 || D == 128)) {
+    static_assert(FwdTile<D>::BM == 256, "fwd_kernel_w4 covers the same 256-row blocks");
+    if (launch_fwd_w4(p, BF16, stream)) {   // 4 waves x 64 rows (fa_fwd_w4.hip)
+      prof_end(kTimeFwd, stream);
+      return;
+    }
+  }
   if constexpr (!CAUSAL && !DROPOUT) {
     if (p.n_split > 0) {
       hipLaunchKernelGGL((fwd_kernel<BF16, D, false, false, false, true>), dim3(grid.x, p.n_split),
