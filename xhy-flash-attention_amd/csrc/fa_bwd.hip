@@ -142,6 +142,22 @@ __global__ void __launch_bounds__(256) bwd_pre_kernel(const BwdParams p) {
   }
 }
 
+#ifdef FA_STAMPS
+// Dev timeline instrumentation (FA_STAMPS builds only, tools/stamps.py): s_memtime at phase
+// boundaries of the dK/dV loop for workgroups 0-3, 64 slices, 8 points per slice.
+constexpr int kStampWg = 4, kStampIt = 64, kStampPts = 8;
+__device__ unsigned long long g_fa_stamps[kStampWg * 8 * kStampIt * kStampPts];
+#define FA_STAMP(k)                                                                             \
+  do {                                                                                          \
+    __builtin_amdgcn_sched_barrier(0);                                                          \
+    if (blockIdx.x < kStampWg && it < kStampIt && lane == 0)                                    \
+      g_fa_stamps[((blockIdx.x * 8 + wave) * kStampIt + it) * kStampPts + (k)] = __builtin_amdgcn_s_memtime(); \
+    __builtin_amdgcn_sched_barrier(0);                                                          \
+  } while (0)
+#else
+#define FA_STAMP(k) do {} while (0)
+#endif
+
 // ------------------------------------------------------------------------------------------------
 // 2. dK / dV  (wave-specialised: 4 "P" waves + 4 "dS" waves per 128-key block)
 // ------------------------------------------------------------------------------------------------
@@ -179,7 +195,6 @@ __global__ void __launch_bounds__(DkdvTile<D>::NW * 64, 1) bwd_dkdv_kernel(const
   constexpr int XBUF = NKG * NQT * XTILE;           // P of one slice: key groups x q-tiles
   constexpr int XBASE = OBASE + 2 * QTILE;
   constexpr int PIECES = QTILE / 1024;
-  constexpr int PPW = (PIECES + NW - 1) / NW;
   static_assert(QTILE % 1024 == 0, "slice must be whole DMA pieces");
   static_assert(BQ % 32 == 0 && NW % 2 == 0, "32-row q-tiles, two roles");
   // ... then (dropout) one 1-KiB random-byte scratch per P wave
@@ -235,11 +250,19 @@ __global__ void __launch_bounds__(DkdvTile<D>::NW * 64, 1) bwd_dkdv_kernel(const
   const int ns = m_count > m_first ? m_count - m_first : 0;
   const int total = ns * nh;
 
-  int voff_q[PPW], voff_o[PPW];
+  // The slice DMA is issued by the dS waves (waves [DW0, DW0 + DWN)): the P waves' step (S, exp,
+  // P store, dV) is the longer one, and taking the DMA issue off it measured -4% (min) / -9%
+  // (median) dK/dV time at C3 against every wave issuing; P waves only: -2%.  4-wave workgroups
+  // (d > 128): every wave.
+  constexpr int DWN = NW == 8 ? 4 : NW, DW0 = NW == 8 ? 4 : 0;
+  constexpr int PPWI = (PIECES + DWN - 1) / DWN;
+  const int dwv = wave - DW0;
+  const bool dma_wave = dwv >= 0 && dwv < DWN;
+  int voff_q[PPWI], voff_o[PPWI];
 #pragma unroll
-  for (int j = 0; j < PPW; ++j) {
-    voff_q[j] = dma_voff<BQ>(wave + j * NW, lane, p.q_row, dlim);
-    voff_o[j] = dma_voff<BQ>(wave + j * NW, lane, p.do_row, dlim);
+  for (int j = 0; j < PPWI; ++j) {
+    voff_q[j] = dma_voff<BQ>(dwv + j * DWN, lane, p.q_row, dlim);
+    voff_o[j] = dma_voff<BQ>(dwv + j * DWN, lane, p.do_row, dlim);
   }
   // Sweep order: the query slices of one head, then the next head of the GQA group.  (Last slice
   // first with the heads innermost -- every key block then starts on the same slice -- measured 3.5%
@@ -247,9 +270,11 @@ __global__ void __launch_bounds__(DkdvTile<D>::NW * 64, 1) bwd_dkdv_kernel(const
   auto slice_head = [&](int it) { return it / ns; };
   auto slice_q0 = [&](int it) { return (m_first + it % ns) * BQ; };
   // slice `sid` into ring position `it` (the same except when FlashMask skips slices)
-  auto issue = [&](int sid, int it) {
-    const int hq = h_begin + slice_head(sid);
-    const int q0 = slice_q0(sid);
+  // DMA of the slice (query head h_begin + hrel, rows q0..) into ring position `it`; the dS waves
+  // issue it (the P waves skip the address arithmetic too: the CU's scalar unit is shared)
+  auto issue = [&](int hrel, int q0, int it) {
+    if (!dma_wave) return;
+    const int hq = h_begin + hrel;
     char* qdst = smem + (it % 3) * QSLOT;
     char* odst = smem + OBASE + (it & 1) * QTILE;
     const u16* Qp = (const u16*)p.q + geo.q_off + (int64_t)hq * p.q_head + (int64_t)q0 * p.q_row;
@@ -257,18 +282,18 @@ __global__ void __launch_bounds__(DkdvTile<D>::NW * 64, 1) bwd_dkdv_kernel(const
     const buf_rsrc_t rq = make_rsrc(Qp, rec_bytes(sq - q0, p.q_row, 2));
     const buf_rsrc_t ro = make_rsrc(Dp, rec_bytes(sq - q0, p.do_row, 2));
 #pragma unroll
-    for (int j = 0; j < PPW; ++j) {
-      const int pc = wave + j * NW;
-      if (PIECES % NW == 0 || pc < PIECES) {
+    for (int j = 0; j < PPWI; ++j) {
+      const int pc = dwv + j * DWN;
+      if (PIECES % DWN == 0 || pc < PIECES) {
         dma16(rq, qdst + pc * 1024, voff_q[j]);
         dma16(ro, odst + pc * 1024, voff_o[j]);
       }
     }
-    if (wave < 2) {   // wave 0: -LSE/scale rows, wave 1: D rows (64 x 4 bytes each; rows past
-                      // the slice land in the slot's padding or are never read)
+    if (dwv == 0 || dwv == 1) {   // -LSE/scale rows, then D rows (64 x 4 bytes each; rows past
+                                  // the slice land in the slot's padding or are never read)
       const int64_t bhi = (int64_t)bidb * s.h + hq;
-      const float* src = ((wave == 0) ? p.lse_s : p.dsum) + bhi * p.seqlen_q_rounded + q0;
-      dma4(make_rsrc(src, rec_bytes(sq - q0, 1, 4)), qdst + QTILE + wave * 64 * 4, lane * 4);
+      const float* src = ((dwv == 0) ? p.lse_s : p.dsum) + bhi * p.seqlen_q_rounded + q0;
+      dma4(make_rsrc(src, rec_bytes(sq - q0, 1, 4)), qdst + QTILE + dwv * 64 * 4, lane * 4);
     }
   };
 
@@ -285,6 +310,7 @@ __global__ void __launch_bounds__(DkdvTile<D>::NW * 64, 1) bwd_dkdv_kernel(const
   // slice at `a1` (query on registers, key on lane), chains started from `init`
   auto phase1 = [&](int a1, f32x16_t (&sp)[NQT]) {
     const TileAddr ta(lb, a1);
+#ifdef FA_PH1_OLD
     constexpr int G = KS >= 4 ? (NQT == 2 ? KS / 2 : KS / 4) : KS;   // A fragments in flight per group
     static_for<0, KS / G>([&](auto GG) {
       constexpr int g0 = decltype(GG)::value * G;
@@ -301,6 +327,35 @@ __global__ void __launch_bounds__(DkdvTile<D>::NW * 64, 1) bwd_dkdv_kernel(const
 #pragma unroll
         for (int qt = 0; qt < NQT; ++qt) sp[qt] = E::mfma(af[qt][k], kv[g0 + k], sp[qt]);
     });
+#else
+    // Software-pipelined: the A fragments of k-group g+1 are requested before the MFMAs of group g
+    // (sched_barrier keeps the scheduler from sinking the reads next to their MFMAs, which left
+    // each LDS read's latency exposed in front of its two MFMAs).
+    constexpr int G = KS >= 4 ? 2 : KS;   // k-steps per group
+    constexpr int NG = KS / G;
+    i16x8_t af[2][NQT][G];
+    auto load = [&](auto GGC, i16x8_t (&dst)[NQT][G]) {
+      constexpr int g0 = decltype(GGC)::value * G;
+      static_for<0, G>([&](auto KK) {
+        constexpr int ks = g0 + decltype(KK)::value;
+        static_for<0, NQT>([&](auto QT) {
+          constexpr int qt = decltype(QT)::value;
+          dst[qt][ks - g0] = row_read_c<BQ, 32 * qt, 2 * ks>(smem, ta);
+        });
+      });
+    };
+    load(std::integral_constant<int, 0>{}, af[0]);
+    static_for<0, NG>([&](auto GG) {
+      constexpr int gg = decltype(GG)::value;
+      if constexpr (gg + 1 < NG) load(std::integral_constant<int, gg + 1>{}, af[(gg + 1) & 1]);
+      __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+      for (int k = 0; k < G; ++k)
+#pragma unroll
+        for (int qt = 0; qt < NQT; ++qt) sp[qt] = E::mfma(af[gg & 1][qt][k], kv[gg * G + k], sp[qt]);
+      __builtin_amdgcn_sched_barrier(0);
+    });
+#endif
   };
   // phase 2: acc += A^T frag, transposed A operand of the slice tile at `a2`; the fragments of
   // d-group dt+1 are requested before the MFMAs of group dt
@@ -423,7 +478,12 @@ __global__ void __launch_bounds__(DkdvTile<D>::NW * 64, 1) bwd_dkdv_kernel(const
   // Static priority for the dS waves: on each SIMD the dS wave's step opens with its (short) VALU
   // block and then feeds the matrix pipe, while the P wave's exp-heavy block can wait; measured at
   // C3: dS waves at prio 1 +9%, P waves at prio 1 +5%, versus none.
+#if defined(FA_DKDV_PRIO_NONE)
+#elif defined(FA_DKDV_PRIO_P)
+  if (pwave) __builtin_amdgcn_s_setprio(1);
+#else
   if (!pwave) __builtin_amdgcn_s_setprio(1);
+#endif
   // FlashMask slice skip: a slice is dead when the bounds hide every key of this workgroup from
   // every row of the slice (fm_tile_dead per 64 keys); all waves walk the same live slices
   auto slice_dead = [&](int sid) {
@@ -447,7 +507,7 @@ __global__ void __launch_bounds__(DkdvTile<D>::NW * 64, 1) bwd_dkdv_kernel(const
     return sid;
   };
   int sid = next_live(-1);
-  if (sid < total) issue(sid, 0);
+  if (sid < total) issue(slice_head(sid), slice_q0(sid), 0);
   wait_vmem_all();   // K/V fragments and slice 0 (compiler-visible: no vmcnt waits inside the loop)
   lds_barrier();
 
@@ -457,20 +517,30 @@ __global__ void __launch_bounds__(DkdvTile<D>::NW * 64, 1) bwd_dkdv_kernel(const
   //   P waves:                            | sp = S(it)     (MFMA) | P(it) (VALU)    | dV   += dO(it)^T P
   f32x16_t sp[NQT];  // S of this slice (P waves) / dP'' of the previous slice (dS waves)
   int it = 0;   // ring position of slice sid (the same slice without a mask)
+  // unmasked walk: (query-slice index, head) of the current and the next slice, kept incrementally
+  // (the slice id -> (head, row) division costs ~20 scalar instructions per use)
+  int cq = 0, chd = 0, nqi = 1, nhd = 0;
+  if (nqi == ns) { nqi = 0; nhd = 1; }
   for (; MASKED ? sid < total : it < total; ++it) {
     const int cur = MASKED ? sid : it;
     const int nxt = MASKED ? next_live(sid) : it + 1;
+    FA_STAMP(0);
 #ifndef FA_ABL_NODMA
-    if (nxt < total) issue(nxt, it + 1);
+    if (nxt < total) {
+      if constexpr (MASKED) issue(slice_head(nxt), slice_q0(nxt), it + 1);
+      else issue(nhd, (m_first + nqi) * BQ, it + 1);
+    }
 #endif
-    const int q0 = slice_q0(cur);
-    const int it_head = slice_head(cur);   // query head of this slice within the group
+    FA_STAMP(1);
+    const int q0 = MASKED ? slice_q0(cur) : (m_first + cq) * BQ;
+    const int it_head = MASKED ? slice_head(cur) : chd;   // query head of this slice within the group
     const int qs = (it % 3) * QSLOT;
     const float* lt = (const float*)(smem + qs + QTILE);
     const int os = OBASE + (it & 1) * QTILE;
     i16x8_t fr[2 * NQT];
     if (!pwave && it > 0)
       ds_step(sp, xw_of(it - 1), (const float*)(smem + ((it + 2) % 3) * QSLOT + QTILE) + 64, fr);
+    FA_STAMP(2);
     // chain start: -LSE / scale (P waves) or D (dS waves), per accumulator row
     const float* init = lt + (pwave ? 0 : 64);
 #pragma unroll
@@ -484,16 +554,19 @@ __global__ void __launch_bounds__(DkdvTile<D>::NW * 64, 1) bwd_dkdv_kernel(const
 #ifndef FA_ABL_NOPH1
     phase1(pwave ? qs : os, sp);                       // S' = Q K^T - LSE/scale  /  dP'' = D - dO V^T
 #endif
+    FA_STAMP(3);
     if (pwave) {
       const bool fast = !MASKED && (q0 + BQ <= sq) && (n0 + BKN <= sk) && (!CAUSAL || q0 >= n0 + BKN - 1);
       if (fast) p_step(std::false_type{}, sp, q0, it_head, xw_of(it), fr);
       else p_step(std::true_type{}, sp, q0, it_head, xw_of(it), fr);
     }
+    FA_STAMP(4);
 #ifndef FA_ABL_NOPH2
     if (pwave || it > 0) phase2(pwave ? os : ((it + 2) % 3) * QSLOT, fr);   // dV^T / dK''^T
 #else
     if (pwave || it > 0) acc[0] = E::mfma(fr[0], fr[1], acc[0]);   // keep fr live
 #endif
+    FA_STAMP(5);
 #if defined(FA_ABL_NODMAWAIT)
     lds_barrier();   // ablation (wrong results): DMA never waited for
 #elif defined(FA_ABL_NOBARRIER)
@@ -501,7 +574,12 @@ __global__ void __launch_bounds__(DkdvTile<D>::NW * 64, 1) bwd_dkdv_kernel(const
 #else
     wait_dma_keep_and_barrier(0);
 #endif
+    FA_STAMP(6);
     if constexpr (MASKED) sid = nxt;
+    else {
+      cq = nqi; chd = nhd;
+      if (++nqi == ns) { nqi = 0; ++nhd; }
+    }
   }
   const int nlive = MASKED ? it : total;
   if (!pwave && nlive > 0) {   // the last slice's dK update (no DMA after it: its Q is resident)
@@ -639,6 +717,7 @@ __global__ void __launch_bounds__(DqTile<D>::NW * 64, DqTile<D>::MINB) bwd_dq_ke
     const int kt = (pos % kBwdBufs) * 2 * TILE;
     const TileAddr tk(lb, kt), tv(lb, kt + TILE);
     f32x16_t st[NT], pt[NT];
+#ifndef FA_DQ_PIPE   // the pipelined form below spills at 256 VGPRs (113 registers): off
     static_for<0, NT>([&](auto T) {
       constexpr int t = decltype(T)::value;
 #pragma unroll
@@ -658,6 +737,43 @@ __global__ void __launch_bounds__(DqTile<D>::NW * 64, DqTile<D>::MINB) bwd_dq_ke
         }
       });
     });
+#else
+    // Software-pipelined over (subtile, k-pair) groups: the K / V fragments of group g+1 are
+    // requested before the MFMAs of group g (with the reads sunk next to their MFMAs, every LDS read
+    // waited at lgkmcnt(0) in front of one MFMA).
+    {
+      constexpr int G2 = 2;                    // k-steps per group
+      constexpr int NGK = KS / G2;             // groups per subtile
+      constexpr int NG = NT * NGK;
+      i16x8_t fa[2][2 * G2];                   // [buffer][ka0, va0, ka1, va1]
+      auto load = [&](auto GC, i16x8_t (&dst)[2 * G2]) {
+        constexpr int g = decltype(GC)::value;
+        constexpr int t = g / NGK, k0 = (g % NGK) * G2;
+        static_for<0, G2>([&](auto KK) {
+          constexpr int k = decltype(KK)::value;
+          dst[2 * k] = row_read_c<BN, t * 32, 2 * (k0 + k)>(smem, tk);
+          dst[2 * k + 1] = row_read_c<BN, t * 32, 2 * (k0 + k)>(smem, tv);
+        });
+      };
+#pragma unroll
+      for (int t = 0; t < NT; ++t)
+#pragma unroll
+        for (int g = 0; g < 16; ++g) { st[t][g] = 0.f; pt[t][g] = -dsum_q; }
+      load(std::integral_constant<int, 0>{}, fa[0]);
+      static_for<0, NG>([&](auto GG) {
+        constexpr int g = decltype(GG)::value;
+        constexpr int t = g / NGK, k0 = (g % NGK) * G2;
+        if constexpr (g + 1 < NG) load(std::integral_constant<int, g + 1>{}, fa[(g + 1) & 1]);
+        __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+        for (int k = 0; k < G2; ++k) {
+          st[t] = E::mfma(fa[g & 1][2 * k], qf[k0 + k], st[t]);
+          pt[t] = E::mfma(fa[g & 1][2 * k + 1], of[k0 + k], pt[t]);
+        }
+        __builtin_amdgcn_sched_barrier(0);
+      });
+    }
+#endif
 #pragma unroll
     for (int t = 0; t < NT; ++t) {
       unsigned rb[4];
@@ -855,3 +971,9 @@ void launch_bwd(const BwdParams& p_in, bool is_bf16, hipStream_t stream) {
 }
 
 }  // namespace fa
+
+#ifdef FA_STAMPS
+extern "C" int flash_attn_debug_stamps(void* dst, size_t bytes) {
+  return (int)hipMemcpyFromSymbol(dst, HIP_SYMBOL(fa::g_fa_stamps), bytes, 0, hipMemcpyDeviceToHost);
+}
+#endif
