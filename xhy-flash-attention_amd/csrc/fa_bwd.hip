@@ -525,11 +525,16 @@ __global__ void __launch_bounds__(DkdvTile<D>::NW * 64, 1) bwd_dkdv_kernel(const
     const int cur = MASKED ? sid : it;
     const int nxt = MASKED ? next_live(sid) : it + 1;
     FA_STAMP(0);
+    auto issue_next = [&]() {
 #ifndef FA_ABL_NODMA
-    if (nxt < total) {
-      if constexpr (MASKED) issue(slice_head(nxt), slice_q0(nxt), it + 1);
-      else issue(nhd, (m_first + nqi) * BQ, it + 1);
-    }
+      if (nxt < total) {
+        if constexpr (MASKED) issue(slice_head(nxt), slice_q0(nxt), it + 1);
+        else issue(nhd, (m_first + nqi) * BQ, it + 1);
+      }
+#endif
+    };
+#ifndef FA_DKDV_ISSUE_LATE
+    issue_next();
 #endif
     FA_STAMP(1);
     const int q0 = MASKED ? slice_q0(cur) : (m_first + cq) * BQ;
@@ -540,6 +545,9 @@ __global__ void __launch_bounds__(DkdvTile<D>::NW * 64, 1) bwd_dkdv_kernel(const
     i16x8_t fr[2 * NQT];
     if (!pwave && it > 0)
       ds_step(sp, xw_of(it - 1), (const float*)(smem + ((it + 2) % 3) * QSLOT + QTILE) + 64, fr);
+#ifdef FA_DKDV_ISSUE_LATE
+    issue_next();
+#endif
     FA_STAMP(2);
     // chain start: -LSE / scale (P waves) or D (dS waves), per accumulator row
     const float* init = lt + (pwave ? 0 : 64);
