@@ -57,7 +57,9 @@ def main():
     ap.add_argument("--rounds", type=int, default=5)
     ap.add_argument("--iters", type=int, default=10)
     ap.add_argument("--bwd", action="store_true")
+    ap.add_argument("--dropout", type=float, default=0.0)
     args = ap.parse_args()
+    pd = args.dropout
 
     b, s, h, hk, d, dt, causal, _kind = WORKLOADS[args.workload]
     dtype = torch.bfloat16 if dt == "bf16" else torch.float16
@@ -74,11 +76,12 @@ def main():
     for rnd in range(args.rounds):
         for lib, name in zip(libs, names):
             m._lib = lib
-            res = m.fwd(q, k, v, None, 0.0, scale, causal, False, None)
+            gen = torch.Generator(device="cuda").manual_seed(7) if pd > 0 else None
+            res = m.fwd(q, k, v, None, pd, scale, causal, False, gen)
             out, lse = res[0], res[5]
             grads = None
             if args.bwd:
-                grads = m.bwd(dout, q, k, v, out, lse, None, None, None, 0.0, scale, causal, None, res[7])[:3]
+                grads = m.bwd(dout, q, k, v, out, lse, None, None, None, pd, scale, causal, None, res[7])[:3]
             torch.cuda.synchronize()
             if rnd == 0:
                 cur = [out, lse] + (list(grads) if grads else [])
@@ -90,9 +93,9 @@ def main():
                           + ", ".join(f"{x:.3e}" for x in diffs), flush=True)
             lib.flash_attn_timing_enable(1)
             for _ in range(args.iters):
-                r2 = m.fwd(q, k, v, None, 0.0, scale, causal, False, None)
+                r2 = m.fwd(q, k, v, None, pd, scale, causal, False, None)
                 if args.bwd:
-                    m.bwd(dout, q, k, v, r2[0], r2[5], None, None, None, 0.0, scale, causal, None, r2[7])
+                    m.bwd(dout, q, k, v, r2[0], r2[5], None, None, None, pd, scale, causal, None, r2[7])
             torch.cuda.synchronize()
             t = read_times(lib)
             lib.flash_attn_timing_enable(0)

@@ -157,6 +157,12 @@ __device__ unsigned long long g_fa_stamps[kStampWg * 8 * kStampIt * kStampPts];
 #else
 #define FA_STAMP(k) do {} while (0)
 #endif
+#ifndef FA_DKDV_DMA_POS      // dev A/B switch: where the dS waves issue the later DMA parts
+#define FA_DKDV_DMA_POS 0
+#endif
+#ifndef FA_DKDV_UNFUSED_P   // dev A/B switch: 1 = the unfused P-wave step
+#define FA_DKDV_UNFUSED_P 0
+#endif
 
 // ------------------------------------------------------------------------------------------------
 // 2. dK / dV  (wave-specialised: 4 "P" waves + 4 "dS" waves per 128-key block)
@@ -272,29 +278,54 @@ __global__ void __launch_bounds__(DkdvTile<D>::NW * 64, 1) bwd_dkdv_kernel(const
   // slice `sid` into ring position `it` (the same except when FlashMask skips slices)
   // DMA of the slice (query head h_begin + hrel, rows q0..) into ring position `it`; the dS waves
   // issue it (the P waves skip the address arithmetic too: the CU's scalar unit is shared)
-  auto issue = [&](int hrel, int q0, int it) {
-    if (!dma_wave) return;
+  // The DMA of one slice is issued in DMA_PARTS parts (pieces [k PPWI / parts, (k+1) PPWI / parts) in
+  // part k, the -LSE/scale and D rows with part 0), spread over the dS waves' step (FA_DKDV_DMA_POS).
+  // (the plan holds plain scalars, made wave-uniform, and the descriptors are formed at each part:
+  // a buffer descriptor kept live across the step can be assigned VGPRs, which the asm rejects)
+  const unsigned smem_lds = lds_addr(smem);
+  struct SliceDma {
+    const u16* qp;
+    const u16* dp;
+    const float* lp;
+    int qrec, orec, lrec, slot;
+  };
+  auto dma_plan = [&](int hrel, int q0, int it) {
+    SliceDma d;
     const int hq = h_begin + hrel;
-    char* qdst = smem + (it % 3) * QSLOT;
-    char* odst = smem + OBASE + (it & 1) * QTILE;
-    const u16* Qp = (const u16*)p.q + geo.q_off + (int64_t)hq * p.q_head + (int64_t)q0 * p.q_row;
-    const u16* Dp = (const u16*)p.dout + geo.do_off + (int64_t)hq * p.do_head + (int64_t)q0 * p.do_row;
-    const buf_rsrc_t rq = make_rsrc(Qp, rec_bytes(sq - q0, p.q_row, 2));
-    const buf_rsrc_t ro = make_rsrc(Dp, rec_bytes(sq - q0, p.do_row, 2));
+    d.slot = it;
+    d.qp = (const u16*)p.q + geo.q_off + (int64_t)hq * p.q_head + (int64_t)q0 * p.q_row;
+    d.dp = (const u16*)p.dout + geo.do_off + (int64_t)hq * p.do_head + (int64_t)q0 * p.do_row;
+    d.qrec = rec_bytes(sq - q0, p.q_row, 2);
+    d.orec = rec_bytes(sq - q0, p.do_row, 2);
+    // -LSE/scale rows (dS wave 0), then D rows (dS wave 1), 64 x 4 bytes each; rows past the slice
+    // land in the slot's padding or are never read
+    const int64_t bhi = (int64_t)bidb * s.h + hq;
+    d.lp = ((dwv == 0) ? p.lse_s : p.dsum) + bhi * p.seqlen_q_rounded + q0;
+    d.lrec = rec_bytes(sq - q0, 1, 4);
+    return d;
+  };
+  auto dma_part = [&](const SliceDma& d, auto KC, auto NC) {
+    constexpr int k = decltype(KC)::value, n = decltype(NC)::value;
+    const int it = wave_uniform(d.slot);
+    const unsigned qdst = smem_lds + (it % 3) * QSLOT;
+    const unsigned odst = smem_lds + OBASE + (it & 1) * QTILE;
+    const buf_rsrc_t rq = make_rsrc(uniform_ptr(d.qp), wave_uniform(d.qrec));
+    const buf_rsrc_t ro = make_rsrc(uniform_ptr(d.dp), wave_uniform(d.orec));
 #pragma unroll
-    for (int j = 0; j < PPWI; ++j) {
+    for (int j = (k * PPWI) / n; j < ((k + 1) * PPWI) / n; ++j) {
       const int pc = dwv + j * DWN;
       if (PIECES % DWN == 0 || pc < PIECES) {
-        dma16(rq, qdst + pc * 1024, voff_q[j]);
-        dma16(ro, odst + pc * 1024, voff_o[j]);
+        dma16_at(rq, qdst + pc * 1024, voff_q[j]);
+        dma16_at(ro, odst + pc * 1024, voff_o[j]);
       }
     }
-    if (dwv == 0 || dwv == 1) {   // -LSE/scale rows, then D rows (64 x 4 bytes each; rows past
-                                  // the slice land in the slot's padding or are never read)
-      const int64_t bhi = (int64_t)bidb * s.h + hq;
-      const float* src = ((dwv == 0) ? p.lse_s : p.dsum) + bhi * p.seqlen_q_rounded + q0;
-      dma4(make_rsrc(src, rec_bytes(sq - q0, 1, 4)), qdst + QTILE + dwv * 64 * 4, lane * 4);
-    }
+    if (k == 0 && (dwv == 0 || dwv == 1))
+      dma4_at(make_rsrc(uniform_ptr(d.lp), wave_uniform(d.lrec)), qdst + QTILE + dwv * 64 * 4, lane * 4);
+  };
+  auto issue = [&](int hrel, int q0, int it) {
+    if (!dma_wave) return;
+    const SliceDma d = dma_plan(hrel, q0, it);
+    dma_part(d, std::integral_constant<int, 0>{}, std::integral_constant<int, 1>{});
   };
 
   // dV^T (P waves) or -dK^T (dS waves): D x 32 keys
@@ -473,6 +504,83 @@ __global__ void __launch_bounds__(DkdvTile<D>::NW * 64, 1) bwd_dkdv_kernel(const
       fr[2 * qi + 1] = pack_frag<BF16>(x, 1);
     }
   };
+  // P waves of the plain instantiations (no dropout, no mask, 2 q-tiles): S(it) -> P(it) ->
+  // dV^T += dO(it)^T P(it) q-tile by q-tile.  The softmax of q-tile 0 (exp, fp32 store for the dS
+  // waves, bf16 pack) is issued between the S MFMAs of q-tile 1 and that of q-tile 1 between the dV
+  // MFMAs of q-tile 0, so it fills MFMA gaps instead of running as a VALU-only block between two
+  // MFMA blocks (unfused: ~1000 of ~3400 cycles per slice on the P waves, tools/stamps.py).
+  constexpr bool kFused = !DROPOUT && !MASKED && NQT == 2 && !FA_DKDV_UNFUSED_P;
+  auto p_fused = [&](int it, int aq, int ao, char* xw, f32x16_t (&sp)[NQT]) {
+    if constexpr (kFused) {
+      const TileAddr ta(lb, aq), ta2(lb, ao);
+      i16x8_t fr[2 * NQT];
+      // half-piece h (0..7) of q-tile QF: elements 2h, 2h+1 of the lane's 16; the fp32 store of a row
+      // group follows its odd half, the pack of a 16-row half follows h = 3 / 7
+      auto half_piece = [&](auto QFC, auto HC) {
+        constexpr int qf = decltype(QFC)::value, h = decltype(HC)::value;
+        constexpr int u = h >> 1;
+  #pragma unroll
+        for (int j = 2 * (h & 1); j < 2 * (h & 1) + 2; ++j) sp[qf][4 * u + j] = fast_exp2(sp[qf][4 * u + j] * c);
+        if constexpr (h & 1) {
+          const f32x4_t pv = {sp[qf][4 * u], sp[qf][4 * u + 1], sp[qf][4 * u + 2], sp[qf][4 * u + 3]};
+          *(f32x4_t*)(xw + qf * XTILE + u * 1024) = pv;
+        }
+        if constexpr ((h & 3) == 3) fr[2 * qf + (h >> 2)] = pack_frag<BF16>(sp[qf], h >> 2);
+      };
+      // an MFMA chain of N steps, operand k fetched two steps ahead, step k followed by fill(k)
+      auto chain = [&](auto NC, auto&& load, auto&& mma, auto&& fill) {
+        constexpr int N = decltype(NC)::value;
+        i16x8_t a[3];
+        a[0] = load(std::integral_constant<int, 0>{});
+        if constexpr (N > 1) a[1] = load(std::integral_constant<int, 1>{});
+        static_for<0, N>([&](auto KC) {
+          constexpr int k = decltype(KC)::value;
+          if constexpr (k + 2 < N) a[(k + 2) % 3] = load(std::integral_constant<int, k + 2>{});
+          __builtin_amdgcn_sched_barrier(0);
+          mma(KC, a[k % 3]);
+          fill(KC);
+          __builtin_amdgcn_sched_barrier(0);
+        });
+      };
+      // fill of an N-step chain with the softmax of q-tile QF: half-pieces [8k/N, 8(k+1)/N) after step k
+      auto softmax_fill = [&](auto QFC, auto NC) {
+        return [&, QFC](auto KC) {
+          constexpr int N = decltype(NC)::value, k = decltype(KC)::value;
+          static_for<(8 * k) / N, (8 * (k + 1)) / N>([&](auto HC) { half_piece(QFC, HC); });
+        };
+      };
+      auto no_fill = [](auto) {};
+      auto s_chain = [&](auto QTC, auto&& fill) {
+        constexpr int qt = decltype(QTC)::value;
+        chain(std::integral_constant<int, KS>{},
+              [&](auto KC) { return row_read_c<BQ, 32 * qt, 2 * decltype(KC)::value>(smem, ta); },
+              [&](auto KC, const i16x8_t& a) { sp[qt] = E::mfma(a, kv[decltype(KC)::value], sp[qt]); },
+              fill);
+      };
+      auto dv_chain = [&](auto QTC, auto&& fill) {
+        constexpr int qt = decltype(QTC)::value;
+        chain(std::integral_constant<int, 2 * NP>{},
+              [&](auto KC) {
+                constexpr int k = decltype(KC)::value;
+                return tr_frag_c<BQ, 16 * (2 * qt + (k & 1)), k / 2>(smem, ta2);
+              },
+              [&](auto KC, const i16x8_t& a) {
+                constexpr int k = decltype(KC)::value;
+                acc[k / 2] = E::mfma(a, fr[2 * qt + (k & 1)], acc[k / 2]);
+              },
+              fill);
+      };
+      using I0 = std::integral_constant<int, 0>;
+      using I1 = std::integral_constant<int, 1>;
+      s_chain(I0{}, no_fill);
+      s_chain(I1{}, softmax_fill(I0{}, std::integral_constant<int, KS>{}));
+      FA_STAMP(3);
+      dv_chain(I0{}, softmax_fill(I1{}, std::integral_constant<int, 2 * NP>{}));
+      FA_STAMP(4);
+      dv_chain(I1{}, no_fill);
+    }
+    (void)it; (void)aq; (void)ao; (void)xw; (void)sp;
+  };
   auto xw_of = [&](int it) { return smem + XBASE + (it & 1) * XBUF + kg * NQT * XTILE + lane * 16; };
 
   // Static priority for the dS waves: on each SIMD the dS wave's step opens with its (short) VALU
@@ -511,46 +619,67 @@ __global__ void __launch_bounds__(DkdvTile<D>::NW * 64, 1) bwd_dkdv_kernel(const
   wait_vmem_all();   // K/V fragments and slice 0 (compiler-visible: no vmcnt waits inside the loop)
   lds_barrier();
 
-  // One instruction skeleton for both roles (phase 1 and phase 2 each have ONE call site, so the
-  // register assignment of `sp` / `acc` is shared and no accumulator copies appear at the joins):
-  //   dS waves: dS''(it-1) from sp (VALU) | sp = dP''(it) (MFMA) |                 | dK'' += Q(it-1)^T dS''
-  //   P waves:                            | sp = S(it)     (MFMA) | P(it) (VALU)    | dV   += dO(it)^T P
-  f32x16_t sp[NQT];  // S of this slice (P waves) / dP'' of the previous slice (dS waves)
-  int it = 0;   // ring position of slice sid (the same slice without a mask)
+  // Each role runs its own copy of the slice loop (same trip count, the same one barrier per slice),
+  // so each is register-allocated and scheduled for its own instruction mix:
+  //   dS waves: dS''(it-1) from sp (VALU) | sp = dP''(it) (MFMA) | dK'' += Q(it-1)^T dS''(it-1)
+  //   P waves:  sp = S(it) (MFMA) | P(it) (VALU) | dV += dO(it)^T P(it), fused q-tile by q-tile in the
+  //             plain instantiations (p_fused)
   // unmasked walk: (query-slice index, head) of the current and the next slice, kept incrementally
   // (the slice id -> (head, row) division costs ~20 scalar instructions per use)
-  int cq = 0, chd = 0, nqi = 1, nhd = 0;
-  if (nqi == ns) { nqi = 0; nhd = 1; }
-  for (; MASKED ? sid < total : it < total; ++it) {
-    const int cur = MASKED ? sid : it;
-    const int nxt = MASKED ? next_live(sid) : it + 1;
-    FA_STAMP(0);
-    auto issue_next = [&]() {
-#ifndef FA_ABL_NODMA
-      if (nxt < total) {
-        if constexpr (MASKED) issue(slice_head(nxt), slice_q0(nxt), it + 1);
-        else issue(nhd, (m_first + nqi) * BQ, it + 1);
+  const int sid0 = sid;
+  // (DMAC: whether this loop's waves issue slice DMA -- the P waves' loop carries no DMA code, so
+  // no DMA offsets stay live in it)
+  // (DMAC: whether this loop's waves issue slice DMA -- the P waves' loop carries no DMA code, so
+  // no DMA offsets stay live in it; NPC: the number of parts the DMA is issued in, part 0 at the
+  // top of the step, part k by the body's dma(k))
+  auto sweep = [&](auto DMAC, auto NPC, auto&& body) {
+    constexpr bool DMA = decltype(DMAC)::value;
+    int it = 0;   // ring position of slice sid (the same slice without a mask)
+    int sd = sid0;
+    int cq = 0, chd = 0, nqi = 1, nhd = 0;
+    if (nqi == ns) { nqi = 0; nhd = 1; }
+    for (; MASKED ? sd < total : it < total; ++it) {
+      const int cur = MASKED ? sd : it;
+      const int nxt = MASKED ? next_live(sd) : it + 1;
+      FA_STAMP(0);
+      const bool more = DMA && nxt < total;
+      SliceDma d{};
+      if (more) {
+        if constexpr (MASKED) d = dma_plan(slice_head(nxt), slice_q0(nxt), it + 1);
+        else d = dma_plan(nhd, (m_first + nqi) * BQ, it + 1);
       }
+#ifndef FA_ABL_NODMA
+      if (more) dma_part(d, std::integral_constant<int, 0>{}, NPC);
 #endif
-    };
-#ifndef FA_DKDV_ISSUE_LATE
-    issue_next();
+      auto dma = [&](auto KC) {
+#ifndef FA_ABL_NODMA
+        if (more) dma_part(d, KC, NPC);
 #endif
-    FA_STAMP(1);
-    const int q0 = MASKED ? slice_q0(cur) : (m_first + cq) * BQ;
-    const int it_head = MASKED ? slice_head(cur) : chd;   // query head of this slice within the group
-    const int qs = (it % 3) * QSLOT;
-    const float* lt = (const float*)(smem + qs + QTILE);
-    const int os = OBASE + (it & 1) * QTILE;
-    i16x8_t fr[2 * NQT];
-    if (!pwave && it > 0)
-      ds_step(sp, xw_of(it - 1), (const float*)(smem + ((it + 2) % 3) * QSLOT + QTILE) + 64, fr);
-#ifdef FA_DKDV_ISSUE_LATE
-    issue_next();
+      };
+      FA_STAMP(1);
+      const int q0 = MASKED ? slice_q0(cur) : (m_first + cq) * BQ;
+      const int it_head = MASKED ? slice_head(cur) : chd;   // query head of this slice within the group
+      body(it, q0, it_head, dma);
+      FA_STAMP(5);
+#if defined(FA_ABL_NODMAWAIT)
+      lds_barrier();   // ablation (wrong results): DMA never waited for
+#elif defined(FA_ABL_NOBARRIER)
+      wait_vmcnt(0);   // ablation (wrong results): no workgroup barrier
+#else
+      wait_dma_keep_and_barrier(0);
 #endif
-    FA_STAMP(2);
-    // chain start: -LSE / scale (P waves) or D (dS waves), per accumulator row
-    const float* init = lt + (pwave ? 0 : 64);
+      FA_STAMP(6);
+      if constexpr (MASKED) sd = nxt;
+      else {
+        cq = nqi; chd = nhd;
+        if (++nqi == ns) { nqi = 0; ++nhd; }
+      }
+    }
+    return it;
+  };
+  // chain start: -LSE / scale (P waves) or D (dS waves) of the slice in ring position it, per row
+  auto chain_init = [&](int it, f32x16_t (&sp)[NQT]) {
+    const float* init = (const float*)(smem + (it % 3) * QSLOT + QTILE) + (pwave ? 0 : 64);
 #pragma unroll
     for (int qi = 0; qi < NQT; ++qi)
 #pragma unroll
@@ -559,42 +688,79 @@ __global__ void __launch_bounds__(DkdvTile<D>::NW * 64, 1) bwd_dkdv_kernel(const
 #pragma unroll
         for (int j = 0; j < 4; ++j) sp[qi][4 * u + j] = iv[j];
       }
-#ifndef FA_ABL_NOPH1
-    phase1(pwave ? qs : os, sp);                       // S' = Q K^T - LSE/scale  /  dP'' = D - dO V^T
-#endif
-    FA_STAMP(3);
-    if (pwave) {
+  };
+
+  int nlive;
+  if (pwave) {
+    nlive = sweep(std::bool_constant<DWN == NW>{}, std::integral_constant<int, 1>{},
+                  [&](int it, int q0, int it_head, auto&&) {
+      const int qs = (it % 3) * QSLOT, os = OBASE + (it & 1) * QTILE;
+      f32x16_t sp[NQT];
+      chain_init(it, sp);
+      FA_STAMP(2);
       const bool fast = !MASKED && (q0 + BQ <= sq) && (n0 + BKN <= sk) && (!CAUSAL || q0 >= n0 + BKN - 1);
-      if (fast) p_step(std::false_type{}, sp, q0, it_head, xw_of(it), fr);
-      else p_step(std::true_type{}, sp, q0, it_head, xw_of(it), fr);
-    }
-    FA_STAMP(4);
+      if constexpr (kFused) {
+        // masked elements (causal, ragged ends): the S' chain starts from -inf, so P = exp2(-inf) = 0
+        // exactly (finite Q K^T), and the fused step itself carries no mask code
+        if (!fast) {
+#pragma unroll
+          for (int qi = 0; qi < NQT; ++qi)
+#pragma unroll
+            for (int g = 0; g < 16; ++g) {
+              const int q = q0 + 32 * qi + 8 * (g >> 2) + 4 * hh + (g & 3);
+              const bool out = (key >= sk) | (q >= sq) | (CAUSAL && key > q);
+              sp[qi][g] = out ? kNegInf : sp[qi][g];
+            }
+        }
+        p_fused(it, qs, os, xw_of(it), sp);
+      } else {
+        i16x8_t fr[2 * NQT];
+#ifndef FA_ABL_NOPH1
+        phase1(qs, sp);                       // S' = Q K^T - LSE/scale
+#endif
+        FA_STAMP(3);
+        if (fast) p_step(std::false_type{}, sp, q0, it_head, xw_of(it), fr);
+        else p_step(std::true_type{}, sp, q0, it_head, xw_of(it), fr);
+        FA_STAMP(4);
 #ifndef FA_ABL_NOPH2
-    if (pwave || it > 0) phase2(pwave ? os : ((it + 2) % 3) * QSLOT, fr);   // dV^T / dK''^T
+        phase2(os, fr);                       // dV^T += dO^T P
 #else
-    if (pwave || it > 0) acc[0] = E::mfma(fr[0], fr[1], acc[0]);   // keep fr live
+        acc[0] = E::mfma(fr[0], fr[1], acc[0]);   // keep fr live
 #endif
-    FA_STAMP(5);
-#if defined(FA_ABL_NODMAWAIT)
-    lds_barrier();   // ablation (wrong results): DMA never waited for
-#elif defined(FA_ABL_NOBARRIER)
-    wait_vmcnt(0);   // ablation (wrong results): no workgroup barrier
+      }
+    });
+  } else {
+    f32x16_t sp[NQT];  // dP'' of the previous slice
+    // DMA parts: at the top of the step, then after the dS step (bit 0 of FA_DKDV_DMA_POS) and
+    // after phase 1 (bit 1)
+    constexpr int kPos = FA_DKDV_DMA_POS;
+    constexpr int kP1 = (kPos & 1) ? 1 : 0, kP2 = kP1 + ((kPos & 2) ? 1 : 0);
+    nlive = sweep(std::true_type{}, std::integral_constant<int, 1 + kP2>{}, [&](int it, int, int, auto&& dma) {
+      const int os = OBASE + (it & 1) * QTILE;
+      i16x8_t fr[2 * NQT];
+      if (it > 0) ds_step(sp, xw_of(it - 1), (const float*)(smem + ((it + 2) % 3) * QSLOT + QTILE) + 64, fr);
+      if constexpr (kPos & 1) dma(std::integral_constant<int, kP1>{});
+      FA_STAMP(2);
+      chain_init(it, sp);
+#ifndef FA_ABL_NOPH1
+      phase1(os, sp);                         // dP'' = D - dO V^T
+#endif
+      if constexpr (kPos & 2) dma(std::integral_constant<int, kP2>{});
+      FA_STAMP(3);
+      FA_STAMP(4);
+#ifndef FA_ABL_NOPH2
+      if (it > 0) phase2(((it + 2) % 3) * QSLOT, fr);   // dK''^T += Q(it-1)^T dS''(it-1)
 #else
-    wait_dma_keep_and_barrier(0);
+      if (it > 0) acc[0] = E::mfma(fr[0], fr[1], acc[0]);
 #endif
-    FA_STAMP(6);
-    if constexpr (MASKED) sid = nxt;
-    else {
-      cq = nqi; chd = nhd;
-      if (++nqi == ns) { nqi = 0; ++nhd; }
+    });
+    if (nlive > 0) {   // the last slice's dK update (no DMA after it: its Q is resident)
+      i16x8_t fr[2 * NQT];
+      ds_step(sp, xw_of(nlive - 1), (const float*)(smem + ((nlive - 1) % 3) * QSLOT + QTILE) + 64, fr);
+      phase2(((nlive - 1) % 3) * QSLOT, fr);
     }
   }
-  const int nlive = MASKED ? it : total;
-  if (!pwave && nlive > 0) {   // the last slice's dK update (no DMA after it: its Q is resident)
-    i16x8_t fr[2 * NQT];
-    ds_step(sp, xw_of(nlive - 1), (const float*)(smem + ((nlive - 1) % 3) * QSLOT + QTILE) + 64, fr);
-    phase2(((nlive - 1) % 3) * QSLOT, fr);
-  }
+  (void)nlive;
 
   // ---- epilogue: dV = (dV^T)^T from the P waves, dK = -scale * (dK''^T)^T from the dS waves ----
   if (key < sk) {
@@ -635,8 +801,8 @@ __global__ void __launch_bounds__(DqTile<D>::NW * 64, DqTile<D>::MINB) bwd_dq_ke
   constexpr int PPW = (PIECES + NW - 1) / NW;
   constexpr int KG = (KS % 4 == 0) ? 4 : ((KS % 3 == 0) ? 3 : 2);
   static_assert(TILE % 1024 == 0 && KS % KG == 0, "tile shape");
-  // [buffer][K | V], then (dropout) one 1-KiB random-byte scratch per wave
-  __shared__ __attribute__((aligned(16))) char smem[kBwdBufs * 2 * TILE + (DROPOUT ? NW * 1024 : 0)];
+  // [buffer][K | V], then (dropout) NT 1-KiB random-byte scratch blocks per wave
+  __shared__ __attribute__((aligned(16))) char smem[kBwdBufs * 2 * TILE + (DROPOUT ? NW * NT * 1024 : 0)];
 
   const AttnShape s = p.s;
   const uint64_t pseed = DROPOUT ? philox_seed_of(s) : 0, poff = DROPOUT ? philox_offset_of(s) : 0;
@@ -724,6 +890,15 @@ __global__ void __launch_bounds__(DqTile<D>::NW * 64, DqTile<D>::MINB) bwd_dq_ke
     const int n0 = nb * BN;
     const int kt = (pos % kBwdBufs) * 2 * TILE;
     const TileAddr tk(lb, kt), tv(lb, kt + TILE);
+    // dropout bytes of the tile's NT 32x32 blocks, generated before the S / dP chains (the Philox
+    // temporaries then never overlap the live score tiles: generated inside the dS loop they made
+    // the causal dropout instantiation spill ~140 registers)
+    char* const dscr = smem + kBwdBufs * 2 * TILE + wave * NT * 1024;
+    if constexpr (DROPOUT) {
+      const uint64_t doff = poff + (uint64_t)bhi * 32;
+#pragma unroll
+      for (int t = 0; t < NT; ++t) dropout_block_bytes<false>(dscr + t * 1024, pseed, doff, wq0, n0 + 32 * t, lane);
+    }
     f32x16_t st[NT], pt[NT];
 #ifndef FA_DQ_PIPE   // the pipelined form below spills at 256 VGPRs (113 registers): off
     static_for<0, NT>([&](auto T) {
@@ -786,11 +961,8 @@ __global__ void __launch_bounds__(DqTile<D>::NW * 64, DqTile<D>::MINB) bwd_dq_ke
     for (int t = 0; t < NT; ++t) {
       unsigned rb[4];
       if constexpr (DROPOUT) {
-        char* dscr = smem + kBwdBufs * 2 * TILE + wave * 1024;
-        const uint64_t doff = poff + (uint64_t)bhi * 32;
-        dropout_block_bytes<false>(dscr, pseed, doff, wq0, n0 + 32 * t, lane);
 #pragma unroll
-        for (int u = 0; u < 4; ++u) rb[u] = dropout_group_bytes(dscr, r, hh, u);
+        for (int u = 0; u < 4; ++u) rb[u] = dropout_group_bytes(dscr + t * 1024, r, hh, u);
       }
 #pragma unroll
       for (int g = 0; g < 16; ++g) {

@@ -216,6 +216,11 @@ __device__ inline float half_swap_sum(float x) {
 __device__ inline float fast_exp2(float x) { return __builtin_amdgcn_exp2f(x); }
 __device__ inline float fast_rcp(float x) { return __builtin_amdgcn_rcpf(x); }
 __device__ inline int wave_uniform(int x) { return __builtin_amdgcn_readfirstlane(x); }
+template <typename T> __device__ inline const T* uniform_ptr(const T* p) {
+  const unsigned long long a = (unsigned long long)p;
+  const unsigned lo = __builtin_amdgcn_readfirstlane((unsigned)a), hi = __builtin_amdgcn_readfirstlane((unsigned)(a >> 32));
+  return (const T*)(((unsigned long long)hi << 32) | lo);
+}
 
 // LDS-DMA: 16 bytes per lane from a range-checked buffer (offsets past `bytes` read as zero) into
 // the wave-uniform LDS address `lds_dst` + 16 * lane.
@@ -248,6 +253,15 @@ __device__ inline void dma16(buf_rsrc_t rsrc, char* lds_dst, int voffset) {
 __device__ inline void dma4(buf_rsrc_t rsrc, char* lds_dst, int voffset) {
   asm volatile("s_nop 4\n\tbuffer_load_dword %1, %2, 0 offen lds"
                :: "{m0}"(lds_addr(lds_dst)), "v"(voffset), "s"(rsrc) : "memory");
+}
+// the same with the LDS destination as a byte address in the LDS aperture (wave-uniform)
+__device__ inline void dma16_at(buf_rsrc_t rsrc, unsigned lds, int voffset) {
+  asm volatile("s_nop 4\n\tbuffer_load_dwordx4 %1, %2, 0 offen lds"
+               :: "{m0}"(wave_uniform((int)lds)), "v"(voffset), "s"(rsrc) : "memory");
+}
+__device__ inline void dma4_at(buf_rsrc_t rsrc, unsigned lds, int voffset) {
+  asm volatile("s_nop 4\n\tbuffer_load_dword %1, %2, 0 offen lds"
+               :: "{m0}"(wave_uniform((int)lds)), "v"(voffset), "s"(rsrc) : "memory");
 }
 __device__ inline void wait_dma_and_barrier() {
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");

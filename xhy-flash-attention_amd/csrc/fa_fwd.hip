@@ -75,8 +75,8 @@ __global__ void __launch_bounds__(FwdTile<D>::NW * 64, FwdTile<D>::MINB) fwd_ker
   constexpr int VBUFS = STAGGER ? 5 : 4;
   constexpr int VBASE = kFwdBufs * TILE;
   constexpr int SCRATCH = VBASE + VBUFS * TILE;
-  // [K ring][V ring], then (dropout) one 1-KiB random-byte scratch per wave
-  __shared__ __attribute__((aligned(16))) char smem[SCRATCH + (DROPOUT ? NW * 1024 : 0)];
+  // [K ring][V ring], then (dropout) NT 1-KiB random-byte scratch blocks per wave
+  __shared__ __attribute__((aligned(16))) char smem[SCRATCH + (DROPOUT ? NW * NT * 1024 : 0)];
   auto kslot = [&](int nb) { return (nb % kFwdBufs) * TILE; };
   auto vslot = [&](int nb) { return VBASE + (nb % VBUFS) * TILE; };
 
@@ -271,8 +271,19 @@ __global__ void __launch_bounds__(FwdTile<D>::NW * 64, FwdTile<D>::MINB) fwd_ker
   // P = exp2(S c - m c) -> packed B operands; adds the partial row sum of this lane to l_run (the
   // sum is over the undropped P, as in the reference); with dropout the dropped elements of the
   // packed P are zero (reference flash_fwd_kernel.h:429-432; O is scaled by 1/keep_prob at the end)
-  char* const dscr = smem + SCRATCH + wave * 1024;
+  char* const dscr = smem + SCRATCH + wave * NT * 1024;
   const uint64_t doff = s.philox_offset + (uint64_t)(bidb * s.h + head) * 32;
+  // dropout bytes of the tile at key n0 into the wave's scratch, generated ahead of the tile's
+  // softmax while no score tile of it is live (generated inside the softmax, the Philox temporaries
+  // made the d = 128 dropout instantiations spill ~70 registers); the refit path reuses them
+  auto gen_bytes = [&](int n0) {
+    if constexpr (DROPOUT) {
+#pragma unroll
+      for (int t = 0; t < NT; ++t) dropout_block_bytes<false>(dscr + t * 1024, s.philox_seed, doff, wq0, n0 + 32 * t, lane);
+      __builtin_amdgcn_sched_barrier(0);
+    }
+    (void)n0;
+  };
   auto softmax_pack = [&](f32x16_t (&st)[NT], i16x8_t (&pf)[2 * NT], int n0) {
     const float ms = (m_run == kNegInf) ? 0.f : m_run * c;
     float ls[4] = {0.f, 0.f, 0.f, 0.f};
@@ -280,9 +291,8 @@ __global__ void __launch_bounds__(FwdTile<D>::NW * 64, FwdTile<D>::MINB) fwd_ker
     for (int t = 0; t < NT; ++t) {
       unsigned rb[4];
       if constexpr (DROPOUT) {
-        dropout_block_bytes<false>(dscr, s.philox_seed, doff, wq0, n0 + 32 * t, lane);
 #pragma unroll
-        for (int u = 0; u < 4; ++u) rb[u] = dropout_group_bytes(dscr, r, hh, u);
+        for (int u = 0; u < 4; ++u) rb[u] = dropout_group_bytes(dscr + t * 1024, r, hh, u);
       }
 #pragma unroll
       for (int g = 0; g < 16; ++g) {
@@ -306,9 +316,8 @@ __global__ void __launch_bounds__(FwdTile<D>::NW * 64, FwdTile<D>::MINB) fwd_ker
     for (int t = 0; t < NT; ++t) {
       unsigned rb[4];
       if constexpr (DROPOUT) {
-        dropout_block_bytes<false>(dscr, s.philox_seed, doff, wq0, n0 + 32 * t, lane);
 #pragma unroll
-        for (int u = 0; u < 4; ++u) rb[u] = dropout_group_bytes(dscr, r, hh, u);
+        for (int u = 0; u < 4; ++u) rb[u] = dropout_group_bytes(dscr + t * 1024, r, hh, u);
       }
       f32x16_t pt;
 #pragma unroll
@@ -381,6 +390,7 @@ __global__ void __launch_bounds__(FwdTile<D>::NW * 64, FwdTile<D>::MINB) fwd_ker
     auto body = [&](int nb, f32x16_t (&scur)[NT], f32x16_t (&snxt)[NT]) {
       if (nb + 3 < nblk) issue(nb + 3);
       i16x8_t pf[2 * NT];
+      gen_bytes(nb * BN);
       float ls = softmax_fast(scur, pf, nb * BN);
       // tile nb+1 is resident (possibly past nblk: then its scores are simply discarded); its
       // MFMAs are independent of the softmax above, so the two interleave in this basic block
@@ -399,6 +409,7 @@ __global__ void __launch_bounds__(FwdTile<D>::NW * 64, FwdTile<D>::MINB) fwd_ker
       if (nb + 3 < nblk) issue(nb + 3);
       if (nb > 0) pv(vslot(nb - 1), pfp);
       __builtin_amdgcn_sched_barrier(0);
+      gen_bytes(nb * BN);
       float ls = softmax_fast(scur, pfp, nb * BN);
       qk(kslot(nb + 1), snxt);
       if (!guard_ok(ls)) ls = refit(nb, pfp);
@@ -432,6 +443,7 @@ __global__ void __launch_bounds__(FwdTile<D>::NW * 64, FwdTile<D>::MINB) fwd_ker
     if (a3 < nblk) issue_at(a3, pos + 3);
     const bool active = (wq0 < sq) && (!CAUSAL || n0 <= wq0 + 31);
     if (active) {
+      gen_bytes(n0);
       f32x16_t st[NT];
       qk(kslot(pos), st);
 #pragma unroll
