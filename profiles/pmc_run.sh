@@ -8,7 +8,7 @@ OUT=${1:-gpurun_out/pmc}
 WL=${2:-c3}
 mkdir -p "$OUT"
 export TMPDIR=/tmp
-CMD="python3 bench.py --workload $WL --steps 3 --warmup 1 --no-cpu-baseline"
+CMD="python3 bench.py --workload $WL --steps 3 --warmup 1 --ramp-s 0 --no-cpu-baseline"
 pass() {   # name counters...
   local name=$1; shift
   timeout -k 10 180 rocprofv3 --kernel-trace --pmc "$@" -d "$OUT/$name" -o run --output-format csv -- $CMD \

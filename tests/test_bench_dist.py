@@ -80,6 +80,20 @@ def test_aggregate_tflops_is_whole_job():
     assert bench.flops_fwd(4, 8192, 16, 128, True) == pytest.approx(1.0995e12, rel=1e-4)
 
 
+def test_ramp_runs_untimed_steps_for_its_duration():
+    sys.path.insert(0, ROOT)
+    import time
+
+    import bench
+
+    calls, syncs = [], []
+    t0 = time.perf_counter()
+    n = bench.ramp(lambda: (calls.append(1), time.sleep(0.002)), 0.05, sync=lambda: syncs.append(1))
+    assert n == len(calls) > 0 and time.perf_counter() - t0 >= 0.05
+    assert syncs   # drained at least once (the last sync)
+    assert bench.ramp(lambda: calls.append(1), 0.0, sync=lambda: None) == 0
+
+
 @pytest.mark.timeout(300)
 def test_bench_gpus_flag_launches_ranks():
     """`bench.py --gpus 2` without torch.distributed.run starts the two rank processes itself and

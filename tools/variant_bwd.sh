@@ -11,7 +11,7 @@ mkdir -p "$ROOT/variants" /tmp/fa_vb/$NAME
 OBJS=""
 for f in $FILES; do
   EXTRA=""
-  case $f in fa_fwd.hip) EXTRA="-fno-slp-vectorize";; esac
+  case $f in fa_fwd.hip|fa_bwd.hip) EXTRA="-fno-slp-vectorize";; esac
   /opt/rocm/bin/hipcc -O3 -std=c++17 -fPIC --offload-arch=gfx950 -Wno-unused-result $EXTRA "$@" -x hip -c "$CS/$f" \
     -o /tmp/fa_vb/$NAME/$f.o &
   OBJS="$OBJS /tmp/fa_vb/$NAME/$f.o"

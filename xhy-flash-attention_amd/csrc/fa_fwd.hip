@@ -441,7 +441,11 @@ __global__ void __launch_bounds__(FwdTile<D>::NW * 64, FwdTile<D>::MINB) fwd_ker
     const int n0 = nb * BN;
     const int a3 = next_live(a2);
     if (a3 < nblk) issue_at(a3, pos + 3);
+#ifdef FA_ABL_NOGEN
+    const bool active = false;   // ablation (wrong results): general-path tiles not computed
+#else
     const bool active = (wq0 < sq) && (!CAUSAL || n0 <= wq0 + 31);
+#endif
     if (active) {
       gen_bytes(n0);
       f32x16_t st[NT];
