@@ -55,6 +55,12 @@ template <int D> struct DqTile {
 };
 constexpr int kDqMinBM = 128;                      // smallest dQ query block (grid-size check)
 constexpr int kBwdBufs = 3;
+#ifndef FA_DQ_STAGGER   // dev switch (A/B): staggered halves in bwd_dq_kernel
+#define FA_DQ_STAGGER 1
+#endif
+#ifndef FA_DQ_PRIO      // dev switch (A/B): waves 4-7 of bwd_dq_kernel at s_setprio 1
+#define FA_DQ_PRIO 1
+#endif
 
 // ------------------------------------------------------------------------------------------------
 // geometry shared by the kernels (reference BlockInfo, block_info.h:14-31)
@@ -801,8 +807,14 @@ __global__ void __launch_bounds__(DqTile<D>::NW * 64, DqTile<D>::MINB) bwd_dq_ke
   constexpr int PPW = (PIECES + NW - 1) / NW;
   constexpr int KG = (KS % 4 == 0) ? 4 : ((KS % 3 == 0) ? 3 : 2);
   static_assert(TILE % 1024 == 0 && KS % KG == 0, "tile shape");
+  // Staggered halves (8-wave workgroups, as in fwd_kernel): waves 4-7 run the dQ MFMAs of each tile
+  // one step late, so on every SIMD one wave opens its step with the S / dP MFMAs while its partner
+  // opens with the dQ MFMAs of the previous tile and then the dS VALU.  The late dQ reads K(nb-1)
+  // while tile nb+2 lands, hence a 4-deep ring.
+  constexpr bool STAGGER = NW == 8 && FA_DQ_STAGGER;
+  constexpr int BUFS = STAGGER ? 4 : kBwdBufs;
   // [buffer][K | V], then (dropout) NT 1-KiB random-byte scratch blocks per wave
-  __shared__ __attribute__((aligned(16))) char smem[kBwdBufs * 2 * TILE + (DROPOUT ? NW * NT * 1024 : 0)];
+  __shared__ __attribute__((aligned(16))) char smem[BUFS * 2 * TILE + (DROPOUT ? NW * NT * 1024 : 0)];
 
   const AttnShape s = p.s;
   const uint64_t pseed = DROPOUT ? philox_seed_of(s) : 0, poff = DROPOUT ? philox_offset_of(s) : 0;
@@ -866,7 +878,7 @@ __global__ void __launch_bounds__(DqTile<D>::NW * 64, DqTile<D>::MINB) bwd_dq_ke
   // K/V tile `nb` into ring position `pos` (the same except when FlashMask skips tiles)
   auto issue_at = [&](int nb, int pos) {
     const int n0 = nb * BN;
-    char* dst = smem + (pos % kBwdBufs) * 2 * TILE;
+    char* dst = smem + (pos % BUFS) * 2 * TILE;
     const buf_rsrc_t rk = make_rsrc(K + (int64_t)n0 * p.k_row, rec_bytes(sk - n0, p.k_row, 2));
     const buf_rsrc_t rv = make_rsrc(V + (int64_t)n0 * p.v_row, rec_bytes(sk - n0, p.v_row, 2));
 #pragma unroll
@@ -885,15 +897,16 @@ __global__ void __launch_bounds__(DqTile<D>::NW * 64, DqTile<D>::MINB) bwd_dq_ke
 #pragma unroll
     for (int g = 0; g < 16; ++g) dq[t][g] = 0.f;
 
-  auto tile = [&](auto MASKC, int nb, int pos) {
+  // S^T, dP^T and dS^T of tile nb (ring position pos), packed to df (the B operands of dQ^T)
+  auto sdp = [&](auto MASKC, int nb, int pos, i16x8_t (&df)[2 * NT]) {
     constexpr bool MASK = decltype(MASKC)::value;
     const int n0 = nb * BN;
-    const int kt = (pos % kBwdBufs) * 2 * TILE;
+    const int kt = (pos % BUFS) * 2 * TILE;
     const TileAddr tk(lb, kt), tv(lb, kt + TILE);
     // dropout bytes of the tile's NT 32x32 blocks, generated before the S / dP chains (the Philox
     // temporaries then never overlap the live score tiles: generated inside the dS loop they made
     // the causal dropout instantiation spill ~140 registers)
-    char* const dscr = smem + kBwdBufs * 2 * TILE + wave * NT * 1024;
+    char* const dscr = smem + BUFS * 2 * TILE + wave * NT * 1024;
     if constexpr (DROPOUT) {
       const uint64_t doff = poff + (uint64_t)bhi * 32;
 #pragma unroll
@@ -987,13 +1000,15 @@ __global__ void __launch_bounds__(DqTile<D>::NW * 64, DqTile<D>::MINB) bwd_dq_ke
           pt[t][g] = pv * pt[t][g];
       }
     }
-    // dQ^T[d][q] += K^T[d][key] dS^T[key][q]
-    i16x8_t df[2 * NT];
 #pragma unroll
     for (int t = 0; t < NT; ++t) {
       df[2 * t] = pack_frag<BF16>(pt[t], 0);
       df[2 * t + 1] = pack_frag<BF16>(pt[t], 1);
     }
+  };
+  // dQ^T[d][q] += K^T[d][key] dS^T[key][q] with K^T from the tile at ring position pos
+  auto dq_mma = [&](int pos, const i16x8_t (&df)[2 * NT]) {
+    const TileAddr tk(lb, (pos % BUFS) * 2 * TILE);
     static_for<0, NP>([&](auto DTC) {
       constexpr int dt = decltype(DTC)::value;
       i16x8_t a[2 * NT];
@@ -1004,6 +1019,11 @@ __global__ void __launch_bounds__(DqTile<D>::NW * 64, DqTile<D>::MINB) bwd_dq_ke
 #pragma unroll
       for (int kk = 0; kk < 2 * NT; ++kk) dq[dt] = E::mfma(a[kk], df[kk], dq[dt]);
     });
+  };
+  auto tile = [&](auto MASKC, int nb, int pos) {
+    i16x8_t df[2 * NT];
+    sdp(MASKC, nb, pos, df);
+    dq_mma(pos, df);
   };
 
   int ndma = 0;   // DMA operations one issue() leaves outstanding in this wave
@@ -1025,10 +1045,25 @@ __global__ void __launch_bounds__(DqTile<D>::NW * 64, DqTile<D>::MINB) bwd_dq_ke
   wait_vmem_all();   // Q / dO fragments, LSE / D and tile 0 (compiler-visible)
   if (tq1 < nblk) issue_at(tq1, 1);
   lds_barrier();
-  for (int nb = 0; nb < nfast; ++nb) {
-    if (nb + 2 < nblk) issue_at(nb + 2, nb + 2);
-    tile(std::false_type{}, nb, nb);
-    wait_dma_keep_and_barrier(nb + 2 < nblk ? ndma : 0);
+  if (STAGGER && FA_DQ_PRIO && wave >= NW / 2) __builtin_amdgcn_s_setprio(1);
+  if (!STAGGER || wave < NW / 2) {
+    for (int nb = 0; nb < nfast; ++nb) {
+      if (nb + 2 < nblk) issue_at(nb + 2, nb + 2);
+      tile(std::false_type{}, nb, nb);
+      wait_dma_keep_and_barrier(nb + 2 < nblk ? ndma : 0);
+    }
+  } else if (nfast > 0) {
+    // late half: dQ of tile nb-1 (its dS^T carried across the barrier in dfp), then S / dP / dS of nb
+    i16x8_t dfp[2 * NT];
+    for (int nb = 0; nb < nfast; ++nb) {
+      if (nb + 2 < nblk) issue_at(nb + 2, nb + 2);
+      if (nb > 0) dq_mma(nb - 1, dfp);
+      __builtin_amdgcn_sched_barrier(0);
+      sdp(std::false_type{}, nb, nb, dfp);
+      wait_dma_keep_and_barrier(nb + 2 < nblk ? ndma : 0);
+    }
+    // the last deferred dQ: K(nfast-1) stays resident until the general path issues tile nfast+3
+    dq_mma(nfast - 1, dfp);
   }
   // ring position pos holds tile nb; a1 is the next live tile (already in flight)
   int nb = MASKED ? tq0 : nfast, a1 = MASKED ? tq1 : nfast + 1;
