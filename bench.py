@@ -51,6 +51,9 @@ WORKLOADS = {
     "c3": (4, 8192, 16, 16, 128, "bf16", True, "fwd_bwd"),     # configs[2]: headline
     "c4": (None, 65536, 32, 32, 128, "bf16", True, "varlen"),  # configs[3]: total tokens
     "c5": (8, 32768, 32, 8, 128, "fp16", True, "fwd_bwd"),     # configs[4]: 8 per GPU
+    # dev shapes (not BASELINE configs): head dim 64 at the C3 length, causal and not
+    "d64": (4, 8192, 32, 32, 64, "bf16", True, "fwd_bwd"),
+    "d64nc": (4, 8192, 32, 32, 64, "bf16", False, "fwd_bwd"),
 }
 
 

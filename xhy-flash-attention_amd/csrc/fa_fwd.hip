@@ -42,8 +42,11 @@ namespace fa {
 // d in (128, 256]: the O accumulator (D/2 registers) and the Q fragments (D/4) no longer fit two
 // waves per SIMD next to the scores, so a workgroup is 4 waves (one per SIMD, 512 registers each)
 // and K/V tiles are 32 keys (the 4-deep ring stays at 4 x 2 x 16 KiB at d = 256).
+#ifndef FA_FWD_NW64   // dev switch (A/B): waves per workgroup at head dims <= 64
+#define FA_FWD_NW64 8
+#endif
 template <int D> struct FwdTile {
-  static constexpr int NW = D <= 128 ? 8 : 4;
+  static constexpr int NW = D <= 64 ? FA_FWD_NW64 : (D <= 128 ? 8 : 4);
   static constexpr int BM = 32 * NW;
   static constexpr int BN = D <= 128 ? 64 : 32;
   static constexpr int MINB = D <= 128 ? 2 : 1;   // __launch_bounds__ blocks per CU (register budget)
@@ -635,8 +638,7 @@ template <bool BF16, int D, bool CAUSAL, bool DROPOUT>
 static void run_fwd(const FwdParams& p, hipStream_t stream) {
   dim3 grid(p.s.b * p.s.h * p.num_m_blocks);   // 1-D: heads fastest, heaviest query block first
   prof_begin(kTimeFwd, stream);
-  if constexpr (!DROPOUT && (D == 64 || D == 128)) {
-    static_assert(FwdTile<D>::BM == 256, "fwd_kernel_w4 covers the same 256-row blocks");
+  if constexpr (!DROPOUT && (D == 64 || D == 128) && FwdTile<D>::BM == 256) {   // the same 256-row blocks
     if (launch_fwd_w4(p, BF16, stream)) {   // 4 waves x 64 rows (fa_fwd_w4.hip)
       prof_end(kTimeFwd, stream);
       return;
@@ -686,8 +688,8 @@ static void dispatch_fwd(const FwdParams& p, hipStream_t stream) {
 }
 
 void fwd_block_size(int d, int* block_m, int* block_n) {
-  *block_m = d <= 128 ? FwdTile<128>::BM : FwdTile<256>::BM;
-  *block_n = d <= 128 ? FwdTile<128>::BN : FwdTile<256>::BN;
+  *block_m = d <= 64 ? FwdTile<64>::BM : (d <= 128 ? FwdTile<128>::BM : FwdTile<256>::BM);
+  *block_n = d <= 64 ? FwdTile<64>::BN : (d <= 128 ? FwdTile<128>::BN : FwdTile<256>::BN);
 }
 
 void launch_fwd(const FwdParams& p_in, bool is_bf16, hipStream_t stream) {
