@@ -26,6 +26,7 @@ import ctypes
 import json
 import os
 import socket
+import statistics
 import subprocess
 import sys
 import time
@@ -185,10 +186,12 @@ def max_over_ranks(x, world, device=None):
     return float(t.item())
 
 
-def timed(step, steps, warmup, world, sync=None, on_start=None, on_stop=None):
+def timed(step, steps, warmup, world, sync=None, on_start=None, on_stop=None, step_ms=None):
     """W untimed steps, then EXACTLY `steps` steps bracketed by barrier + synchronize on every
     rank; returns the MAX elapsed seconds over ranks.  on_start / on_stop run right inside the
-    bracket (the kernel timer: its windows then cover the timed steps only)."""
+    bracket (the kernel timer: its windows then cover the timed steps only).  `step_ms` (a list)
+    receives this rank's per-step device times from events recorded between the steps on the
+    current stream (median and min next to the mean)."""
     if sync is None:
         import torch
         sync = torch.cuda.synchronize
@@ -196,15 +199,25 @@ def timed(step, steps, warmup, world, sync=None, on_start=None, on_stop=None):
         step()
     barrier(world)
     sync()
+    ev = None
+    if step_ms is not None:
+        import torch
+        ev = [torch.cuda.Event(enable_timing=True) for _ in range(steps + 1)]
     if on_start:
         on_start()
     t0 = time.perf_counter()
-    for _ in range(steps):
+    for i in range(steps):
+        if ev is not None:
+            ev[i].record()
         step()
+    if ev is not None:
+        ev[steps].record()
     sync()
     t1 = time.perf_counter()
     if on_stop:
         on_stop()
+    if ev is not None:
+        step_ms.extend(ev[i].elapsed_time(ev[i + 1]) for i in range(steps))
     barrier(world)
     return max_over_ranks(t1 - t0, world)
 
@@ -397,7 +410,9 @@ def main():
     # forward-only leg (the north_star's >= 50%-of-peak target is quoted on the forward)
     t_fwd = timed(fwd_only, args.steps, args.warmup, world)
     # headline leg, with live per-kernel event timing over the timed steps only
-    t_step = timed(headline_step, args.steps, args.warmup, world, on_start=timer.start, on_stop=timer.stop)
+    step_ms = []
+    t_step = timed(headline_step, args.steps, args.warmup, world, on_start=timer.start, on_stop=timer.stop,
+                   step_ms=step_ms)
     kt = timer.result
     ms_per_step = t_step / args.steps * 1e3
     windows_per_step = sum(x["total_ms"] for x in kt.values()) / args.steps
@@ -453,6 +468,8 @@ def main():
             "steps": args.steps,
             "warmup": args.warmup,
             "ms_per_step": round(ms_per_step, 4),
+            "ms_per_step_median": round(statistics.median(step_ms), 4) if step_ms else None,
+            "ms_per_step_min": round(min(step_ms), 4) if step_ms else None,
             "higher_is_better": True,
             "scaling": "weak",
             "vs_baseline": round(value / world / H100_FWD_BWD_TFLOPS, 4) if args.workload == "c3" else None,
