@@ -94,6 +94,9 @@ def parse(argv=None):
                     help="CPU-baseline threads (0: the affinity set, capped by OMP_NUM_THREADS)")
     ap.add_argument("--pmc", default=os.path.join(ROOT, "profiles", "pmc.json"),
                     help="JSON with rocprof PMC figures per workload and kernel (profiles/pmc.py)")
+    ap.add_argument("--rank-timeout", type=float, default=None,
+                    help="--gpus N launcher: seconds before every rank is terminated and the launcher exits "
+                         "non-zero (default 900 + 5 s per warm-up / timed step)")
     ap.add_argument("--dry-run", action="store_true",
                     help="harness only (gloo, CPU sleep as the step): tests the launcher and timing")
     return ap.parse_args(argv)
@@ -378,7 +381,10 @@ def main():
     world_env = os.environ.get("WORLD_SIZE")
     if args.gpus > 1 and world_env is None:
         # launcher: no torch / GPU call has happened in this process
-        sys.exit(launch_ranks(args.gpus, sys.argv[1:]))
+        # a rank that hangs (e.g. in RCCL init) must not hang the launcher: bounded wait, then every
+        # child is terminated and the launcher exits non-zero (124)
+        limit = args.rank_timeout if args.rank_timeout is not None else 900.0 + 5.0 * (args.steps + args.warmup)
+        sys.exit(launch_ranks(args.gpus, sys.argv[1:], timeout=limit))
 
     import torch
 
@@ -387,6 +393,9 @@ def main():
         raise SystemExit(f"bench.py: --gpus {args.gpus} but the process group has {world} ranks")
 
     if args.dry_run:
+        hang = os.environ.get("FA_BENCH_DRYRUN_HANG_RANK")   # test hook: this rank never reaches the barrier
+        if hang is not None and int(hang) == rank:
+            time.sleep(3600)
         t = timed(lambda: time.sleep(0.005), args.steps, args.warmup, world, sync=lambda: None)
         if rank == 0:
             print(json.dumps({"dry_run": True, "n_gpus": world, "steps": args.steps,

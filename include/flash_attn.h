@@ -25,8 +25,8 @@
  *     attn_mask[b][h % mask_dims[1]][q % mask_dims[2]][k] * softmax_unscale
  *     added before the softmax scale (reference flash_fwd_kernel.h:640-660,
  *     softmax.h:361-379); mask_dims = {batch, head modulus, row modulus,
- *     seqlen_k} (host int64[4], reference flash_attn.cu:623-624); not combined
- *     with return_softmax;
+ *     seqlen_k} (host int64[4], reference flash_attn.cu:623-624); with
+ *     return_softmax the S_dmask probabilities include the mask;
  *   - FlashMask (flash_attn_fwd / flash_attn_bwd*, not varlen, reference
  *     flash_attn.cu:204-209): active iff flashmask_downstart_ptr != NULL.
  *     int32 row bounds of shape (batch, flashmask_dims[1], seqlen_k) each;
@@ -36,8 +36,9 @@
  *     [upstart, upend) when upstart is given, else rows >= downstart or
  *     < upend; upend is required (reference softmax.h:180-298).  Pass the same
  *     pointers to the backward.  flashmask_maxmin_ptr (the reference's
- *     tile-scan scratch) is accepted and not used.  Not combined with attn_mask
- *     or return_softmax.  Rows that see no key give out = 0, LSE = +inf;
+ *     tile-scan scratch) is accepted and not used.  Not combined with attn_mask;
+ *     with return_softmax the S_dmask zeroes the hidden entries.  Rows that see
+ *     no key give out = 0, LSE = +inf;
  *   - backward: softmax_d (b, h, seqlen_q_rounded) fp32 is a caller-owned
  *     output (D = rowsum(dO * O)); dq_accum is caller-owned fp32 SCRATCH of at
  *     least batch * num_heads * seqlen_q_rounded floats (the reference's

@@ -110,6 +110,24 @@ def test_bench_gpus_flag_launches_ranks():
     assert len(lines) == 1 and lines[0]["n_gpus"] == 2 and lines[0]["steps"] == 3
 
 
+@pytest.mark.timeout(240)
+def test_bench_launcher_times_out_a_hung_rank():
+    """A rank that never reaches the barrier (FA_BENCH_DRYRUN_HANG_RANK) does not hang the launcher:
+    after --rank-timeout every child is terminated and bench.py exits non-zero (124) within it."""
+    import subprocess
+
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    env["FA_BENCH_DRYRUN_HANG_RANK"] = "1"
+    limit = 40.0
+    t0 = time.time()
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--dry-run",
+                        "--no-cpu-baseline", "--steps", "3", "--warmup", "1", "--rank-timeout", str(limit)],
+                       capture_output=True, text=True, env=env, timeout=200)
+    elapsed = time.time() - t0
+    assert r.returncode == 124, (r.returncode, r.stderr[-2000:])
+    assert elapsed < limit + 35, elapsed   # terminate + join of the children after the limit
+
+
 @pytest.mark.timeout(120)
 def test_bench_world_mismatch_is_an_error():
     """A process group whose size differs from --gpus is refused (no silent 1-GPU timing)."""

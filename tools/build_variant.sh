@@ -10,6 +10,7 @@ SCR=/tmp/fa_variant_$NAME
 rm -rf "$SCR"; mkdir -p "$SCR/pkg/csrc" "$SCR/include" "$ROOT/variants"
 if [ "$REV" = "-" ]; then
   cp "$ROOT"/xhy-flash-attention_amd/csrc/*.* "$ROOT"/xhy-flash-attention_amd/csrc/Makefile "$SCR/pkg/csrc/"
+  cp -r "$ROOT"/xhy-flash-attention_amd/csrc/asm "$SCR/pkg/csrc/"
   cp "$ROOT"/include/* "$SCR/include/"
 else
   (cd "$ROOT" && git archive "$REV" xhy-flash-attention_amd/csrc include) | tar -x -C "$SCR"

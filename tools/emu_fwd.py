@@ -1,0 +1,127 @@
+#!/usr/bin/env python3
+"""Runs the generated assembly forward (csrc/asm/gen_fwd.py) in the CPU emulator (tools/asm_emu.py)
+on small inputs and compares O / LSE with a float64 reference (dev / test tool).
+
+    python tools/emu_fwd.py [--b 1 --sq 300 --sk 300 --h 2 --hk 1 --causal --fp16 --varlen 100,250]
+"""
+import argparse
+import os
+import struct
+import subprocess
+import sys
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "tools"))
+from asm_emu import Emu, Heap, bf16_to_f32, f16_to_f32, f32_to_bf16, f32_to_f16  # noqa: E402
+
+GEN = os.path.join(ROOT, "xhy-flash-attention_amd", "csrc", "asm", "gen_fwd.py")
+D = 128
+BM = 256
+
+
+def asm_text():
+    return subprocess.run([sys.executable, GEN], check=True, capture_output=True, text=True).stdout
+
+
+def sched_table(b, h, hk, nmb):
+    nbh = b * h
+    tab = np.zeros((nbh * nmb, 2), dtype=np.uint32)
+    for L in range(nbh * nmb):
+        m_idx, bh = divmod(L, nbh)
+        mb = nmb - 1 - m_idx
+        bidb, head = divmod(bh, h)
+        kvh = head // (h // hk)
+        tab[L] = (bidb | (head << 16), kvh | (mb << 16))
+    return tab
+
+
+def pack_args(**kw):
+    head = struct.pack("<11Q4q", kw["q"], kw["k"], kw["v"], kw["o"], kw["lse"], kw["sched"], kw["cuq"], kw["cuk"],
+                       kw["rng"], kw["seed"], kw["off"], kw["q_batch"], kw["k_batch"], kw["v_batch"], kw["o_batch"])
+    assert len(head) == 120
+    tail = struct.pack("<11i", kw["q_row"], kw["kv_row"], kw["o_row"], kw["q_head"], kw["k_head"], kw["v_head"],
+                       kw["o_head"], kw["sq"], kw["sk"], kw["lse_pitch"], kw["h"])
+    tail += struct.pack("<fii", kw["c"], kw["flags"], 0)
+    out = head + tail
+    assert len(out) == 176, len(out)
+    return out
+
+
+def reference(q, k, v, causal, scale, seqs_q=None, seqs_k=None):
+    """float64 attention; q (b, sq, h, d), k/v (b, sk, hk, d); returns o, lse (b, h, sq)"""
+    b, sq, h, d = q.shape
+    sk, hk = k.shape[1], k.shape[2]
+    g = h // hk
+    o = np.zeros((b, sq, h, d))
+    lse = np.full((b, h, sq), np.inf)
+    for bi in range(b):
+        lq = seqs_q[bi] if seqs_q is not None else sq
+        lk = seqs_k[bi] if seqs_k is not None else sk
+        for hi in range(h):
+            s = q[bi, :lq, hi].astype(np.float64) @ k[bi, :lk, hi // g].astype(np.float64).T * scale
+            if causal:
+                s = np.where(np.arange(lk)[None, :] > np.arange(lq)[:, None], -np.inf, s)
+            m = s.max(axis=1, keepdims=True)
+            p = np.exp(s - m)
+            l = p.sum(axis=1, keepdims=True)
+            o[bi, :lq, hi] = (p / l) @ v[bi, :lk, hi // g]
+            lse[bi, hi, :lq] = (m + np.log(l))[:, 0]
+    return o, lse
+
+
+def run(b=1, sq=300, sk=300, h=2, hk=1, causal=True, bf16=True, seed=0, big=None, text=None, verbose=True):
+    rng = np.random.default_rng(seed)
+    q = rng.standard_normal((b, sq, h, D)).astype(np.float32)
+    k = rng.standard_normal((b, sk, hk, D)).astype(np.float32)
+    v = rng.standard_normal((b, sk, hk, D)).astype(np.float32)
+    if big is not None:   # a late score jump: forces the refit path
+        q[:, :, :, :] *= 0.3
+        k[:, big:big + 3] *= 12.0
+    enc, dec = (f32_to_bf16, bf16_to_f32) if bf16 else (f32_to_f16, f16_to_f32)
+    q16, k16, v16 = (enc(x).astype(np.uint16) for x in (q, k, v))
+    qf, kf, vf = (dec(x).astype(np.float64) for x in (q16, k16, v16))
+    scale = D ** -0.5
+    heap = Heap(64 << 20)
+    aq, ak, av = heap.put(q16), heap.put(k16), heap.put(v16)
+    ao = heap.alloc(b * sq * h * D * 2)
+    heap.get(ao, b * sq * h * D * 2)[:] = 0xAB   # poison
+    alse = heap.alloc(b * h * sq * 4)
+    nmb = (sq + BM - 1) // BM
+    tab = sched_table(b, h, hk, nmb)
+    asch = heap.put(tab)
+    kw = dict(q=aq, k=ak, v=av, o=ao, lse=alse, sched=asch, cuq=0, cuk=0, rng=0, seed=0, off=0,
+              q_batch=sq * h * D * 2, k_batch=sk * hk * D * 2, v_batch=sk * hk * D * 2, o_batch=sq * h * D * 2,
+              q_row=h * D * 2, kv_row=hk * D * 2, o_row=h * D * 2, q_head=D * 2, k_head=D * 2, v_head=D * 2,
+              o_head=D * 2, sq=sq, sk=sk, lse_pitch=sq, h=h, c=float(np.float32(scale * 1.4426950408889634)), flags=0)
+    akarg = heap.put(np.frombuffer(pack_args(**kw), dtype=np.uint8))
+    text = text or asm_text()
+    name = f"fa_fwd_asm_d128_{'bf16' if bf16 else 'f16'}_{'causal' if causal else 'full'}"
+    emu = Emu(text, name, heap)
+    for L in range(len(tab)):
+        emu.run_wg(L, akarg)
+    o = dec(heap.get(ao, b * sq * h * D * 2).view(np.uint16)).reshape(b, sq, h, D).astype(np.float64)
+    lse = heap.get(alse, b * h * sq * 4).view(np.float32).reshape(b, h, sq).astype(np.float64)
+    o_ref, lse_ref = reference(qf, kf, vf, causal, scale)
+    eo = np.abs(o - o_ref).max()
+    el = np.abs(lse - lse_ref).max()
+    if verbose:
+        print(f"b={b} sq={sq} sk={sk} h={h} hk={hk} causal={causal} bf16={bf16}: max|dO| {eo:.3e} max|dLSE| {el:.3e}"
+              f"  ({emu.count} instructions, {emu.mfma_count} MFMAs)")
+    return eo, el, o, o_ref, lse, lse_ref
+
+
+if __name__ == "__main__":
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--b", type=int, default=1)
+    ap.add_argument("--sq", type=int, default=300)
+    ap.add_argument("--sk", type=int, default=300)
+    ap.add_argument("--h", type=int, default=2)
+    ap.add_argument("--hk", type=int, default=1)
+    ap.add_argument("--full", action="store_true")
+    ap.add_argument("--fp16", action="store_true")
+    ap.add_argument("--big", type=int, default=None)
+    ap.add_argument("--seed", type=int, default=0)
+    a = ap.parse_args()
+    run(a.b, a.sq, a.sk, a.h, a.hk, not a.full, not a.fp16, a.seed, a.big)

@@ -1,0 +1,900 @@
+#!/usr/bin/env python3
+"""Generates fa_fwd_asm.s: the gfx950 FlashAttention-2 forward for head dim 128, written as a
+hand-scheduled assembly kernel (one wave per SIMD).
+
+    python3 gen_fwd.py > fa_fwd_asm.s
+
+Algorithm: the reference's compute_attn_1rowblock (csrc/flash_attn/src/flash_fwd_kernel.h:121-583):
+per (query block, batch, head) stream K/V tiles, S = Q K^T, online softmax with running max / sum,
+O += P V, epilogue O /= l, LSE = m * scale + ln l (+inf when l == 0 or NaN, :509-518), causal mask
+top-left (key <= query, softmax.h:143-178).
+
+MI355X structure (MI355X_MICROARCH.md "one wave per SIMD"; cdna_hip_programming.md "4-wave,
+one-wave-per-SIMD" attention structure):
+  * workgroup = 4 waves x 64 query rows = a 256-row query block; every wave owns two 32-row query
+    blocks a (rows 64w..64w+31) and b (+32) and the whole 512-entry register file:
+      a[0:127]   O^T accumulators (2 q-blocks x 4 d-tiles x 16)
+      a[128:191] Q fragments (B operands of S^T = K Q^T), loaded once
+      a[192:223] K fragment ring (8 x 4), a[224:255] V fragment ring (8 x 4)
+      v[0:143]   S^T tiles (a: 32, b: 2 x 32) and packed P fragments (a: 2 x 16, b: 16)
+  * K/V tiles of 64 keys arrive by LDS-DMA (buffer_load_dwordx4 ... lds, 1 KiB per instruction,
+    range-checked descriptors zero-fill keys past seqlen_k) into a 5-deep ring of K and V slots
+    (5 x 32 KiB = the whole 160 KiB LDS); tile n+4 is issued during step n, so every tile has about
+    three steps to land.  One s_waitcnt vmcnt + s_barrier per step.
+  * step n = two phases of 32 MFMAs (v_mfma_f32_32x32x16), each carrying one q-block's softmax in
+    its gaps:  phase X: S(n+1, a), S(n+1, b) = K(n+1) Q^T  ||  P(n, b) = exp2(c S(n, b) - c m_b)
+               phase Y: O_a, O_b += V(n)^T P(n)            ||  P(n+1, a)
+    Each K fragment (ds_read_b128) and V fragment (2 x ds_read_b64_tr_b16) feeds two MFMAs (q-blocks
+    a and b).  The filler instructions are placed into the MFMA gaps by isa.schedule (issue budget
+    per 32-cycle gap), the wait states by isa.fix_hazards, the counted lgkmcnt waits by isa.add_waits.
+  * max-free online softmax: P = exp2(c S - c m_run) against the running max of the first tile; a
+    tile whose per-lane partial row sum exceeds 2^8 (or is NaN) is recomputed with the true max
+    ("refit", out of line, rare); the deferred-max rule of fa_fwd.hip.
+  * tiles that need a mask (causal diagonal, ragged last tile) run a MASKED step variant that sets
+    the masked scores to -inf before the exponent (per lane limit min(q, sk-1) - key base).
+  * work order comes from a host-built table (block -> batch, head, kv head, query block): heaviest
+    causal blocks first, heads fastest, as the HIP kernel's xcd_order_grouped.
+"""
+import os
+import sys
+
+sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+from isa import (ACCR, ACCW, BARRIER, BRANCH, DMA, LABEL, LDS, MFMA, NOP, PERM, SALU, SMEM, SOPP,  # noqa: E402
+                 TRANS, VALU, VLOAD, VSTORE, WAIT, Counters, Inst, add_waits, ar, fix_hazards, label, nop,
+                 rtxt, schedule, sr, vr)
+
+D = 128
+KS = D // 16          # QK^T k-steps
+NP = D // 32          # d tiles of O
+BN = 64               # keys per K/V tile
+BM = 256              # query rows per workgroup
+TILE = BN * D * 2     # bytes per K (or V) tile
+NSLOT = 5
+VBASE = NSLOT * TILE
+LDS_BYTES = 2 * NSLOT * TILE
+assert LDS_BYTES <= 163840
+
+# ---- AGPRs ----
+def O_(j, dt):
+    return 64 * j + 16 * dt
+
+
+def Q_(j, ks):
+    return 128 + 32 * j + 4 * ks
+
+
+KF = 192
+VF = 224
+
+# ---- VGPRs ----
+SA = 0
+
+
+def SB(p):
+    return 32 + 32 * p
+
+
+def PA(p):
+    return 96 + 16 * p
+
+
+PB = 128
+V_RB0, V_RB1, V_TB0, V_TB1 = 144, 145, 146, 147        # lane LDS bases (no slot)
+V_KB0, V_KB1, V_VB0, V_VB1 = 148, 149, 150, 151        # current K / V read bases
+V_VOFF = 152                                             # 4 DMA voffsets (152..155)
+V_NEGMC = (156, 157)                                     # -m*c per q-block
+V_L = (158, 159)                                         # running row sums (this lane's keys)
+V_PS = (160, 161)                                        # partial sums of the current tile
+V_LB = (162, 163)                                        # mask limit bases
+V_LM = (164, 165)                                        # mask limits of the current tile (st 0, 1)
+V_NINF = 166
+V_T = 167                                                # temps 167..183
+V_QOFF = (184, 185)                                      # Q / O row offsets per q-block
+V_LSEOFF = (186, 187)
+V_LANE = 188
+V_OOFF = (189, 190)
+NVGPR = 192
+
+# ---- SGPRs ----
+S_KD, S_VD, S_QD, S_OD, S_LD = 4, 8, 12, 16, 20          # buffer descriptors
+S_C = 24
+S_N = 25          # step n
+S_N0 = 26         # 64 n
+S_NF2 = 27        # nfast - 2
+S_NL1 = 28        # nblk - 1
+S_KOFF = 29       # K slot offset of the tile phase X reads
+S_VOFF = 30       # V slot offset (incl. VBASE) of the tile phase Y reads
+S_DOFF = 31       # K slot offset of the next DMA tile + wave * 1024
+S_TB = 32         # tile bytes = 64 * kv_row
+S_DT = 33         # index of the next DMA tile
+S_NBLK = 34
+S_WAVE = 35
+S_TMP = 36        # 36..39 temps
+S_KA = 40         # kernarg block 40..83
+S_RNGD = 92       # rng_state store descriptor (92..95), written once
+NSGPR = 100
+
+KARG_SIZE = 176
+
+# dev A/B switches, read when the .s is generated (tools/asm_variant.sh)
+OPT_NOZERO = os.environ.get("FA_GEN_NOZERO") == "1"          # never zero K/V record counts
+OPT_ZERO_NOP = int(os.environ.get("FA_GEN_ZERO_NOP", "0"))    # s_nop 15 x N before zeroing them
+
+
+class K:
+    """one kernel variant"""
+
+    def __init__(self, bf16, causal):
+        self.bf16 = bf16
+        self.causal = causal
+        self.ty = "bf16" if bf16 else "f16"
+        self.name = f"fa_fwd_asm_d{D}_{self.ty}_{'causal' if causal else 'full'}"
+        self.lines = []
+        self.uid = 0
+
+    def lab(self, s):
+        self.uid += 1
+        return f".L{self.name}_{s}_{self.uid}"
+
+    # ------------------------------------------------------------------ instruction builders
+    def mfma_s(self, st_reg, kslot, j, ks, first):
+        c = "0" if first else rtxt("v", st_reg, 16)
+        t = (f"v_mfma_f32_32x32x16_{self.ty} {rtxt('v', st_reg, 16)}, {rtxt('a', KF + 4 * kslot, 4)}, "
+             f"{rtxt('a', Q_(j, ks), 4)}, {c}")
+        rd = ar(KF + 4 * kslot, 4) + ar(Q_(j, ks), 4) + ([] if first else vr(st_reg, 16))
+        return Inst(t, MFMA, rd=rd, wr=vr(st_reg, 16), rd_c=[] if first else vr(st_reg, 16))
+
+    def mfma_o(self, j, dt, vslot, preg):
+        o = O_(j, dt)
+        t = (f"v_mfma_f32_32x32x16_{self.ty} {rtxt('a', o, 16)}, {rtxt('a', VF + 4 * vslot, 4)}, "
+             f"{rtxt('v', preg, 4)}, {rtxt('a', o, 16)}")
+        return Inst(t, MFMA, rd=ar(VF + 4 * vslot, 4) + vr(preg, 4) + ar(o, 16), wr=ar(o, 16), rd_c=ar(o, 16))
+
+    def kread(self, f, kslot, **kw):
+        st, ks = f // 8, f % 8
+        base = V_KB0 if ks % 2 == 0 else V_KB1
+        off = (ks // 2) * BN * 64 + st * 32 * 64
+        return Inst(f"ds_read_b128 {rtxt('a', KF + 4 * kslot, 4)}, v{base} offset:{off}", LDS,
+                    rd=vr(base), wr=ar(KF + 4 * kslot, 4), **kw)
+
+    def vread(self, f, vslot, half, **kw):
+        dt, kk = f // 4, f % 4
+        base = V_VB0 if half == 0 else V_VB1
+        off = dt * BN * 64 + kk * 16 * 64 + half * 8 * 64
+        dst = VF + 4 * vslot + 2 * half
+        return Inst(f"ds_read_b64_tr_b16 {rtxt('a', dst, 2)}, v{base} offset:{off}", LDS,
+                    rd=vr(base), wr=ar(dst, 2), **kw)
+
+    def cvt(self, dst, s0, s1, **kw):
+        return Inst(f"v_cvt_pk_{self.ty}_f32 v{dst}, v{s0}, v{s1}", VALU, rd=vr(s0) + vr(s1), wr=vr(dst), **kw)
+
+    # ------------------------------------------------------------------ softmax op lists
+    def mask_ops(self, j, sreg, kbase_sgpr_add, lm, key0=0):
+        """scores of q-block j at v[sreg..+31] whose key exceeds the lane limit become -inf.  The limit
+        of subtile st (32 keys) is V_LB[j] - key base - 32 st, kept in v[lm[st]]; element g of a lane
+        holds key base + acc_row(g, hh), masked iff (g & 3) + 8 (g >> 2) > V_LB - base (V_LB already
+        holds min(q, sk - 1) - 4 hh).  kbase_sgpr_add: key base = sgpr + add."""
+        ops = []
+        sg, add = kbase_sgpr_add
+        ops.append(Inst(f"v_subrev_u32 v{lm[0]}, s{sg}, v{V_LB[j]}", VALU, rd=sr(sg) + vr(V_LB[j]), wr=vr(lm[0]), key=key0))
+        if add:
+            ops.append(Inst(f"v_subrev_u32 v{lm[0]}, {add}, v{lm[0]}", VALU, rd=vr(lm[0]), wr=vr(lm[0]), key=key0))
+        ops.append(Inst(f"v_subrev_u32 v{lm[1]}, 32, v{lm[0]}", VALU, rd=vr(lm[0]), wr=vr(lm[1]), key=key0))
+        for e in range(32):
+            st, g = e // 16, e % 16
+            reg = sreg + e
+            const = (g & 3) + 8 * (g >> 2)
+            ops.append(Inst(f"v_cmp_gt_i32_e32 vcc, {const}, v{lm[st]}", VALU, rd=vr(lm[st]), wr=[("vcc", 0)], key=key0 + 4 * e))
+            ops.append(Inst(f"v_cndmask_b32_e32 v{reg}, v{reg}, v{V_NINF}, vcc", VALU,
+                            rd=vr(reg) + vr(V_NINF) + [("vcc", 0)], wr=vr(reg), key=key0 + 4 * e))
+        return ops
+
+    def softmax_ops(self, j, sreg, preg, masked, kbase_sgpr_add, key0, lm=None):
+        """ops of P = exp2(c S - c m) for q-block j on the 32 scores at v[sreg..+31] -> packed P at
+        v[preg..+15]; partial row sum into V_PS[j] (masked: mask_ops first).  Dependencies among the
+        ops are derived from their registers by isa.schedule.  Returns (ops, last sum op)."""
+        ops = self.mask_ops(j, sreg, kbase_sgpr_add, lm or V_LM, key0) if masked else []
+        k = key0
+        last_sum = None
+        for e in range(32):
+            st, g = e // 16, e % 16
+            reg = sreg + e
+            kk = 4 * e
+            ops.append(Inst(f"v_fma_f32 v{reg}, v{reg}, s{S_C}, v{V_NEGMC[j]}", VALU, rd=vr(reg) + sr(S_C) + vr(V_NEGMC[j]),
+                            wr=vr(reg), key=k + kk + 1))
+            ops.append(Inst(f"v_exp_f32_e32 v{reg}, v{reg}", TRANS, rd=vr(reg), wr=vr(reg), key=k + kk + 2))
+            if e == 0:
+                a = Inst(f"v_mov_b32_e32 v{V_PS[j]}, v{reg}", VALU, rd=vr(reg), wr=vr(V_PS[j]), key=k + kk + 3)
+            else:
+                a = Inst(f"v_add_f32_e32 v{V_PS[j]}, v{reg}, v{V_PS[j]}", VALU, rd=vr(reg) + vr(V_PS[j]),
+                         wr=vr(V_PS[j]), key=k + kk + 3)
+            last_sum = a
+            ops.append(a)
+            if e % 2 == 1:
+                kkf = 2 * st + (g >> 3)
+                w = (g & 7) >> 1
+                ops.append(self.cvt(preg + 4 * kkf + w, reg - 1, reg, key=k + kk + 3))
+        return ops, last_sum
+
+    def guard_ops(self, j, refit_label, key, deadline=None):
+        """partial sum <= 2^8 on every lane (and not NaN), else refit; then l += partial.  The branch
+        and its return label are one instruction so that nothing is scheduled between them."""
+        cmp = Inst(f"v_cmp_nge_f32_e32 vcc, 0x43800000, v{V_PS[j]}", VALU, rd=vr(V_PS[j]), wr=[("vcc", 0)],
+                   key=key, deadline=deadline)
+        sc = Inst("s_cmp_lg_u64 vcc, 0", SALU, rd=[("vcc", 0)], wr=[("scc", 0)], key=key, deadline=deadline)
+        br = Inst(f"s_cbranch_scc1 {refit_label}\n{refit_label}_back:", BRANCH, rd=[("scc", 0)], key=key, deadline=deadline)
+        add = Inst(f"v_add_f32_e32 v{V_L[j]}, v{V_L[j]}, v{V_PS[j]}", VALU, rd=vr(V_L[j]) + vr(V_PS[j]),
+                   wr=vr(V_L[j]), key=key, deadline=deadline)
+        return [cmp, sc, br, add]
+
+    # ------------------------------------------------------------------ one pipelined step
+    def step(self, p, variant, tag):
+        """step n: phase X (QK(n+1) || softmax(n, b)), phase Y (PV(n) || softmax(n+1, a)).
+        variant: 'fast', 'masked' or 'last'.  Returns (instruction list, refit blocks)."""
+        last = variant == "last"
+        masked = variant != "fast"
+        refits = []
+        # ---------------- phase X
+        mx = []
+        if not last:
+            for i in range(32):
+                st, ks, j = i // 16, (i % 16) // 2, i % 2
+                f = st * 8 + ks
+                sreg = (SA if j == 0 else SB(p ^ 1)) + 16 * st
+                mx.append(self.mfma_s(sreg, f % 8, j, ks, ks == 0))
+        fx = []
+        # V base of tile n (slot offset S_VOFF, already advanced at the end of the previous step)
+        fx.append(Inst(f"v_add_u32_e32 v{V_VB0}, s{S_VOFF}, v{V_TB0}", VALU, rd=sr(S_VOFF) + vr(V_TB0), wr=vr(V_VB0), key=0))
+        fx.append(Inst(f"v_add_u32_e32 v{V_VB1}, s{S_VOFF}, v{V_TB1}", VALU, rd=sr(S_VOFF) + vr(V_TB1), wr=vr(V_VB1), key=0))
+        vb = fx[-2:]
+        if not last:
+            # K fragments 3..15 (0..2 were prefetched at the end of the previous step)
+            for f in range(3, 16):
+                eg = max(2 * (f - 3), 2 * (f - 8) + 3)
+                fx.append(self.kread(f, f % 8, key=-100 + f, earliest=eg, deadline=2 * f - 1))
+            # K DMA of tile n+4 (4 pieces)
+            for jj in range(4):
+                m = Inst(f"s_add_u32 m0, s{S_DOFF}, {jj * 4096}", SALU, rd=sr(S_DOFF), wr=[("m0", 0)], key=-60 + 4 * jj,
+                         earliest=3 + 7 * jj)
+                d = Inst(f"buffer_load_dwordx4 v{V_VOFF + jj}, s[{S_KD}:{S_KD + 3}], 0 offen lds", DMA,
+                         rd=vr(V_VOFF + jj) + sr(S_KD, 4) + [("m0", 0)], key=-60 + 4 * jj, earliest=3 + 7 * jj)
+                fx += [m, d]
+        # softmax (n, b)
+        sm_b, sum_b = self.softmax_ops(1, SB(p), PB, masked, (S_N0, 0), key0=0)
+        fx += sm_b
+        # V fragments of d-tiles 0 and 1 (8 frags) for phase Y
+        for f in range(8):
+            for h in range(2):
+                fx.append(self.vread(f, f % 8, h, key=-80 + 2 * f + h, earliest=(14 + 2 * f) if not last else None))
+        xs = schedule(mx, fx) if mx else schedule([], fx)
+        # ---------------- phase Y
+        my = []
+        for i in range(32):
+            dt, w = i // 8, i % 8
+            j, kk = w // 4, w % 4
+            f = 4 * dt + kk
+            preg = (PA(p) if j == 0 else PB) + 4 * kk
+            my.append(self.mfma_o(j, dt, f % 8, preg))
+        fy = []
+        rl_b = self.lab(f"{tag}_refit_b")
+        refits.append(self.refit(1, SB(p), PB, rl_b, tile_add=0, phase="Y"))
+        fy += self.guard_ops(1, rl_b, key=-200, deadline=4)
+        # V fragments of d-tiles 2, 3
+        for f in range(8, 16):
+            dt, kk = f // 4, f % 4
+            eg = 8 * (dt - 2) + 4 + kk + 1
+            dl = 8 * dt + kk - 2
+            for h in range(2):
+                fy.append(self.vread(f, f % 8, h, key=-150 + 2 * f + h, earliest=eg, deadline=dl))
+        t = S_TMP
+        if not last:
+            # softmax (n+1, a)
+            sm_a, sum_a = self.softmax_ops(0, SA, PA(p ^ 1), masked, (S_N0, 64), key0=0)
+            fy += sm_a
+            # V DMA of tile n+4, then advance the DMA offsets / slot / record counts
+            for jj in range(4):
+                fy.append(Inst(f"s_add_u32 m0, s{S_DOFF}, {VBASE + jj * 4096}", SALU, rd=sr(S_DOFF), wr=[("m0", 0)],
+                               key=-60 + 4 * jj, earliest=2 + 6 * jj))
+                fy.append(Inst(f"buffer_load_dwordx4 v{V_VOFF + jj}, s[{S_VD}:{S_VD + 3}], 0 offen lds", DMA,
+                               rd=vr(V_VOFF + jj) + sr(S_VD, 4) + [("m0", 0)], key=-60 + 4 * jj, earliest=2 + 6 * jj))
+                fy.append(Inst(f"v_add_u32_e32 v{V_VOFF + jj}, s{S_TB}, v{V_VOFF + jj}", VALU,
+                               rd=sr(S_TB) + vr(V_VOFF + jj), wr=vr(V_VOFF + jj), key=-58 + 4 * jj))
+            # next DMA slot / tile, zero the record counts once the tile index passes the end
+            fy += [
+                Inst(f"s_add_u32 s{S_DOFF}, s{S_DOFF}, {TILE}", SALU, rd=sr(S_DOFF), wr=sr(S_DOFF) + [("scc", 0)], key=-30),
+                Inst(f"s_sub_u32 s{t}, s{S_DOFF}, {NSLOT * TILE}", SALU, rd=sr(S_DOFF), wr=sr(t) + [("scc", 0)], key=-30),
+                Inst(f"s_cmp_ge_u32 s{S_DOFF}, {NSLOT * TILE}", SALU, rd=sr(S_DOFF), wr=[("scc", 0)], key=-30),
+                Inst(f"s_cselect_b32 s{S_DOFF}, s{t}, s{S_DOFF}", SALU, rd=sr(t) + sr(S_DOFF) + [("scc", 0)], wr=sr(S_DOFF), key=-30),
+                Inst(f"s_add_u32 s{S_DT}, s{S_DT}, 1", SALU, rd=sr(S_DT), wr=sr(S_DT) + [("scc", 0)], key=-30),
+            ]
+            if not OPT_NOZERO:
+                fy += [nop(15) for _ in range(OPT_ZERO_NOP)] + [
+                    Inst(f"s_cmp_lt_u32 s{S_DT}, s{S_NBLK}", SALU, rd=sr(S_DT) + sr(S_NBLK), wr=[("scc", 0)], key=-30),
+                    Inst(f"s_cselect_b32 s{S_KD + 2}, s{S_KD + 2}, 0", SALU, rd=sr(S_KD + 2) + [("scc", 0)], wr=sr(S_KD + 2), key=-30),
+                    Inst(f"s_cselect_b32 s{S_VD + 2}, s{S_VD + 2}, 0", SALU, rd=sr(S_VD + 2) + [("scc", 0)], wr=sr(S_VD + 2), key=-30)]
+            # K read base of tile n+2 and prefetch of its first three fragments (next phase X)
+            fy += [
+                Inst(f"s_add_u32 s{S_KOFF}, s{S_KOFF}, {TILE}", SALU, rd=sr(S_KOFF), wr=sr(S_KOFF) + [("scc", 0)], key=-20, earliest=18),
+                Inst(f"s_sub_u32 s{t + 1}, s{S_KOFF}, {NSLOT * TILE}", SALU, rd=sr(S_KOFF), wr=sr(t + 1) + [("scc", 0)], key=-20),
+                Inst(f"s_cmp_ge_u32 s{S_KOFF}, {NSLOT * TILE}", SALU, rd=sr(S_KOFF), wr=[("scc", 0)], key=-20),
+                Inst(f"s_cselect_b32 s{S_KOFF}, s{t + 1}, s{S_KOFF}", SALU, rd=sr(t + 1) + sr(S_KOFF) + [("scc", 0)], wr=sr(S_KOFF), key=-20),
+                Inst(f"v_add_u32_e32 v{V_KB0}, s{S_KOFF}, v{V_RB0}", VALU, rd=sr(S_KOFF) + vr(V_RB0), wr=vr(V_KB0), key=-20),
+                Inst(f"v_add_u32_e32 v{V_KB1}, s{S_KOFF}, v{V_RB1}", VALU, rd=sr(S_KOFF) + vr(V_RB1), wr=vr(V_KB1), key=-20),
+            ]
+            for f in range(3):
+                fy.append(self.kread(f, f % 8, key=-19 + f, earliest=22 + 2 * f))
+            rl_a = self.lab(f"{tag}_refit_a")
+            refits.append(self.refit(0, SA, PA(p ^ 1), rl_a, tile_add=64, phase="end"))
+            fy += self.guard_ops(0, rl_a, key=700)
+        # V read slot of the next tile
+        fy += [Inst(f"s_add_u32 s{S_VOFF}, s{S_VOFF}, {TILE}", SALU, rd=sr(S_VOFF), wr=sr(S_VOFF) + [("scc", 0)], key=800, earliest=28),
+               Inst(f"s_sub_u32 s{t + 2}, s{S_VOFF}, {NSLOT * TILE}", SALU, rd=sr(S_VOFF), wr=sr(t + 2) + [("scc", 0)], key=801),
+               Inst(f"s_cmp_ge_u32 s{S_VOFF}, {VBASE + NSLOT * TILE}", SALU, rd=sr(S_VOFF), wr=[("scc", 0)], key=802),
+               Inst(f"s_cselect_b32 s{S_VOFF}, s{t + 2}, s{S_VOFF}", SALU, rd=sr(t + 2) + sr(S_VOFF) + [("scc", 0)], wr=sr(S_VOFF), key=803)]
+        ys = schedule(my, fy)
+        body = xs + ys
+        if not last:
+            # tiles <= n+3 landed in every wave (K(n+3) is prefetched in the next step's phase Y)
+            body += [Inst(f"s_add_u32 s{S_N}, s{S_N}, 1", SALU, rd=sr(S_N), wr=sr(S_N) + [("scc", 0)]),
+                     Inst(f"s_add_u32 s{S_N0}, s{S_N0}, {BN}", SALU, rd=sr(S_N0), wr=sr(S_N0) + [("scc", 0)]),
+                     Inst("s_waitcnt vmcnt(8) lgkmcnt(0)", WAIT),
+                     Inst("s_barrier", BARRIER)]
+        return body, refits
+
+    # ------------------------------------------------------------------ refit (rare, out of line)
+    def refit(self, j, sreg, preg, lab, tile_add, phase):
+        """Out-of-line slow path (rare): recompute S of q-block j for its tile from the K slot that
+        still holds it, mask it, take the true row max, rescale O_j / l_j to it and redo P and the
+        partial sum.  phase 'Y' (tile n, checked before its first PV MFMA): S_KOFF still addresses
+        tile n+1; phase 'end' (tile n+1, checked at the end of phase Y): S_KOFF was advanced to tile
+        n+2.  Either way the tile's K slot is S_KOFF - TILE (mod the ring)."""
+        ins = [label(lab), nop(15), Inst("s_waitcnt lgkmcnt(0)", WAIT)]
+        t = V_T
+        s0 = S_TMP + 3
+        ins += [Inst(f"s_sub_u32 s{s0}, s{S_KOFF}, {TILE}", SALU, rd=sr(S_KOFF), wr=sr(s0)),
+                Inst(f"s_add_u32 s{S_TMP}, s{s0}, {NSLOT * TILE}", SALU, rd=sr(s0), wr=sr(S_TMP)),
+                Inst(f"s_cmp_lt_i32 s{s0}, 0", SALU, rd=sr(s0), wr=[("scc", 0)]),
+                Inst(f"s_cselect_b32 s{s0}, s{S_TMP}, s{s0}", SALU, rd=sr(S_TMP) + sr(s0), wr=sr(s0)),
+                Inst(f"v_add_u32_e32 v{t}, s{s0}, v{V_RB0}", VALU, rd=sr(s0) + vr(V_RB0), wr=vr(t)),
+                Inst(f"v_add_u32_e32 v{t + 1}, s{s0}, v{V_RB1}", VALU, rd=sr(s0) + vr(V_RB1), wr=vr(t + 1))]
+        # K fragment ring to use: phase Y -> the K ring (idle), end -> the V ring (the K ring holds
+        # the next phase X's prefetch)
+        ring = KF if phase == "Y" else VF
+        for st in range(2):
+            for ks in range(KS):
+                base = t if ks % 2 == 0 else t + 1
+                off = (ks // 2) * BN * 64 + st * 32 * 64
+                ins.append(Inst(f"ds_read_b128 {rtxt('a', ring + 4 * ks, 4)}, v{base} offset:{off}", LDS,
+                                rd=vr(base), wr=ar(ring + 4 * ks, 4)))
+            for ks in range(KS):
+                sreg_st = sreg + 16 * st
+                c = "0" if ks == 0 else rtxt("v", sreg_st, 16)
+                ins.append(Inst(f"v_mfma_f32_32x32x16_{self.ty} {rtxt('v', sreg_st, 16)}, {rtxt('a', ring + 4 * ks, 4)}, "
+                                f"{rtxt('a', Q_(j, ks), 4)}, {c}", MFMA,
+                                rd=ar(ring + 4 * ks, 4) + ar(Q_(j, ks), 4) + ([] if ks == 0 else vr(sreg_st, 16)),
+                                wr=vr(sreg_st, 16), rd_c=[] if ks == 0 else vr(sreg_st, 16)))
+        ins.append(nop(15))
+        # mask with the tile's limits (own limit registers: the interrupted stream may hold V_LM)
+        ins += self.mask_ops(j, sreg, (S_N0, tile_add), (t + 5, t + 6))
+        # row max -> v[t+2]
+        mx = t + 2
+        ins.append(Inst(f"v_max3_f32 v{mx}, v{sreg}, v{sreg + 1}, v{sreg + 2}", VALU, rd=vr(sreg, 3), wr=vr(mx)))
+        for e in range(3, 32, 2):
+            if e + 1 < 32:
+                ins.append(Inst(f"v_max3_f32 v{mx}, v{mx}, v{sreg + e}, v{sreg + e + 1}", VALU, rd=vr(mx) + vr(sreg + e, 2), wr=vr(mx)))
+            else:
+                ins.append(Inst(f"v_max_f32_e32 v{mx}, v{mx}, v{sreg + e}", VALU, rd=vr(mx) + vr(sreg + e), wr=vr(mx)))
+        ins += self.half_max(mx, t + 3)
+        # mnc = max(mc_old, mt * c); alpha = exp2(mc_old - mnc)
+        ins += [Inst(f"v_mul_f32_e32 v{mx}, s{S_C}, v{mx}", VALU, rd=sr(S_C) + vr(mx), wr=vr(mx)),
+                Inst(f"v_max_f32_e64 v{mx}, -v{V_NEGMC[j]}, v{mx}", VALU, rd=vr(V_NEGMC[j]) + vr(mx), wr=vr(mx)),
+                Inst(f"v_add_f32_e32 v{t + 3}, v{V_NEGMC[j]}, v{mx}", VALU, rd=vr(V_NEGMC[j]) + vr(mx), wr=vr(t + 3)),
+                Inst(f"v_exp_f32_e64 v{t + 3}, -v{t + 3}", TRANS, rd=vr(t + 3), wr=vr(t + 3)),
+                Inst(f"v_sub_f32_e32 v{V_NEGMC[j]}, 0, v{mx}", VALU, rd=vr(mx), wr=vr(V_NEGMC[j])),
+                Inst(f"v_mul_f32_e32 v{V_L[j]}, v{V_L[j]}, v{t + 3}", VALU, rd=vr(V_L[j]) + vr(t + 3), wr=vr(V_L[j]))]
+        for dt in range(NP):
+            for g in range(16):
+                a = O_(j, dt) + g
+                ins += [Inst(f"v_accvgpr_read_b32 v{t + 4}, a{a}", ACCR, rd=ar(a), wr=vr(t + 4)),
+                        Inst(f"v_mul_f32_e32 v{t + 4}, v{t + 4}, v{t + 3}", VALU, rd=vr(t + 4, 1) + vr(t + 3), wr=vr(t + 4)),
+                        Inst(f"v_accvgpr_write_b32 a{a}, v{t + 4}", ACCW, rd=vr(t + 4), wr=ar(a))]
+        sm, _ = self.softmax_ops(j, sreg, preg, False, None, key0=0)
+        ins += sm
+        ins.append(nop(7))
+        ins.append(Inst(f"s_branch {lab}_back", BRANCH))
+        out, _ = add_waits(ins)
+        out, _ = fix_hazards(out)
+        return out
+
+    def half_max(self, x, tmp):
+        """x = max over the two lane halves (lanes l, l^32 hold the same query)"""
+        return [Inst(f"v_mov_b32_e32 v{tmp}, v{x}", VALU, rd=vr(x), wr=vr(tmp)),
+                Inst(f"v_permlane32_swap_b32_e32 v{x}, v{tmp}", PERM, rd=vr(x) + vr(tmp), wr=vr(x) + vr(tmp)),
+                Inst(f"v_max_f32_e32 v{x}, v{x}, v{tmp}", VALU, rd=vr(x) + vr(tmp), wr=vr(x))]
+
+    def half_sum(self, x, tmp):
+        return [Inst(f"v_mov_b32_e32 v{tmp}, v{x}", VALU, rd=vr(x), wr=vr(tmp)),
+                Inst(f"v_permlane32_swap_b32_e32 v{x}, v{tmp}", PERM, rd=vr(x) + vr(tmp), wr=vr(x) + vr(tmp)),
+                Inst(f"v_add_f32_e32 v{x}, v{x}, v{tmp}", VALU, rd=vr(x) + vr(tmp), wr=vr(x))]
+
+    # ------------------------------------------------------------------ prologue / epilogue
+    def prologue(self, l_epi, l_entry_last, l_entry_fast, l_entry_masked):
+        I = Inst
+        ins = []
+        ka = S_KA
+        # kernargs: 40..55 pointers (q k v o lse sched cuq cuk); 56..63 rng seed offset q_batch;
+        # 64..79 k_batch v_batch o_batch q_row kv_row o_row q_head k_head v_head o_head sq sk lse_pitch;
+        # 80..83 h c flags pad
+        ins += [I(f"s_load_dwordx16 s[{ka}:{ka + 15}], s[0:1], 0x0", SMEM, rd=sr(0, 2), wr=sr(ka, 16)),
+                I(f"s_load_dwordx8 s[{ka + 16}:{ka + 23}], s[0:1], 0x40", SMEM, rd=sr(0, 2), wr=sr(ka + 16, 8)),
+                I(f"s_load_dwordx16 s[{ka + 24}:{ka + 39}], s[0:1], 0x60", SMEM, rd=sr(0, 2), wr=sr(ka + 24, 16)),
+                I(f"s_load_dwordx4 s[{ka + 40}:{ka + 43}], s[0:1], 0xa0", SMEM, rd=sr(0, 2), wr=sr(ka + 40, 4)),
+                I("s_waitcnt lgkmcnt(0)", WAIT)]
+        Pq, Pk, Pv, Po, Pl, Psch, Pcq, Pck = (ka + 2 * i for i in range(8))
+        Prng, Pseed, Poff, Bq = ka + 16, ka + 18, ka + 20, ka + 22
+        Bk, Bv, Bo = ka + 24, ka + 26, ka + 28
+        Rq, Rkv, Ro, Hq, Hk, Hv, Ho, SQ, SK, LP = (ka + 30 + i for i in range(10))
+        NH, CC, FL = ka + 40, ka + 41, ka + 42
+        T0, T1, T2, T3 = S_TMP, S_TMP + 1, S_TMP + 2, S_TMP + 3
+        # wave index, lane values
+        ins += [I("v_lshrrev_b32_e32 v1, 6, v0", VALU, rd=vr(0), wr=vr(1)),
+                I(f"v_readfirstlane_b32 s{S_WAVE}, v1", VALU, rd=vr(1), wr=sr(S_WAVE)),
+                I(f"v_and_b32_e32 v{V_LANE}, 63, v0", VALU, rd=vr(0), wr=vr(V_LANE))]
+        # rng_state (block 0, wave 0): {seed, offset}; lanes >= 1 fall outside the 16-byte record
+        l_norng = self.lab("norng")
+        ins += [I(f"s_or_b32 s{T0}, s2, s{S_WAVE}", SALU, rd=sr(2) + sr(S_WAVE), wr=sr(T0)),
+                I(f"s_cmp_lg_u32 s{T0}, 0", SALU, rd=sr(T0), wr=[("scc", 0)]),
+                I(f"s_cbranch_scc1 {l_norng}", BRANCH),
+                I(f"s_cmp_eq_u64 s[{Prng}:{Prng + 1}], 0", SALU, rd=sr(Prng, 2), wr=[("scc", 0)]),
+                I(f"s_cbranch_scc1 {l_norng}", BRANCH),
+                # descriptor in SGPRs that nothing rewrites while the store may still read them
+                I(f"s_mov_b32 s{S_RNGD}, s{Prng}", SALU, rd=sr(Prng), wr=sr(S_RNGD)),
+                I(f"s_and_b32 s{S_RNGD + 1}, s{Prng + 1}, 0xffff", SALU, rd=sr(Prng + 1), wr=sr(S_RNGD + 1)),
+                I(f"s_mov_b32 s{S_RNGD + 2}, 16", SALU, wr=sr(S_RNGD + 2)),
+                I(f"s_mov_b32 s{S_RNGD + 3}, 0x20000", SALU, wr=sr(S_RNGD + 3)),
+                I(f"v_lshlrev_b32_e32 v2, 4, v{V_LANE}", VALU, rd=vr(V_LANE), wr=vr(2)),
+                I(f"v_mov_b32_e32 v4, s{Pseed}", VALU, rd=sr(Pseed), wr=vr(4)),
+                I(f"v_mov_b32_e32 v5, s{Pseed + 1}", VALU, rd=sr(Pseed + 1), wr=vr(5)),
+                I(f"v_mov_b32_e32 v6, s{Poff}", VALU, rd=sr(Poff), wr=vr(6)),
+                I(f"v_mov_b32_e32 v7, s{Poff + 1}", VALU, rd=sr(Poff + 1), wr=vr(7)),
+                I(f"buffer_store_dwordx4 v[4:7], v2, s[{S_RNGD}:{S_RNGD + 3}], 0 offen", VSTORE, rd=vr(4, 4) + vr(2) + sr(S_RNGD, 4)),
+                label(l_norng)]
+        # schedule entry: (bidb | head << 16, kvh | m_block << 16)
+        ins += [I(f"s_lshl_b32 s{T0}, s2, 3", SALU, rd=sr(2), wr=sr(T0)),
+                I(f"s_load_dwordx2 s[{T0}:{T1}], s[{Psch}:{Psch + 1}], s{T0}", SMEM, rd=sr(Psch, 2) + sr(T0), wr=sr(T0, 2)),
+                I("s_waitcnt lgkmcnt(0)", WAIT)]
+        # scalars kept: bidb (T2), head (T3), kvh (S_N), m_block (S_N0) -- temporarily
+        BIDB, HEAD, KVH, MB = T2, T3, S_N, S_N0
+        ins += [I(f"s_and_b32 s{BIDB}, s{T0}, 0xffff", SALU, rd=sr(T0), wr=sr(BIDB)),
+                I(f"s_lshr_b32 s{HEAD}, s{T0}, 16", SALU, rd=sr(T0), wr=sr(HEAD)),
+                I(f"s_and_b32 s{KVH}, s{T1}, 0xffff", SALU, rd=sr(T1), wr=sr(KVH)),
+                I(f"s_lshr_b32 s{MB}, s{T1}, 16", SALU, rd=sr(T1), wr=sr(MB))]
+        # varlen geometry (BlockInfo, block_info.h:14-31): 64-bit byte offsets (lo, hi) of row 0 of
+        # this sequence in Q, O and K/V; seqlens in SQ / SK (overwritten in place)
+        QOFF, OOFF, KOFF = (84, 85), (86, 87), (88, 89)
+        l_q_fixed, l_q_done = self.lab("qfixed"), self.lab("qdone")
+        l_o_fixed, l_o_done = self.lab("ofixed"), self.lab("odone")
+        l_k_fixed, l_k_done = self.lab("kfixed"), self.lab("kdone")
+
+        def mul64(dst, a32, b32):
+            return [I(f"s_mul_i32 s{dst[0]}, s{a32}, s{b32}", SALU, rd=sr(a32) + sr(b32), wr=sr(dst[0])),
+                    I(f"s_mul_hi_u32 s{dst[1]}, s{a32}, s{b32}", SALU, rd=sr(a32) + sr(b32), wr=sr(dst[1]))]
+
+        def mul64_i64(dst, a32, b64):   # a32 * (b64 lo, hi) -> dst (lo, hi)
+            return [I(f"s_mul_i32 s{dst[0]}, s{a32}, s{b64}", SALU, rd=sr(a32) + sr(b64), wr=sr(dst[0])),
+                    I(f"s_mul_hi_u32 s{dst[1]}, s{a32}, s{b64}", SALU, rd=sr(a32) + sr(b64), wr=sr(dst[1])),
+                    I(f"s_mul_i32 s{T0}, s{a32}, s{b64 + 1}", SALU, rd=sr(a32) + sr(b64 + 1), wr=sr(T0)),
+                    I(f"s_add_u32 s{dst[1]}, s{dst[1]}, s{T0}", SALU, rd=sr(dst[1]) + sr(T0), wr=sr(dst[1]))]
+
+        for cu, bstride, rstride, off, seq, lf, ld in ((Pcq, Bq, Rq, QOFF, SQ, l_q_fixed, l_q_done),
+                                                       (Pcq, Bo, Ro, OOFF, None, l_o_fixed, l_o_done),
+                                                       (Pck, Bk, Rkv, KOFF, SK, l_k_fixed, l_k_done)):
+            ins += [I(f"s_cmp_eq_u64 s[{cu}:{cu + 1}], 0", SALU, rd=sr(cu, 2), wr=[("scc", 0)]),
+                    I(f"s_cbranch_scc1 {lf}", BRANCH),
+                    I(f"s_lshl_b32 s{T1}, s{BIDB}, 2", SALU, rd=sr(BIDB), wr=sr(T1)),
+                    I(f"s_load_dwordx2 s[{off[0]}:{off[1]}], s[{cu}:{cu + 1}], s{T1}", SMEM, rd=sr(cu, 2) + sr(T1), wr=sr(off[0], 2)),
+                    I("s_waitcnt lgkmcnt(0)", WAIT)]
+            if seq is not None:
+                ins += [I(f"s_sub_u32 s{seq}, s{off[1]}, s{off[0]}", SALU, rd=sr(off[0], 2), wr=sr(seq))]
+            ins += [I(f"s_bitcmp1_b32 s{FL}, 0", SALU, rd=sr(FL), wr=[("scc", 0)]),
+                    I(f"s_cbranch_scc1 {lf}", BRANCH),
+                    I(f"s_mov_b32 s{T1}, s{off[0]}", SALU, rd=sr(off[0]), wr=sr(T1))]
+            ins += mul64(off, T1, rstride)
+            ins += [I(f"s_branch {ld}", BRANCH), label(lf)]
+            ins += mul64_i64(off, BIDB, bstride)
+            ins += [label(ld)]
+        # m0 = 256 m_block; exit when m0 >= sq
+        M0R = S_DT
+        ins += [I(f"s_lshl_b32 s{M0R}, s{MB}, 8", SALU, rd=sr(MB), wr=sr(M0R)),
+                I(f"s_cmp_ge_i32 s{M0R}, s{SQ}", SALU, rd=sr(M0R) + sr(SQ), wr=[("scc", 0)]),
+                I(f"s_cbranch_scc1 {self.lab_end}", BRANCH)]
+        # rows of this workgroup: nrow = min(sq - m0, 256)
+        NROW = S_NBLK
+        ins += [I(f"s_sub_u32 s{NROW}, s{SQ}, s{M0R}", SALU, rd=sr(SQ) + sr(M0R), wr=sr(NROW)),
+                I(f"s_min_u32 s{NROW}, s{NROW}, {BM}", SALU, rd=sr(NROW), wr=sr(NROW))]
+
+        def addr(dst4, ptr, off64, head, hstride, rows=None, rstride=None, nrec=None):
+            """descriptor at ptr + off64 + head * hstride (+ rows * rstride)"""
+            o = []
+            o += [I(f"s_mul_i32 s{T0}, s{head}, s{hstride}", SALU, rd=sr(head) + sr(hstride), wr=sr(T0)),
+                  I(f"s_mul_hi_u32 s{T1}, s{head}, s{hstride}", SALU, rd=sr(head) + sr(hstride), wr=sr(T1)),
+                  I(f"s_add_u32 s{dst4}, s{ptr}, s{T0}", SALU, rd=sr(ptr) + sr(T0), wr=sr(dst4) + [("scc", 0)]),
+                  I(f"s_addc_u32 s{dst4 + 1}, s{ptr + 1}, s{T1}", SALU, rd=sr(ptr + 1) + sr(T1) + [("scc", 0)], wr=sr(dst4 + 1) + [("scc", 0)]),
+                  I(f"s_add_u32 s{dst4}, s{dst4}, s{off64[0]}", SALU, rd=sr(dst4) + sr(off64[0]), wr=sr(dst4) + [("scc", 0)]),
+                  I(f"s_addc_u32 s{dst4 + 1}, s{dst4 + 1}, s{off64[1]}", SALU, rd=sr(dst4 + 1) + sr(off64[1]) + [("scc", 0)], wr=sr(dst4 + 1))]
+            if rows is not None:
+                o += [I(f"s_mul_i32 s{T0}, s{rows}, s{rstride}", SALU, rd=sr(rows) + sr(rstride), wr=sr(T0)),
+                      I(f"s_mul_hi_u32 s{T1}, s{rows}, s{rstride}", SALU, rd=sr(rows) + sr(rstride), wr=sr(T1)),
+                      I(f"s_add_u32 s{dst4}, s{dst4}, s{T0}", SALU, rd=sr(dst4) + sr(T0), wr=sr(dst4) + [("scc", 0)]),
+                      I(f"s_addc_u32 s{dst4 + 1}, s{dst4 + 1}, s{T1}", SALU, rd=sr(dst4 + 1) + sr(T1), wr=sr(dst4 + 1))]
+            o += [I(f"s_and_b32 s{dst4 + 1}, s{dst4 + 1}, 0xffff", SALU, rd=sr(dst4 + 1), wr=sr(dst4 + 1))]
+            o += nrec
+            o += [I(f"s_mov_b32 s{dst4 + 3}, 0x20000", SALU, wr=sr(dst4 + 3))]
+            return o
+
+        # Q / O descriptors: rows [m0, m0 + nrow) of this sequence and head
+        ins += addr(S_QD, Pq, QOFF, HEAD, Hq, rows=M0R, rstride=Rq,
+                    nrec=[I(f"s_mul_i32 s{S_QD + 2}, s{NROW}, s{Rq}", SALU, rd=sr(NROW) + sr(Rq), wr=sr(S_QD + 2))])
+        ins += addr(S_OD, Po, OOFF, HEAD, Ho, rows=M0R, rstride=Ro,
+                    nrec=[I(f"s_mul_i32 s{S_OD + 2}, s{NROW}, s{Ro}", SALU, rd=sr(NROW) + sr(Ro), wr=sr(S_OD + 2))])
+        # K / V descriptors: every key of this sequence and kv head (host checks sk * kv_row < 2^31)
+        ins += addr(S_KD, Pk, KOFF, KVH, Hk,
+                    nrec=[I(f"s_mul_i32 s{S_KD + 2}, s{SK}, s{Rkv}", SALU, rd=sr(SK) + sr(Rkv), wr=sr(S_KD + 2))])
+        ins += addr(S_VD, Pv, KOFF, KVH, Hv,
+                    nrec=[I(f"s_mul_i32 s{S_VD + 2}, s{SK}, s{Rkv}", SALU, rd=sr(SK) + sr(Rkv), wr=sr(S_VD + 2))])
+        # LSE descriptor: lse + ((bidb * h + head) * lse_pitch + m0) * 4
+        # idx (64-bit, in S_LD+2 lo / S_LD+3 hi) = (bidb * h + head) * lse_pitch + m0; bytes = 4 idx
+        ins += [I(f"s_mul_i32 s{T0}, s{BIDB}, s{NH}", SALU, rd=sr(BIDB) + sr(NH), wr=sr(T0)),
+                I(f"s_add_u32 s{T0}, s{T0}, s{HEAD}", SALU, rd=sr(T0) + sr(HEAD), wr=sr(T0)),
+                I(f"s_mul_i32 s{S_LD + 2}, s{T0}, s{LP}", SALU, rd=sr(T0) + sr(LP), wr=sr(S_LD + 2)),
+                I(f"s_mul_hi_u32 s{S_LD + 3}, s{T0}, s{LP}", SALU, rd=sr(T0) + sr(LP), wr=sr(S_LD + 3)),
+                I(f"s_add_u32 s{S_LD + 2}, s{S_LD + 2}, s{M0R}", SALU, rd=sr(S_LD + 2) + sr(M0R), wr=sr(S_LD + 2) + [("scc", 0)]),
+                I(f"s_addc_u32 s{S_LD + 3}, s{S_LD + 3}, 0", SALU, rd=sr(S_LD + 3), wr=sr(S_LD + 3)),
+                I(f"s_lshl_b64 s[{S_LD + 2}:{S_LD + 3}], s[{S_LD + 2}:{S_LD + 3}], 2", SALU, rd=sr(S_LD + 2, 2), wr=sr(S_LD + 2, 2)),
+                I(f"s_add_u32 s{S_LD}, s{Pl}, s{S_LD + 2}", SALU, rd=sr(Pl) + sr(S_LD + 2), wr=sr(S_LD) + [("scc", 0)]),
+                I(f"s_addc_u32 s{S_LD + 1}, s{Pl + 1}, s{S_LD + 3}", SALU, rd=sr(Pl + 1) + sr(S_LD + 3), wr=sr(S_LD + 1)),
+                I(f"s_and_b32 s{S_LD + 1}, s{S_LD + 1}, 0xffff", SALU, rd=sr(S_LD + 1), wr=sr(S_LD + 1)),
+                I(f"s_lshl_b32 s{S_LD + 2}, s{NROW}, 2", SALU, rd=sr(NROW), wr=sr(S_LD + 2)),
+                I(f"s_mov_b32 s{S_LD + 3}, 0x20000", SALU, wr=sr(S_LD + 3))]
+        # tile counts: n_end = causal ? min(sk, m0 + 256) : sk; nblk = ceil(n_end / 64);
+        # nfast = min(nblk, (causal ? min(sk, m0 + 1) : sk) / 64)
+        if self.causal:
+            ins += [I(f"s_add_u32 s{T0}, s{M0R}, {BM}", SALU, rd=sr(M0R), wr=sr(T0)),
+                    I(f"s_min_i32 s{T0}, s{T0}, s{SK}", SALU, rd=sr(T0) + sr(SK), wr=sr(T0)),
+                    I(f"s_add_u32 s{T1}, s{M0R}, 1", SALU, rd=sr(M0R), wr=sr(T1)),
+                    I(f"s_min_i32 s{T1}, s{T1}, s{SK}", SALU, rd=sr(T1) + sr(SK), wr=sr(T1))]
+        else:
+            ins += [I(f"s_mov_b32 s{T0}, s{SK}", SALU, rd=sr(SK), wr=sr(T0)),
+                    I(f"s_mov_b32 s{T1}, s{SK}", SALU, rd=sr(SK), wr=sr(T1))]
+        ins += [I(f"s_max_i32 s{T0}, s{T0}, 0", SALU, rd=sr(T0), wr=sr(T0)),
+                I(f"s_add_u32 s{T0}, s{T0}, {BN - 1}", SALU, rd=sr(T0), wr=sr(T0)),
+                I(f"s_lshr_b32 s{S_NBLK}, s{T0}, 6", SALU, rd=sr(T0), wr=sr(S_NBLK)),
+                I(f"s_max_i32 s{T1}, s{T1}, 0", SALU, rd=sr(T1), wr=sr(T1)),
+                I(f"s_lshr_b32 s{T1}, s{T1}, 6", SALU, rd=sr(T1), wr=sr(T1)),
+                I(f"s_min_u32 s{T1}, s{T1}, s{S_NBLK}", SALU, rd=sr(T1) + sr(S_NBLK), wr=sr(T1)),
+                I(f"s_sub_i32 s{S_NF2}, s{T1}, 2", SALU, rd=sr(T1), wr=sr(S_NF2)),
+                I(f"s_sub_i32 s{S_NL1}, s{S_NBLK}, 1", SALU, rd=sr(S_NBLK), wr=sr(S_NL1)),
+                I(f"s_mov_b32 s{S_C}, s{CC}", SALU, rd=sr(CC), wr=sr(S_C)),
+                I(f"s_lshl_b32 s{S_TB}, s{Rkv}, 6", SALU, rd=sr(Rkv), wr=sr(S_TB))]
+        # ---- per-lane values (v1 = wave, V_LANE = lane) ----
+        r, hh = "v2", "v3"
+        ins += [I(f"v_and_b32_e32 v2, 31, v{V_LANE}", VALU, rd=vr(V_LANE), wr=vr(2)),
+                I(f"v_lshrrev_b32_e32 v3, 5, v{V_LANE}", VALU, rd=vr(V_LANE), wr=vr(3))]
+        # Q / O row offsets: row (in the block) = 64 wave + 32 j + r
+        for j in range(2):
+            ins += [I(f"v_lshl_add_u32 v4, v1, 6, v2", VALU, rd=vr(1) + vr(2), wr=vr(4)),
+                    I(f"v_add_u32_e32 v4, {32 * j}, v4", VALU, rd=vr(4), wr=vr(4)),
+                    I(f"v_mul_lo_u32 v{V_QOFF[j]}, v4, s{Rq}", VALU, rd=vr(4) + sr(Rq), wr=vr(V_QOFF[j])),
+                    I(f"v_lshl_add_u32 v{V_QOFF[j]}, v3, 4, v{V_QOFF[j]}", VALU, rd=vr(3) + vr(V_QOFF[j]), wr=vr(V_QOFF[j])),
+                    I(f"v_lshlrev_b32_e32 v{V_LSEOFF[j]}, 2, v4", VALU, rd=vr(4), wr=vr(V_LSEOFF[j])),
+                    # mask limit base: (causal ? min(m0 + row, sk - 1) : sk - 1) - 4 hh
+                    I(f"v_add_u32_e32 v5, s{M0R}, v4", VALU, rd=sr(M0R) + vr(4), wr=vr(5)),
+                    I(f"s_sub_i32 s{T0}, s{SK}, 1", SALU, rd=sr(SK), wr=sr(T0))]
+            if self.causal:
+                ins += [I(f"v_min_i32_e32 v5, s{T0}, v5", VALU, rd=sr(T0) + vr(5), wr=vr(5))]
+            else:
+                ins += [I(f"v_mov_b32_e32 v5, s{T0}", VALU, rd=sr(T0), wr=vr(5))]
+            ins += [I(f"v_lshlrev_b32_e32 v6, 2, v3", VALU, rd=vr(3), wr=vr(6)),
+                    I(f"v_sub_u32_e32 v{V_LB[j]}, v5, v6", VALU, rd=vr(5) + vr(6), wr=vr(V_LB[j]))]
+        # Q fragments into the accumulator file: lane holds Q[row][16 ks + 8 hh .. +7]
+        for j in range(2):
+            for ks in range(KS):
+                ins.append(I(f"buffer_load_dwordx4 {rtxt('a', Q_(j, ks), 4)}, v{V_QOFF[j]}, s[{S_QD}:{S_QD + 3}], 0 offen offset:{32 * ks}",
+                             VLOAD, rd=vr(V_QOFF[j]) + sr(S_QD, 4), wr=ar(Q_(j, ks), 4)))
+        # O row offsets for the stores: row * o_row + 16 hh
+        for j in range(2):
+            ins += [I(f"v_lshl_add_u32 v4, v1, 6, v2", VALU, rd=vr(1) + vr(2), wr=vr(4)),
+                    I(f"v_add_u32_e32 v4, {32 * j}, v4", VALU, rd=vr(4), wr=vr(4)),
+                    I(f"v_mul_lo_u32 v{V_OOFF[j]}, v4, s{Ro}", VALU, rd=vr(4) + sr(Ro), wr=vr(V_OOFF[j])),
+                    I(f"v_lshl_add_u32 v{V_OOFF[j]}, v3, 4, v{V_OOFF[j]}", VALU, rd=vr(3) + vr(V_OOFF[j]), wr=vr(V_OOFF[j]))]
+        # LDS lane bases (fa_common.h LdsBases): rb = r*64 + ((c ^ xr) << 4), c = hh / 2+hh, xr = (r>>2)&3
+        ins += [I("v_bfe_u32 v4, v2, 2, 2", VALU, rd=vr(2), wr=vr(4)),                      # xr
+                I("v_xor_b32_e32 v5, v3, v4", VALU, rd=vr(3) + vr(4), wr=vr(5)),
+                I("v_lshlrev_b32_e32 v6, 6, v2", VALU, rd=vr(2), wr=vr(6)),
+                I(f"v_lshl_add_u32 v{V_RB0}, v5, 4, v6", VALU, rd=vr(5) + vr(6), wr=vr(V_RB0)),
+                I("v_add_u32_e32 v5, 2, v3", VALU, rd=vr(3), wr=vr(5)),
+                I("v_xor_b32_e32 v5, v5, v4", VALU, rd=vr(5) + vr(4), wr=vr(5)),
+                I(f"v_lshl_add_u32 v{V_RB1}, v5, 4, v6", VALU, rd=vr(5) + vr(6), wr=vr(V_RB1))]
+        # tb: i = lane & 15, q = i >> 2, pp = i & 3, trc = 2 (r >> 4) + (pp >> 1)
+        #     tb0 = (4 hh + q) 64 + ((trc ^ hh) << 4) + (pp & 1) 8 ; tb1 = ... ((trc ^ (2 + hh)) << 4) ...
+        ins += [I(f"v_and_b32_e32 v4, 15, v{V_LANE}", VALU, rd=vr(V_LANE), wr=vr(4)),        # i
+                I("v_lshrrev_b32_e32 v5, 2, v4", VALU, rd=vr(4), wr=vr(5)),                  # q
+                I("v_and_b32_e32 v6, 3, v4", VALU, rd=vr(4), wr=vr(6)),                      # pp
+                I("v_lshrrev_b32_e32 v7, 4, v2", VALU, rd=vr(2), wr=vr(7)),                  # r >> 4
+                I("v_lshrrev_b32_e32 v8, 1, v6", VALU, rd=vr(6), wr=vr(8)),                  # pp >> 1
+                I("v_lshl_add_u32 v7, v7, 1, v8", VALU, rd=vr(7) + vr(8), wr=vr(7)),          # trc
+                I("v_lshl_add_u32 v8, v3, 2, v5", VALU, rd=vr(3) + vr(5), wr=vr(8)),          # 4 hh + q
+                I("v_lshlrev_b32_e32 v8, 6, v8", VALU, rd=vr(8), wr=vr(8)),
+                I("v_and_b32_e32 v9, 1, v6", VALU, rd=vr(6), wr=vr(9)),
+                I("v_lshl_add_u32 v8, v9, 3, v8", VALU, rd=vr(9) + vr(8), wr=vr(8)),          # + (pp & 1) 8
+                I("v_xor_b32_e32 v9, v7, v3", VALU, rd=vr(7) + vr(3), wr=vr(9)),
+                I(f"v_lshl_add_u32 v{V_TB0}, v9, 4, v8", VALU, rd=vr(9) + vr(8), wr=vr(V_TB0)),
+                I("v_add_u32_e32 v9, 2, v3", VALU, rd=vr(3), wr=vr(9)),
+                I("v_xor_b32_e32 v9, v7, v9", VALU, rd=vr(7) + vr(9), wr=vr(9)),
+                I(f"v_lshl_add_u32 v{V_TB1}, v9, 4, v8", VALU, rd=vr(9) + vr(8), wr=vr(V_TB1))]
+        # DMA voffsets: row = 16 wave + lane / 4, chunk = (lane & 3) ^ ((row >> 2) & 3);
+        # voff_j = row * kv_row + 64 j + 16 chunk
+        ins += [I(f"v_lshrrev_b32_e32 v4, 2, v{V_LANE}", VALU, rd=vr(V_LANE), wr=vr(4)),
+                I("v_lshl_add_u32 v4, v1, 4, v4", VALU, rd=vr(1) + vr(4), wr=vr(4)),              # row
+                I("v_bfe_u32 v5, v4, 2, 2", VALU, rd=vr(4), wr=vr(5)),
+                I(f"v_and_b32_e32 v6, 3, v{V_LANE}", VALU, rd=vr(V_LANE), wr=vr(6)),
+                I("v_xor_b32_e32 v5, v5, v6", VALU, rd=vr(5) + vr(6), wr=vr(5)),                   # chunk
+                I(f"v_mul_lo_u32 v4, v4, s{Rkv}", VALU, rd=vr(4) + sr(Rkv), wr=vr(4)),
+                I(f"v_lshl_add_u32 v{V_VOFF}, v5, 4, v4", VALU, rd=vr(5) + vr(4), wr=vr(V_VOFF))]
+        for jj in range(1, 4):
+            ins.append(I(f"v_add_u32_e32 v{V_VOFF + jj}, {64 * jj}, v{V_VOFF}", VALU, rd=vr(V_VOFF), wr=vr(V_VOFF + jj)))
+        ins += [I(f"v_mov_b32_e32 v{V_NINF}, 0xff800000", VALU, wr=vr(V_NINF)),
+                I(f"s_lshl_b32 s{S_DOFF}, s{S_WAVE}, 10", SALU, rd=sr(S_WAVE), wr=sr(S_DOFF)),
+                I(f"s_mov_b32 s{S_KOFF}, 0", SALU, wr=sr(S_KOFF)),
+                I(f"s_mov_b32 s{S_VOFF}, {VBASE}", SALU, wr=sr(S_VOFF)),
+                I(f"s_mov_b32 s{S_DT}, 0", SALU, wr=sr(S_DT)),
+                I(f"s_mov_b32 s{S_N}, 0", SALU, wr=sr(S_N)),
+                I(f"s_mov_b32 s{S_N0}, 0", SALU, wr=sr(S_N0))]
+        # zero O, running sums
+        for i in range(128):
+            ins.append(I(f"v_accvgpr_write_b32 a{i}, 0", ACCW, wr=ar(i)))
+        ins += [I(f"v_mov_b32_e32 v{V_L[0]}, 0", VALU, wr=vr(V_L[0])),
+                I(f"v_mov_b32_e32 v{V_L[1]}, 0", VALU, wr=vr(V_L[1])),
+                I(f"v_mov_b32_e32 v{V_NEGMC[0]}, 0", VALU, wr=vr(V_NEGMC[0])),
+                I(f"v_mov_b32_e32 v{V_NEGMC[1]}, 0", VALU, wr=vr(V_NEGMC[1]))]
+        # no tiles at all: epilogue (O = 0, LSE = +inf)
+        ins += [I(f"s_cmp_eq_u32 s{S_NBLK}, 0", SALU, rd=sr(S_NBLK), wr=[("scc", 0)]),
+                I("s_waitcnt vmcnt(0)", WAIT),
+                I(f"s_cbranch_scc1 {l_epi}", BRANCH)]
+        # DMA of tiles 0..3 (tiles past nblk: zero records)
+        for tile in range(4):
+            if not OPT_NOZERO:
+                ins += [nop(15) for _ in range(OPT_ZERO_NOP)] + [
+                    I(f"s_cmp_lt_u32 s{S_DT}, s{S_NBLK}", SALU, rd=sr(S_DT) + sr(S_NBLK), wr=[("scc", 0)]),
+                    I(f"s_cselect_b32 s{S_KD + 2}, s{S_KD + 2}, 0", SALU, rd=sr(S_KD + 2), wr=sr(S_KD + 2)),
+                    I(f"s_cselect_b32 s{S_VD + 2}, s{S_VD + 2}, 0", SALU, rd=sr(S_VD + 2), wr=sr(S_VD + 2))]
+            for jj in range(4):
+                ins += [I(f"s_add_u32 m0, s{S_DOFF}, {jj * 4096}", SALU, rd=sr(S_DOFF), wr=[("m0", 0)]),
+                        I(f"buffer_load_dwordx4 v{V_VOFF + jj}, s[{S_KD}:{S_KD + 3}], 0 offen lds", DMA,
+                          rd=vr(V_VOFF + jj) + sr(S_KD, 4) + [("m0", 0)])]
+            for jj in range(4):
+                ins += [I(f"s_add_u32 m0, s{S_DOFF}, {VBASE + jj * 4096}", SALU, rd=sr(S_DOFF), wr=[("m0", 0)]),
+                        I(f"buffer_load_dwordx4 v{V_VOFF + jj}, s[{S_VD}:{S_VD + 3}], 0 offen lds", DMA,
+                          rd=vr(V_VOFF + jj) + sr(S_VD, 4) + [("m0", 0)])]
+            for jj in range(4):
+                ins.append(I(f"v_add_u32_e32 v{V_VOFF + jj}, s{S_TB}, v{V_VOFF + jj}", VALU, rd=sr(S_TB) + vr(V_VOFF + jj), wr=vr(V_VOFF + jj)))
+            ins += [I(f"s_add_u32 s{S_DOFF}, s{S_DOFF}, {TILE}", SALU, rd=sr(S_DOFF), wr=sr(S_DOFF)),
+                    I(f"s_add_u32 s{S_DT}, s{S_DT}, 1", SALU, rd=sr(S_DT), wr=sr(S_DT))]
+        # Q + tiles 0, 1, 2 landed (tile 3 in flight; K(2) is prefetched during step 0)
+        ins += [I("s_waitcnt vmcnt(8)", WAIT), I("s_barrier", BARRIER)]
+        # ---- tile 0: S(0, a), S(0, b) -> masked, explicit row max, P(0, a)
+        ins += [I(f"v_add_u32_e32 v{V_KB0}, 0, v{V_RB0}", VALU, rd=vr(V_RB0), wr=vr(V_KB0)),
+                I(f"v_add_u32_e32 v{V_KB1}, 0, v{V_RB1}", VALU, rd=vr(V_RB1), wr=vr(V_KB1))]
+        mfm = []
+        for i in range(32):
+            st, ks, j = i // 16, (i % 16) // 2, i % 2
+            f = st * 8 + ks
+            sreg = (SA if j == 0 else SB(0)) + 16 * st
+            mfm.append(self.mfma_s(sreg, f % 8, j, ks, ks == 0))
+        reads = []
+        for f in range(16):
+            reads.append(self.kread(f, f % 8, key=f, earliest=max(2 * (f - 3), 2 * (f - 8) + 3) if f >= 3 else None,
+                                    deadline=2 * f - 1 if f >= 3 else 0))
+        body = schedule(mfm, reads)
+        ins += body
+        ins.append(nop(15))
+        for j, sreg in ((0, SA), (1, SB(0))):
+            ins += self.mask_ops(j, sreg, (S_N0, 0), V_LM)
+            mx = V_T + 2
+            ins.append(Inst(f"v_max3_f32 v{mx}, v{sreg}, v{sreg + 1}, v{sreg + 2}", VALU, rd=vr(sreg, 3), wr=vr(mx)))
+            for e in range(3, 32, 2):
+                if e + 1 < 32:
+                    ins.append(Inst(f"v_max3_f32 v{mx}, v{mx}, v{sreg + e}, v{sreg + e + 1}", VALU, rd=vr(mx) + vr(sreg + e, 2), wr=vr(mx)))
+                else:
+                    ins.append(Inst(f"v_max_f32_e32 v{mx}, v{mx}, v{sreg + e}", VALU, rd=vr(mx) + vr(sreg + e), wr=vr(mx)))
+            ins += self.half_max(mx, V_T + 3)
+            # negmc = m == -inf ? 0 : -m c
+            ins += [Inst(f"v_mul_f32_e32 v{V_T + 4}, s{S_C}, v{mx}", VALU, rd=sr(S_C) + vr(mx), wr=vr(V_T + 4)),
+                    Inst(f"v_sub_f32_e32 v{V_NEGMC[j]}, 0, v{V_T + 4}", VALU, rd=vr(V_T + 4), wr=vr(V_NEGMC[j])),
+                    Inst(f"v_cmp_eq_f32_e32 vcc, v{V_NINF}, v{mx}", VALU, rd=vr(V_NINF) + vr(mx), wr=[("vcc", 0)]),
+                    Inst(f"v_cndmask_b32_e64 v{V_NEGMC[j]}, v{V_NEGMC[j]}, 0, vcc", VALU,
+                         rd=vr(V_NEGMC[j]) + [("vcc", 0)], wr=vr(V_NEGMC[j]))]
+        sm, _ = self.softmax_ops(0, SA, PA(0), False, None, key0=0)
+        ins += sm
+        ins += [Inst(f"v_mov_b32_e32 v{V_L[0]}, v{V_PS[0]}", VALU, rd=vr(V_PS[0]), wr=vr(V_L[0]))]
+        # entry (S_KOFF addresses tile n+1 = 1 at step 0; the LAST step's refit takes S_KOFF - TILE)
+        ins += [I(f"s_mov_b32 s{S_KOFF}, {TILE}", SALU, wr=sr(S_KOFF)),
+                I(f"s_cmp_eq_u32 s{S_NBLK}, 1", SALU, rd=sr(S_NBLK), wr=[("scc", 0)]),
+                I(f"s_cbranch_scc1 {l_entry_last}", BRANCH)]
+        # K(1) base + prefetch of its first three fragments
+        ins += [I(f"v_add_u32_e32 v{V_KB0}, s{S_KOFF}, v{V_RB0}", VALU, rd=sr(S_KOFF) + vr(V_RB0), wr=vr(V_KB0)),
+                I(f"v_add_u32_e32 v{V_KB1}, s{S_KOFF}, v{V_RB1}", VALU, rd=sr(S_KOFF) + vr(V_RB1), wr=vr(V_KB1))]
+        for f in range(3):
+            ins.append(self.kread(f, f % 8))
+        ins += [I("s_waitcnt lgkmcnt(0)", WAIT),
+                I(f"s_cmp_ge_i32 s{S_NF2}, 0", SALU, rd=sr(S_NF2), wr=[("scc", 0)]),
+                I(f"s_cbranch_scc1 {l_entry_fast}", BRANCH),
+                I(f"s_branch {l_entry_masked}", BRANCH)]
+        return ins
+
+    def epilogue(self):
+        ins = []
+        t = 0   # the score registers are free after the last step
+        for j in range(2):
+            l, inv, lse = V_L[j], t, t + 1
+            ins += self.half_sum(l, t + 2)
+            # bad = l == 0 || l != l  -> inv = 1, lse = +inf
+            ins += [Inst(f"v_rcp_f32_e32 v{inv}, v{l}", TRANS, rd=vr(l), wr=vr(inv)),
+                    Inst(f"v_log_f32_e32 v{lse}, v{l}", TRANS, rd=vr(l), wr=vr(lse)),
+                    Inst(f"v_sub_f32_e32 v{lse}, v{lse}, v{V_NEGMC[j]}", VALU, rd=vr(lse) + vr(V_NEGMC[j]), wr=vr(lse)),
+                    Inst(f"v_mul_f32_e32 v{lse}, 0x3f317218, v{lse}", VALU, rd=vr(lse), wr=vr(lse)),
+                    Inst(f"v_cmp_neq_f32_e32 vcc, 0, v{l}", VALU, rd=vr(l), wr=[("vcc", 0)]),
+                    Inst(f"v_cmp_eq_f32_e64 s[{S_TMP}:{S_TMP + 1}], v{l}, v{l}", VALU, rd=vr(l), wr=sr(S_TMP, 2)),
+                    Inst(f"s_and_b64 vcc, vcc, s[{S_TMP}:{S_TMP + 1}]", SALU, rd=sr(S_TMP, 2) + [("vcc", 0)], wr=[("vcc", 0)]),
+                    Inst(f"v_cndmask_b32_e64 v{inv}, 1.0, v{inv}, vcc", VALU, rd=vr(inv) + [("vcc", 0)], wr=vr(inv)),
+                    Inst(f"v_mov_b32_e32 v{t + 3}, 0x7f800000", VALU, wr=vr(t + 3)),
+                    Inst(f"v_cndmask_b32_e32 v{lse}, v{t + 3}, v{lse}, vcc", VALU, rd=vr(lse) + vr(t + 3) + [("vcc", 0)], wr=vr(lse)),
+                    Inst(f"buffer_store_dword v{lse}, v{V_LSEOFF[j]}, s[{S_LD}:{S_LD + 3}], 0 offen", VSTORE,
+                         rd=vr(lse) + vr(V_LSEOFF[j]) + sr(S_LD, 4))]
+            for dt in range(NP):
+                for u in (0, 2):
+                    w = t + 4 + 4 * ((dt * 2 + u // 2) % 4)
+                    o = O_(j, dt) + 4 * u
+                    x = t + 20
+                    ins += [Inst(f"v_accvgpr_read_b32 v{x + k}, a{o + k}", ACCR, rd=ar(o + k), wr=vr(x + k)) for k in range(8)]
+                    ins += [Inst(f"v_mul_f32_e32 v{x + k}, v{x + k}, v{inv}", VALU, rd=vr(x + k) + vr(inv), wr=vr(x + k)) for k in range(8)]
+                    ins += [self.cvt(w + 0, x + 0, x + 1), self.cvt(w + 1, x + 2, x + 3),
+                            self.cvt(w + 2, x + 4, x + 5), self.cvt(w + 3, x + 6, x + 7)]
+                    ins += [Inst(f"v_permlane32_swap_b32_e32 v{w}, v{w + 2}", PERM, rd=vr(w) + vr(w + 2), wr=vr(w) + vr(w + 2)),
+                            Inst(f"v_permlane32_swap_b32_e32 v{w + 1}, v{w + 3}", PERM, rd=vr(w + 1) + vr(w + 3), wr=vr(w + 1) + vr(w + 3))]
+                    ins.append(Inst(f"buffer_store_dwordx4 v[{w}:{w + 3}], v{V_OOFF[j]}, s[{S_OD}:{S_OD + 3}], 0 offen offset:{64 * dt + 16 * u}",
+                                    VSTORE, rd=vr(w, 4) + vr(V_OOFF[j]) + sr(S_OD, 4)))
+        return ins
+
+    # ------------------------------------------------------------------ whole kernel
+    def build(self):
+        self.lab_end = self.lab("end")
+        l_epi = self.lab("epi")
+        L = {k: self.lab(k) for k in ("fast0", "fast1", "sel0", "sel1", "masked0", "masked1", "last0", "last1")}
+        pro = self.prologue(l_epi, L["last0"], L["fast0"], L["sel0"])
+        blocks = []     # (instructions, predecessors' tail for hazard checks)
+        refits = []
+        code = []
+
+        def emit_block(insts, pre=()):
+            out, _ = add_waits(insts)
+            out, nops = fix_hazards(out, pre=pre)
+            code.extend(out)
+            return out
+
+        pro_out = emit_block(pro)
+        f0, r = self.step(0, "fast", "f0"); refits += r
+        f1, r = self.step(1, "fast", "f1"); refits += r
+        m0, r = self.step(0, "masked", "m0"); refits += r
+        m1, r = self.step(1, "masked", "m1"); refits += r
+        la0, r = self.step(0, "last", "l0"); refits += r
+        la1, r = self.step(1, "last", "l1"); refits += r
+        I = Inst
+        tailpad = [nop(15)]   # block entries: every predecessor ends with a barrier / branch; pad anyway
+        code.append(label(L["fast0"]))
+        emit_block(f0, pre=tailpad)
+        code += [I(f"s_cmp_gt_i32 s{S_N}, s{S_NF2}", SALU), I(f"s_cbranch_scc1 {L['sel1']}", BRANCH)]
+        code.append(label(L["fast1"]))
+        emit_block(f1, pre=tailpad)
+        code += [I(f"s_cmp_le_i32 s{S_N}, s{S_NF2}", SALU), I(f"s_cbranch_scc1 {L['fast0']}", BRANCH)]
+        code.append(label(L["sel0"]))
+        code += [I(f"s_cmp_eq_u32 s{S_N}, s{S_NL1}", SALU), I(f"s_cbranch_scc1 {L['last0']}", BRANCH)]
+        code.append(label(L["masked0"]))
+        emit_block(m0, pre=tailpad)
+        code.append(label(L["sel1"]))
+        code += [I(f"s_cmp_eq_u32 s{S_N}, s{S_NL1}", SALU), I(f"s_cbranch_scc1 {L['last1']}", BRANCH)]
+        code.append(label(L["masked1"]))
+        emit_block(m1, pre=tailpad)
+        code += [I(f"s_branch {L['sel0']}", BRANCH)]
+        code.append(label(L["last0"]))
+        emit_block(la0, pre=tailpad)
+        code += [I(f"s_branch {l_epi}", BRANCH)]
+        code.append(label(L["last1"]))
+        emit_block(la1, pre=tailpad)
+        code.append(label(l_epi))
+        emit_block([nop(15)] + self.epilogue(), pre=tailpad)
+        code.append(label(self.lab_end))
+        code.append(I("s_endpgm", SOPP))
+        for rb in refits:
+            code.extend(rb)
+        return code
+
+    def render(self):
+        code = self.build()
+        out = []
+        out.append(f"\t.globl {self.name}")
+        out.append("\t.p2align 8")
+        out.append(f"\t.type {self.name},@function")
+        out.append(f"{self.name}:")
+        nm = 0
+        for ins in code:
+            if ins.kind == LABEL:
+                out.append(ins.text)
+            else:
+                out.append("\t" + ins.text)
+                nm += ins.kind == MFMA
+        out.append(f".L{self.name}_fend:")
+        out.append(f"\t.size {self.name}, .L{self.name}_fend-{self.name}")
+        return "\n".join(out)
+
+    def descriptor(self):
+        return f"""
+	.rodata
+	.p2align 6
+	.amdhsa_kernel {self.name}
+		.amdhsa_group_segment_fixed_size {LDS_BYTES}
+		.amdhsa_private_segment_fixed_size 0
+		.amdhsa_kernarg_size {KARG_SIZE}
+		.amdhsa_user_sgpr_count 2
+		.amdhsa_user_sgpr_kernarg_segment_ptr 1
+		.amdhsa_system_sgpr_workgroup_id_x 1
+		.amdhsa_system_vgpr_workitem_id 0
+		.amdhsa_next_free_vgpr 512
+		.amdhsa_next_free_sgpr {NSGPR}
+		.amdhsa_accum_offset 256
+		.amdhsa_reserve_vcc 1
+		.amdhsa_float_denorm_mode_32 3
+		.amdhsa_float_denorm_mode_16_64 3
+		.amdhsa_dx10_clamp 1
+		.amdhsa_ieee_mode 0
+	.end_amdhsa_kernel
+	.text
+"""
+
+    def metadata(self):
+        return f"""  - .agpr_count: 256
+    .args:
+      - .offset: 0
+        .size: {KARG_SIZE}
+        .value_kind: by_value
+    .group_segment_fixed_size: {LDS_BYTES}
+    .kernarg_segment_align: 8
+    .kernarg_segment_size: {KARG_SIZE}
+    .max_flat_workgroup_size: 256
+    .name: {self.name}
+    .private_segment_fixed_size: 0
+    .sgpr_count: {NSGPR + 2}
+    .sgpr_spill_count: 0
+    .symbol: {self.name}.kd
+    .uniform_work_group_size: 1
+    .vgpr_count: 512
+    .vgpr_spill_count: 0
+    .wavefront_size: 64
+"""
+
+
+def main():
+    kernels = [K(bf, ca) for bf in (True, False) for ca in (True, False)]
+    out = ['\t.amdgcn_target "amdgcn-amd-amdhsa--gfx950"', "\t.amdhsa_code_object_version 5", "\t.text"]
+    for k in kernels:
+        out.append(k.render())
+        out.append(k.descriptor())
+    out.append("\t.amdgpu_metadata\n---\namdhsa.kernels:")
+    for k in kernels:
+        out.append(k.metadata().rstrip("\n"))
+    out.append("amdhsa.target: amdgcn-amd-amdhsa--gfx950\namdhsa.version:\n  - 1\n  - 2\n...\n\t.end_amdgpu_metadata")
+    sys.stdout.write("\n".join(out) + "\n")
+
+
+if __name__ == "__main__":
+    main()

@@ -347,24 +347,6 @@ __global__ void __launch_bounds__(DkdvTile<D>::NW * 64, 1) bwd_dkdv_kernel(const
   // slice at `a1` (query on registers, key on lane), chains started from `init`
   auto phase1 = [&](int a1, f32x16_t (&sp)[NQT]) {
     const TileAddr ta(lb, a1);
-#ifdef FA_PH1_OLD
-    constexpr int G = KS >= 4 ? (NQT == 2 ? KS / 2 : KS / 4) : KS;   // A fragments in flight per group
-    static_for<0, KS / G>([&](auto GG) {
-      constexpr int g0 = decltype(GG)::value * G;
-      i16x8_t af[NQT][G];
-      static_for<0, G>([&](auto KK) {
-        constexpr int ks = g0 + decltype(KK)::value;
-        static_for<0, NQT>([&](auto QT) {
-          constexpr int qt = decltype(QT)::value;
-          af[qt][ks - g0] = row_read_c<BQ, 32 * qt, 2 * ks>(smem, ta);
-        });
-      });
-#pragma unroll
-      for (int k = 0; k < G; ++k)
-#pragma unroll
-        for (int qt = 0; qt < NQT; ++qt) sp[qt] = E::mfma(af[qt][k], kv[g0 + k], sp[qt]);
-    });
-#else
     // Software-pipelined: the A fragments of k-group g+1 are requested before the MFMAs of group g
     // (sched_barrier keeps the scheduler from sinking the reads next to their MFMAs, which left
     // each LDS read's latency exposed in front of its two MFMAs).
@@ -392,7 +374,6 @@ __global__ void __launch_bounds__(DkdvTile<D>::NW * 64, 1) bwd_dkdv_kernel(const
         for (int qt = 0; qt < NQT; ++qt) sp[qt] = E::mfma(af[gg & 1][qt][k], kv[gg * G + k], sp[qt]);
       __builtin_amdgcn_sched_barrier(0);
     });
-#endif
   };
   // phase 2: acc += A^T frag, transposed A operand of the slice tile at `a2`; the fragments of
   // d-group dt+1 are requested before the MFMAs of group dt
@@ -460,11 +441,7 @@ __global__ void __launch_bounds__(DkdvTile<D>::NW * 64, 1) bwd_dkdv_kernel(const
             }
             x = fast_exp2(out ? kNegInf : sc * c);
           } else {
-#ifdef FA_ABL_NOEXP
-            x = sp[qi][4 * u + j] * c;   // ablation (wrong results): no exp
-#else
             x = fast_exp2(sp[qi][4 * u + j] * c);
-#endif
           }
           if constexpr (DROPOUT) {
             const bool keep = dropout_keep(rb[u], j, s.keep_u8);
@@ -490,12 +467,7 @@ __global__ void __launch_bounds__(DkdvTile<D>::NW * 64, 1) bwd_dkdv_kernel(const
       f32x16_t x;
 #pragma unroll
       for (int u = 0; u < 4; ++u) {
-#ifdef FA_ABL_NOPREAD
-        const f32x4_t pv = {0.5f, 0.5f, 0.5f, 0.5f};   // ablation (wrong results): no P exchange read
-        (void)xw;
-#else
         const f32x4_t pv = *(const f32x4_t*)(xw + qi * XTILE + u * 1024);
-#endif
         if constexpr (DROPOUT) {
           const f32x4_t dv = *(const f32x4_t*)(dl + 32 * qi + 8 * u + 4 * hh);
 #pragma unroll
@@ -654,26 +626,16 @@ __global__ void __launch_bounds__(DkdvTile<D>::NW * 64, 1) bwd_dkdv_kernel(const
         if constexpr (MASKED) d = dma_plan(slice_head(nxt), slice_q0(nxt), it + 1);
         else d = dma_plan(nhd, (m_first + nqi) * BQ, it + 1);
       }
-#ifndef FA_ABL_NODMA
       if (more) dma_part(d, std::integral_constant<int, 0>{}, NPC);
-#endif
       auto dma = [&](auto KC) {
-#ifndef FA_ABL_NODMA
         if (more) dma_part(d, KC, NPC);
-#endif
       };
       FA_STAMP(1);
       const int q0 = MASKED ? slice_q0(cur) : (m_first + cq) * BQ;
       const int it_head = MASKED ? slice_head(cur) : chd;   // query head of this slice within the group
       body(it, q0, it_head, dma);
       FA_STAMP(5);
-#if defined(FA_ABL_NODMAWAIT)
-      lds_barrier();   // ablation (wrong results): DMA never waited for
-#elif defined(FA_ABL_NOBARRIER)
-      wait_vmcnt(0);   // ablation (wrong results): no workgroup barrier
-#else
       wait_dma_keep_and_barrier(0);
-#endif
       FA_STAMP(6);
       if constexpr (MASKED) sd = nxt;
       else {
@@ -721,18 +683,12 @@ __global__ void __launch_bounds__(DkdvTile<D>::NW * 64, 1) bwd_dkdv_kernel(const
         p_fused(it, qs, os, xw_of(it), sp);
       } else {
         i16x8_t fr[2 * NQT];
-#ifndef FA_ABL_NOPH1
         phase1(qs, sp);                       // S' = Q K^T - LSE/scale
-#endif
         FA_STAMP(3);
         if (fast) p_step(std::false_type{}, sp, q0, it_head, xw_of(it), fr);
         else p_step(std::true_type{}, sp, q0, it_head, xw_of(it), fr);
         FA_STAMP(4);
-#ifndef FA_ABL_NOPH2
         phase2(os, fr);                       // dV^T += dO^T P
-#else
-        acc[0] = E::mfma(fr[0], fr[1], acc[0]);   // keep fr live
-#endif
       }
     });
   } else {
@@ -748,17 +704,11 @@ __global__ void __launch_bounds__(DkdvTile<D>::NW * 64, 1) bwd_dkdv_kernel(const
       if constexpr (kPos & 1) dma(std::integral_constant<int, kP1>{});
       FA_STAMP(2);
       chain_init(it, sp);
-#ifndef FA_ABL_NOPH1
       phase1(os, sp);                         // dP'' = D - dO V^T
-#endif
       if constexpr (kPos & 2) dma(std::integral_constant<int, kP2>{});
       FA_STAMP(3);
       FA_STAMP(4);
-#ifndef FA_ABL_NOPH2
       if (it > 0) phase2(((it + 2) % 3) * QSLOT, fr);   // dK''^T += Q(it-1)^T dS''(it-1)
-#else
-      if (it > 0) acc[0] = E::mfma(fr[0], fr[1], acc[0]);
-#endif
     });
     if (nlive > 0) {   // the last slice's dK update (no DMA after it: its Q is resident)
       i16x8_t fr[2 * NQT];
@@ -913,7 +863,6 @@ __global__ void __launch_bounds__(DqTile<D>::NW * 64, DqTile<D>::MINB) bwd_dq_ke
       for (int t = 0; t < NT; ++t) dropout_block_bytes<false>(dscr + t * 1024, pseed, doff, wq0, n0 + 32 * t, lane);
     }
     f32x16_t st[NT], pt[NT];
-#ifndef FA_DQ_PIPE   // the pipelined form below spills at 256 VGPRs (113 registers): off
     static_for<0, NT>([&](auto T) {
       constexpr int t = decltype(T)::value;
 #pragma unroll
@@ -933,43 +882,6 @@ __global__ void __launch_bounds__(DqTile<D>::NW * 64, DqTile<D>::MINB) bwd_dq_ke
         }
       });
     });
-#else
-    // Software-pipelined over (subtile, k-pair) groups: the K / V fragments of group g+1 are
-    // requested before the MFMAs of group g (with the reads sunk next to their MFMAs, every LDS read
-    // waited at lgkmcnt(0) in front of one MFMA).
-    {
-      constexpr int G2 = 2;                    // k-steps per group
-      constexpr int NGK = KS / G2;             // groups per subtile
-      constexpr int NG = NT * NGK;
-      i16x8_t fa[2][2 * G2];                   // [buffer][ka0, va0, ka1, va1]
-      auto load = [&](auto GC, i16x8_t (&dst)[2 * G2]) {
-        constexpr int g = decltype(GC)::value;
-        constexpr int t = g / NGK, k0 = (g % NGK) * G2;
-        static_for<0, G2>([&](auto KK) {
-          constexpr int k = decltype(KK)::value;
-          dst[2 * k] = row_read_c<BN, t * 32, 2 * (k0 + k)>(smem, tk);
-          dst[2 * k + 1] = row_read_c<BN, t * 32, 2 * (k0 + k)>(smem, tv);
-        });
-      };
-#pragma unroll
-      for (int t = 0; t < NT; ++t)
-#pragma unroll
-        for (int g = 0; g < 16; ++g) { st[t][g] = 0.f; pt[t][g] = -dsum_q; }
-      load(std::integral_constant<int, 0>{}, fa[0]);
-      static_for<0, NG>([&](auto GG) {
-        constexpr int g = decltype(GG)::value;
-        constexpr int t = g / NGK, k0 = (g % NGK) * G2;
-        if constexpr (g + 1 < NG) load(std::integral_constant<int, g + 1>{}, fa[(g + 1) & 1]);
-        __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-        for (int k = 0; k < G2; ++k) {
-          st[t] = E::mfma(fa[g & 1][2 * k], qf[k0 + k], st[t]);
-          pt[t] = E::mfma(fa[g & 1][2 * k + 1], of[k0 + k], pt[t]);
-        }
-        __builtin_amdgcn_sched_barrier(0);
-      });
-    }
-#endif
 #pragma unroll
     for (int t = 0; t < NT; ++t) {
       unsigned rb[4];

@@ -40,7 +40,7 @@ typedef __attribute__((ext_vector_type(2))) unsigned u32x2_t;
 typedef __attribute__((address_space(3))) i16x4_t lds_i16x4_t;
 
 constexpr float kNegInf = -__builtin_huge_valf();
-// forward online softmax (fa_fwd.hip, fa_fwd_w4.hip)
+// forward online softmax (fa_fwd.hip; the assembly forward uses the same constants, asm/gen_fwd.py)
 constexpr float kFwdRescaleThr = 8.f;   // deferred-max threshold, log2 units (P <= 256)
 constexpr float kFwdSumThr = 256.f;     // fast-path guard on a lane's per-tile sum of P (= 2^8)
 constexpr float kLog2e = 1.4426950408889634f;

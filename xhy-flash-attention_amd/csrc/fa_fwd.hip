@@ -444,11 +444,7 @@ __global__ void __launch_bounds__(FwdTile<D>::NW * 64, FwdTile<D>::MINB) fwd_ker
     const int n0 = nb * BN;
     const int a3 = next_live(a2);
     if (a3 < nblk) issue_at(a3, pos + 3);
-#ifdef FA_ABL_NOGEN
-    const bool active = false;   // ablation (wrong results): general-path tiles not computed
-#else
     const bool active = (wq0 < sq) && (!CAUSAL || n0 <= wq0 + 31);
-#endif
     if (active) {
       gen_bytes(n0);
       f32x16_t st[NT];
@@ -638,8 +634,8 @@ template <bool BF16, int D, bool CAUSAL, bool DROPOUT>
 static void run_fwd(const FwdParams& p, hipStream_t stream) {
   dim3 grid(p.s.b * p.s.h * p.num_m_blocks);   // 1-D: heads fastest, heaviest query block first
   prof_begin(kTimeFwd, stream);
-  if constexpr (!DROPOUT && (D == 64 || D == 128) && FwdTile<D>::BM == 256) {   // the same 256-row blocks
-    if (launch_fwd_w4(p, BF16, stream)) {   // 4 waves x 64 rows (fa_fwd_w4.hip)
+  if constexpr (!DROPOUT && D == 128) {   // hand-scheduled assembly kernel (fa_fwd_asm.cpp)
+    if (launch_fwd_asm(p, BF16, stream)) {
       prof_end(kTimeFwd, stream);
       return;
     }

@@ -1,0 +1,180 @@
+// Host side of the hand-scheduled assembly forward (csrc/asm/gen_fwd.py -> fa_fwd_asm.s, assembled
+// for gfx950 and embedded in this library as a code object).
+//
+// The kernel covers the headline path: head dim 128, bf16 / fp16, causal or not, fixed length or
+// varlen (cu_seqlens, varlen_padded_input), GQA, no dropout / mask / return_softmax / split-KV.
+// Everything else -- and this path when it is switched off -- goes to fwd_kernel (fa_fwd.hip).
+//
+// Loading: the embedded code object is loaded with hipModuleLoadData once per device (first call),
+// and its four kernels are launched with hipModuleLaunchKernel on the caller's stream; kernel
+// arguments are one packed struct (FwdAsmArgs, the layout gen_fwd.py's prologue reads).
+//
+// Work order: a per-shape table maps workgroup -> (batch, head, kv head, query block), built on the
+// host in the HIP kernel's order (heaviest causal block first, heads fastest, xcd_order_grouped for
+// K/V streams beyond the Infinity Cache) and cached in device memory per (device, shape).
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+#include <cstdlib>
+#include <cstring>
+#include <map>
+#include <mutex>
+#include <stdexcept>
+#include <string>
+#include <tuple>
+#include <vector>
+
+#include "fa_params.h"
+
+extern "C" const unsigned char fa_fwd_asm_co[];
+extern "C" const unsigned long fa_fwd_asm_co_size;
+
+namespace fa {
+namespace {
+
+// must match the kernarg loads of gen_fwd.py (K.prologue) and KARG_SIZE
+struct FwdAsmArgs {
+  const void* q; const void* k; const void* v; void* o; float* lse;
+  const uint32_t* sched; const int* cu_q; const int* cu_k;
+  uint64_t* rng; uint64_t seed, offset;
+  int64_t q_batch, k_batch, v_batch, o_batch;                       // bytes
+  int32_t q_row, kv_row, o_row, q_head, k_head, v_head, o_head;    // bytes
+  int32_t sq, sk, lse_pitch, h;
+  float c;
+  int32_t flags;    // bit 0: varlen_padded_input
+  int32_t pad;
+};
+static_assert(sizeof(FwdAsmArgs) == 176, "FwdAsmArgs layout");
+
+constexpr int kMaxDev = 64;
+struct DevModule {
+  hipModule_t mod = nullptr;
+  hipFunction_t fn[4] = {};   // [bf16 causal, bf16 full, f16 causal, f16 full]
+  std::map<std::tuple<int, int, int, int, int>, uint32_t*> tables;
+};
+std::mutex g_mu;
+DevModule g_dev[kMaxDev];
+int g_enabled = -1;   // -1: not read yet
+
+const char* kNames[4] = {"fa_fwd_asm_d128_bf16_causal", "fa_fwd_asm_d128_bf16_full",
+                         "fa_fwd_asm_d128_f16_causal", "fa_fwd_asm_d128_f16_full"};
+
+void check(hipError_t e, const char* what) {
+  if (e != hipSuccess) throw std::runtime_error(std::string("flash_attn_fwd (asm path): ") + what + ": " + hipGetErrorString(e));
+}
+
+DevModule& module_for(int dev) {
+  if (dev < 0 || dev >= kMaxDev) throw std::runtime_error("flash_attn_fwd (asm path): device index out of range");
+  DevModule& m = g_dev[dev];
+  if (m.mod == nullptr) {
+    check(hipModuleLoadData(&m.mod, fa_fwd_asm_co), "hipModuleLoadData");
+    for (int i = 0; i < 4; ++i) check(hipModuleGetFunction(&m.fn[i], m.mod, kNames[i]), kNames[i]);
+  }
+  return m;
+}
+
+// workgroup -> (bidb | head << 16, kvh | m_block << 16), the order of xcd_order_grouped (fa_common.h)
+std::vector<uint32_t> build_table(int b, int h, int hk, int nmb, int hp) {
+  const int nbh = b * h;
+  const long long n = (long long)nbh * nmb;
+  std::vector<uint32_t> t((size_t)n * 2);
+  const int g = h / hk;
+  for (long long L = 0; L < n; ++L) {
+    int bh, blk;
+    if ((nbh & 7) == 0 && hp > 0 && ((nbh >> 3) % hp) == 0) {
+      const long long i = L >> 3;
+      const long long per_group = (long long)hp * nmb;
+      const long long gi = i / per_group;
+      const long long r = i - gi * per_group;
+      blk = (int)(r / hp);
+      const long long hl = gi * hp + (r - (long long)blk * hp);
+      bh = (int)(hl * 8 + (L & 7));
+    } else {
+      blk = (int)(L / nbh);
+      bh = (int)(L - (long long)blk * nbh);
+    }
+    const int mb = nmb - 1 - blk;   // heaviest causal query block first
+    const int bidb = bh / h, head = bh - bidb * h;
+    t[2 * L] = (uint32_t)bidb | ((uint32_t)head << 16);
+    t[2 * L + 1] = (uint32_t)(head / g) | ((uint32_t)mb << 16);
+  }
+  return t;
+}
+
+bool fits32(int64_t x) { return x >= 0 && x < (1ll << 31); }
+
+}  // namespace
+
+void fwd_asm_enable(int on) {
+  std::lock_guard<std::mutex> lk(g_mu);
+  g_enabled = on ? 1 : 0;
+}
+
+bool launch_fwd_asm(const FwdParams& p, bool is_bf16, hipStream_t stream) {
+  const AttnShape& s = p.s;
+  {
+    std::lock_guard<std::mutex> lk(g_mu);
+    if (g_enabled < 0) {   // FLASH_ATTN_MI355X_FWD_ASM=1 switches the path on (read once)
+      const char* e = std::getenv("FLASH_ATTN_MI355X_FWD_ASM");
+      g_enabled = (e != nullptr && e[0] == '1') ? 1 : 0;
+    }
+    if (!g_enabled) return false;
+  }
+  if (s.d != 128 || s.dropout || s.mask != nullptr || s.fm_lts != nullptr || p.p_out != nullptr ||
+      p.n_split != 0 || p.pack_g != 1)
+    return false;
+  if (p.k_row != p.v_row) return false;   // the K and V DMA share per-lane offsets
+  if (s.b > 65535 || s.h > 65535 || p.num_m_blocks > 65535 || s.h % s.hk != 0) return false;
+  const int64_t q_row = 2 * p.q_row, kv_row = 2 * p.k_row, o_row = 2 * p.o_row;
+  const int64_t q_head = 2 * p.q_head, k_head = 2 * p.k_head, v_head = 2 * p.v_head, o_head = 2 * p.o_head;
+  for (int64_t x : {q_row, kv_row, o_row, q_head, k_head, v_head, o_head})
+    if (!fits32(x)) return false;
+  // K / V records of one (sequence, kv head) and the per-tile offsets must stay below 2^31 bytes
+  if (!fits32(((int64_t)s.seqlen_k + 64) * kv_row)) return false;
+  if (!fits32((int64_t)256 * (q_row > o_row ? q_row : o_row))) return false;
+
+  int dev = 0;
+  check(hipGetDevice(&dev), "hipGetDevice");
+  const long long nwg = (long long)s.b * s.h * p.num_m_blocks;
+  if (nwg <= 0) return true;
+  if (nwg > 0x7fffffff) return false;
+  hipFunction_t fn;
+  uint32_t* table;
+  {
+    std::lock_guard<std::mutex> lk(g_mu);
+    DevModule& m = module_for(dev);
+    fn = m.fn[(is_bf16 ? 0 : 2) + (s.causal ? 0 : 1)];
+    auto key = std::make_tuple(s.b, s.h, s.hk, p.num_m_blocks, p.head_group);
+    auto it = m.tables.find(key);
+    if (it == m.tables.end()) {
+      std::vector<uint32_t> t = build_table(s.b, s.h, s.hk, p.num_m_blocks, p.head_group);
+      uint32_t* d = nullptr;
+      check(hipMalloc(&d, t.size() * sizeof(uint32_t)), "hipMalloc (schedule table)");
+      check(hipMemcpy(d, t.data(), t.size() * sizeof(uint32_t), hipMemcpyHostToDevice), "hipMemcpy (schedule table)");
+      it = m.tables.emplace(key, d).first;
+    }
+    table = it->second;
+  }
+  FwdAsmArgs a;
+  std::memset(&a, 0, sizeof(a));
+  a.q = p.q; a.k = p.k; a.v = p.v; a.o = p.o; a.lse = p.lse;
+  a.sched = table;
+  a.cu_q = s.cu_seqlens_q; a.cu_k = s.cu_seqlens_k;
+  a.rng = p.rng_state; a.seed = p.seed; a.offset = p.offset;
+  a.q_batch = 2 * p.q_batch; a.k_batch = 2 * p.k_batch; a.v_batch = 2 * p.v_batch; a.o_batch = 2 * p.o_batch;
+  a.q_row = (int32_t)q_row; a.kv_row = (int32_t)kv_row; a.o_row = (int32_t)o_row;
+  a.q_head = (int32_t)q_head; a.k_head = (int32_t)k_head; a.v_head = (int32_t)v_head; a.o_head = (int32_t)o_head;
+  a.sq = s.seqlen_q; a.sk = s.seqlen_k; a.lse_pitch = s.lse_pitch; a.h = s.h;
+  a.c = s.scale_log2;
+  a.flags = s.varlen_padded_input ? 1 : 0;
+  size_t sz = sizeof(a);
+  void* cfg[] = {HIP_LAUNCH_PARAM_BUFFER_POINTER, &a, HIP_LAUNCH_PARAM_BUFFER_SIZE, &sz, HIP_LAUNCH_PARAM_END};
+  check(hipModuleLaunchKernel(fn, (unsigned)nwg, 1, 1, 256, 1, 1, 0, stream, nullptr, cfg), "hipModuleLaunchKernel");
+  return true;
+}
+
+}  // namespace fa
+
+// Test / A-B hook: 0 routes every forward to fwd_kernel (HIP), 1 lets launch_fwd use the assembly
+// kernel where it applies (the default; FLASH_ATTN_MI355X_FWD_ASM=0 sets 0 at the first launch).
+extern "C" void flash_attn_fwd_use_asm(int on) { fa::fwd_asm_enable(on); }

@@ -135,7 +135,9 @@ struct RotaryParams {
 
 // Host launchers (fa_fwd.hip / fa_bwd.hip).  Throw std::runtime_error on invalid configuration.
 void launch_fwd(const FwdParams& p, bool is_bf16, hipStream_t stream);
-bool launch_fwd_w4(const FwdParams& p, bool is_bf16, hipStream_t stream);   // fa_fwd_w4.hip
+// fa_fwd_asm.cpp: the assembly forward (d = 128, no dropout / mask); false when it does not apply
+bool launch_fwd_asm(const FwdParams& p, bool is_bf16, hipStream_t stream);
+void fwd_asm_enable(int on);
 void launch_bwd(const BwdParams& p, bool is_bf16, hipStream_t stream);
 void launch_reduced_scores(const ReducedParams& p, bool is_bf16, hipStream_t stream);
 void launch_rotary(const RotaryParams& p, bool interleaved, bool conj, bool is_bf16, hipStream_t stream);
