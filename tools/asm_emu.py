@@ -136,6 +136,10 @@ class Emu:
         self.heap = heap
         self.count = 0
         self.mfma_count = 0
+        self.trace_labels = None   # substrings of labels to log (wave, label) when reached
+        self.hooks = {}            # label -> fn(emu, wave) called when a wave reaches it
+        self.trace = []
+        self.label_at = {v: k for k, v in self.labels.items()}
 
     # ---------------------------------------------------------------- operands
     def reg_index(self, tok):
@@ -235,6 +239,12 @@ class Emu:
                 raise RuntimeError("deadlock")
 
     def step(self, w, lds):
+        if self.hooks and w.pc in self.label_at and self.label_at[w.pc] in self.hooks:
+            self.hooks[self.label_at[w.pc]](self, w)
+        if self.trace_labels is not None and w.pc in self.label_at:
+            name = self.label_at[w.pc]
+            if any(t in name for t in self.trace_labels) and not name.endswith('_back'):
+                self.trace.append((w.wid, name))
         op, a, mods, text = self.insts[w.pc]
         w.pc += 1
         self.count += 1
@@ -360,6 +370,8 @@ class Emu:
                 return np.minimum(I_(a[1]), I_(a[2])).view(np.uint32)
             if base == "v_bfe_u32":
                 return (U(a[1]) >> U(a[2])) & ((np.uint32(1) << U(a[3])) - 1)
+            if base == "v_cvt_f32_u32":
+                return f2u(U(a[1]).astype(np.float32))
             if base == "v_fma_f32":
                 return f2u(np.float32(F(a[1]).astype(np.float64) * F(a[2]) + F(a[3])))
             if base == "v_exp_f32":

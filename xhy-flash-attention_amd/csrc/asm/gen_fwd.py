@@ -39,7 +39,7 @@ import os
 import sys
 
 sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
-from isa import (ACCR, ACCW, BARRIER, BRANCH, DMA, LABEL, LDS, MFMA, NOP, PERM, SALU, SMEM, SOPP,  # noqa: E402
+from isa import (ACCR, ACCW, BARRIER, BRANCH, DMA, LABEL, LDS, MFMA, NOP, PERM, RFL, SALU, SMEM, SOPP,  # noqa: E402
                  TRANS, VALU, VLOAD, VSTORE, WAIT, Counters, Inst, add_waits, ar, fix_hazards, label, nop,
                  rtxt, schedule, sr, vr)
 
@@ -119,6 +119,10 @@ KARG_SIZE = 176
 # dev A/B switches, read when the .s is generated (tools/asm_variant.sh)
 OPT_NOZERO = os.environ.get("FA_GEN_NOZERO") == "1"          # never zero K/V record counts
 OPT_ZERO_NOP = int(os.environ.get("FA_GEN_ZERO_NOP", "0"))    # s_nop 15 x N before zeroing them
+# debug: at the named point, workgroup 0 stores every register of each wave (and wave 0 the LDS) to
+# the buffer whose address is passed as the `seed` kernarg, then ends (tools/asm_dump.py)
+OPT_DUMP = os.environ.get("FA_GEN_DUMP")
+DUMP_SLOTS = 512 + 128   # per wave: v0..v255, a0..a255, s0..s127 -- 256 bytes (64 lanes) each
 
 
 class K:
@@ -325,7 +329,12 @@ class K:
                 fy.append(self.kread(f, f % 8, key=-19 + f, earliest=22 + 2 * f))
             rl_a = self.lab(f"{tag}_refit_a")
             refits.append(self.refit(0, SA, PA(p ^ 1), rl_a, tile_add=64, phase="end"))
-            fy += self.guard_ops(0, rl_a, key=700)
+            # after the phase's LAST MFMA: refit_a borrows the V fragment ring as scratch and rescales
+            # O_a, so no PV MFMA may still be pending (placed earlier, it corrupted the d-tile 3 MFMAs)
+            ga = self.guard_ops(0, rl_a, key=700)
+            for op in ga:
+                op.eg = 31
+            fy += ga
         # V read slot of the next tile
         fy += [Inst(f"s_add_u32 s{S_VOFF}, s{S_VOFF}, {TILE}", SALU, rd=sr(S_VOFF), wr=sr(S_VOFF) + [("scc", 0)], key=800, earliest=28),
                Inst(f"s_sub_u32 s{t + 2}, s{S_VOFF}, {NSLOT * TILE}", SALU, rd=sr(S_VOFF), wr=sr(t + 2) + [("scc", 0)], key=801),
@@ -406,6 +415,47 @@ class K:
         out, _ = fix_hazards(out)
         return out
 
+    def dump(self, point):
+        """register / LDS dump of workgroup 0 at `point` (OPT_DUMP), then s_endpgm"""
+        if OPT_DUMP != point:
+            return []
+        I = Inst
+        D, SO, SW = 96, 90, 91
+        ins = [Inst("s_waitcnt vmcnt(0) lgkmcnt(0)", WAIT), nop(15), nop(15),
+               I(f"s_mov_b32 s{D}, s{S_KA + 18}", SALU), I(f"s_and_b32 s{D + 1}, s{S_KA + 19}, 0xffff", SALU),
+               I(f"s_cmp_eq_u32 s2, 0", SALU), I(f"s_cselect_b32 s{D + 2}, 0x7fffffff, 0", SALU),
+               I(f"s_mov_b32 s{D + 3}, 0x20000", SALU),
+               I(f"s_mul_i32 s{SW}, s{S_WAVE}, {DUMP_SLOTS * 256}", SALU),
+               I(f"v_lshlrev_b32_e32 v255, 2, v{V_LANE}", VALU), nop(4)]
+        # SGPRs first (their copies go through v254)
+        for i in range(128):
+            if i >= NSGPR and i not in (D, D + 1, D + 2, D + 3):
+                continue
+            src = f"s{i}" if i < 102 else None
+            if src is None:
+                continue
+            ins += [I(f"v_mov_b32_e32 v254, {src}", VALU), I(f"s_add_u32 s{SO}, s{SW}, {(512 + i) * 256}", SALU), nop(1),
+                    I(f"buffer_store_dword v254, v255, s[{D}:{D + 3}], s{SO} offen", VSTORE), nop(1)]
+        for i in range(254):
+            ins += [I(f"s_add_u32 s{SO}, s{SW}, {i * 256}", SALU), nop(1),
+                    I(f"buffer_store_dword v{i}, v255, s[{D}:{D + 3}], s{SO} offen", VSTORE)]
+        for i in range(256):
+            ins += [I(f"v_accvgpr_read_b32 v254, a{i}", ACCR), I(f"s_add_u32 s{SO}, s{SW}, {(256 + i) * 256}", SALU), nop(1),
+                    I(f"buffer_store_dword v254, v255, s[{D}:{D + 3}], s{SO} offen", VSTORE), nop(1)]
+        # LDS (wave 0): 160 KiB after the 4 waves' register slots
+        l_skip = self.lab("dumpskip")
+        ins += [I(f"s_cmp_lg_u32 s{S_WAVE}, 0", SALU), I(f"s_cbranch_scc1 {l_skip}", BRANCH),
+                I("v_lshlrev_b32_e32 v253, 4, v{0}".format(V_LANE), VALU), nop(4)]
+        for blk in range(LDS_BYTES // 1024):
+            if blk % 64 == 0 and blk:
+                ins += [I("v_add_u32_e32 v253, 0x10000, v253", VALU), nop(4)]
+            ins += [I(f"ds_read_b128 v[0:3], v253 offset:{(blk % 64) * 1024}", LDS), Inst("s_waitcnt lgkmcnt(0)", WAIT),
+                    I(f"s_mov_b32 s{SO}, {4 * DUMP_SLOTS * 256 + blk * 1024}", SALU),
+                    I(f"v_lshlrev_b32_e32 v252, 4, v{V_LANE}", VALU), nop(1),
+                    I(f"buffer_store_dwordx4 v[0:3], v252, s[{D}:{D + 3}], s{SO} offen", VSTORE), nop(2)]
+        ins += [label(l_skip), Inst("s_waitcnt vmcnt(0)", WAIT), I("s_endpgm", SOPP)]
+        return ins
+
     def half_max(self, x, tmp):
         """x = max over the two lane halves (lanes l, l^32 hold the same query)"""
         return [Inst(f"v_mov_b32_e32 v{tmp}, v{x}", VALU, rd=vr(x), wr=vr(tmp)),
@@ -438,7 +488,7 @@ class K:
         T0, T1, T2, T3 = S_TMP, S_TMP + 1, S_TMP + 2, S_TMP + 3
         # wave index, lane values
         ins += [I("v_lshrrev_b32_e32 v1, 6, v0", VALU, rd=vr(0), wr=vr(1)),
-                I(f"v_readfirstlane_b32 s{S_WAVE}, v1", VALU, rd=vr(1), wr=sr(S_WAVE)),
+                I(f"v_readfirstlane_b32 s{S_WAVE}, v1", RFL, rd=vr(1), wr=sr(S_WAVE)),
                 I(f"v_and_b32_e32 v{V_LANE}, 63, v0", VALU, rd=vr(0), wr=vr(V_LANE))]
         # rng_state (block 0, wave 0): {seed, offset}; lanes >= 1 fall outside the 16-byte record
         l_norng = self.lab("norng")
@@ -682,6 +732,7 @@ class K:
                     I(f"s_add_u32 s{S_DT}, s{S_DT}, 1", SALU, rd=sr(S_DT), wr=sr(S_DT))]
         # Q + tiles 0, 1, 2 landed (tile 3 in flight; K(2) is prefetched during step 0)
         ins += [I("s_waitcnt vmcnt(8)", WAIT), I("s_barrier", BARRIER)]
+        ins += self.dump("pro_lds")
         # ---- tile 0: S(0, a), S(0, b) -> masked, explicit row max, P(0, a)
         ins += [I(f"v_add_u32_e32 v{V_KB0}, 0, v{V_RB0}", VALU, rd=vr(V_RB0), wr=vr(V_KB0)),
                 I(f"v_add_u32_e32 v{V_KB1}, 0, v{V_RB1}", VALU, rd=vr(V_RB1), wr=vr(V_KB1))]
@@ -698,6 +749,7 @@ class K:
         body = schedule(mfm, reads)
         ins += body
         ins.append(nop(15))
+        ins += self.dump("pro_qk")
         for j, sreg in ((0, SA), (1, SB(0))):
             ins += self.mask_ops(j, sreg, (S_N0, 0), V_LM)
             mx = V_T + 2
@@ -717,6 +769,7 @@ class K:
         sm, _ = self.softmax_ops(0, SA, PA(0), False, None, key0=0)
         ins += sm
         ins += [Inst(f"v_mov_b32_e32 v{V_L[0]}, v{V_PS[0]}", VALU, rd=vr(V_PS[0]), wr=vr(V_L[0]))]
+        ins += self.dump("pro_end")
         # entry (S_KOFF addresses tile n+1 = 1 at step 0; the LAST step's refit takes S_KOFF - TILE)
         ins += [I(f"s_mov_b32 s{S_KOFF}, {TILE}", SALU, wr=sr(S_KOFF)),
                 I(f"s_cmp_eq_u32 s{S_NBLK}, 1", SALU, rd=sr(S_NBLK), wr=[("scc", 0)]),
@@ -792,7 +845,7 @@ class K:
         I = Inst
         tailpad = [nop(15)]   # block entries: every predecessor ends with a barrier / branch; pad anyway
         code.append(label(L["fast0"]))
-        emit_block(f0, pre=tailpad)
+        emit_block(f0 + self.dump("f0_end"), pre=tailpad)
         code += [I(f"s_cmp_gt_i32 s{S_N}, s{S_NF2}", SALU), I(f"s_cbranch_scc1 {L['sel1']}", BRANCH)]
         code.append(label(L["fast1"]))
         emit_block(f1, pre=tailpad)
@@ -800,14 +853,14 @@ class K:
         code.append(label(L["sel0"]))
         code += [I(f"s_cmp_eq_u32 s{S_N}, s{S_NL1}", SALU), I(f"s_cbranch_scc1 {L['last0']}", BRANCH)]
         code.append(label(L["masked0"]))
-        emit_block(m0, pre=tailpad)
+        emit_block(m0 + self.dump("m0_end"), pre=tailpad)
         code.append(label(L["sel1"]))
         code += [I(f"s_cmp_eq_u32 s{S_N}, s{S_NL1}", SALU), I(f"s_cbranch_scc1 {L['last1']}", BRANCH)]
         code.append(label(L["masked1"]))
         emit_block(m1, pre=tailpad)
         code += [I(f"s_branch {L['sel0']}", BRANCH)]
         code.append(label(L["last0"]))
-        emit_block(la0, pre=tailpad)
+        emit_block(la0 + self.dump("l0_end"), pre=tailpad)
         code += [I(f"s_branch {l_epi}", BRANCH)]
         code.append(label(L["last1"]))
         emit_block(la1, pre=tailpad)

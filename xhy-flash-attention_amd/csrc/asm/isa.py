@@ -5,19 +5,21 @@ reads and writes; the verifier walks the final instruction order and inserts the
 requires between dependent instructions (the rules below are the ones LLVM's hazard recognizer
 applies for gfx950, confirmed by compiling probe kernels with hipcc: VALU write -> MFMA read 2,
 8-pass XDL write -> VALU read 12 (`s_nop 11`), transcendental -> VALU use 1, VALU write ->
-v_permlane read 2, SALU M0 write -> LDS-DMA 1, VALU SGPR write -> VMEM read 5).  The counter pass
+v_permlane read 2, VALU write -> v_readfirstlane read 1, SALU M0 write -> LDS-DMA 1, VALU SGPR
+write -> VMEM read 5).  The v_readfirstlane rule was learnt the hard way: without it the wave index
+was read stale on hardware, which misplaced every LDS-DMA piece (tools/probe_gen.py, asm_dump.py).  The counter pass
 inserts `s_waitcnt lgkmcnt(N)` / `vmcnt(N)` before the first reader of a register that a still
 outstanding LDS or VMEM load writes, counted (only the loads that have to land are waited for).
 """
 
 # instruction kinds
 MFMA, VALU, TRANS, PERM, ACCR, ACCW, SALU, SMEM, LDS, DMA, VLOAD, VSTORE, WAIT, NOP, BRANCH, LABEL, \
-    BARRIER, SOPP = range(18)
-VALU_LIKE = (VALU, TRANS, PERM, ACCR, ACCW)
+    BARRIER, SOPP, RFL = range(19)
+VALU_LIKE = (VALU, TRANS, PERM, ACCR, ACCW, RFL)
 
 # issue cost in cycles (one wave alone on its SIMD; MI355X_MICROARCH.md per-instruction constants)
 COST = {MFMA: 8, VALU: 4, TRANS: 8, PERM: 4, ACCR: 4, ACCW: 4, SALU: 2, SMEM: 2, LDS: 2, DMA: 8,
-        VLOAD: 4, VSTORE: 4, WAIT: 1, NOP: 4, BRANCH: 2, LABEL: 0, BARRIER: 4, SOPP: 2}
+        VLOAD: 4, VSTORE: 4, WAIT: 1, NOP: 4, BRANCH: 2, LABEL: 0, BARRIER: 4, SOPP: 2, RFL: 4}
 
 
 def vr(i, n=1):
@@ -80,6 +82,7 @@ XDL_RAW = 12      # 8-pass XDL (v_mfma_f32_32x32x16_*) write -> any non-chain ac
 VALU_MFMA = 2     # VALU / v_accvgpr_write write -> MFMA read
 TRANS_USE = 1
 VALU_PERM = 2
+VALU_RFL = 1      # VALU write -> v_readfirstlane / v_readlane read of that VGPR
 M0_DMA = 1
 VSGPR_VMEM = 5
 STORE_WAR = 2     # buffer_store_dwordx4 data -> VALU overwrite
@@ -106,6 +109,8 @@ def required(prev, cur):
         need = max(need, TRANS_USE)
     if prev.kind in VALU_LIKE and cur.kind == PERM and prev.wr & cur.rd:
         need = max(need, VALU_PERM)
+    if prev.kind in VALU_LIKE and cur.kind == RFL and prev.wr & cur.rd:
+        need = max(need, VALU_RFL)
     if prev.kind == SALU and ("m0", 0) in prev.wr and cur.kind == DMA:
         need = max(need, M0_DMA)
     if prev.kind in VALU_LIKE and cur.kind in (DMA, VLOAD, VSTORE, SMEM):

@@ -27,6 +27,8 @@
 //     their accumulators are directly the B operands of dV^T = dO^T P and dK^T = Q^T dS; dO^T and
 //     Q^T come from the row-major LDS slice through ds_read_b64_tr_b16.
 //   * Slices that need no mask skip the mask arithmetic (one wave-uniform test per slice).
+#include <cstdlib>
+#include <mutex>
 #include <stdexcept>
 #include <string>
 
@@ -1006,28 +1008,80 @@ __global__ void __launch_bounds__(DqTile<D>::NW * 64, DqTile<D>::MINB) bwd_dq_ke
 }
 
 // ------------------------------------------------------------------------------------------------
+// dK/dV and dQ are independent once bwd_pre_kernel has written D and -LSE/scale, so dQ runs on a
+// second stream of the device, forked from and joined back into the caller's stream with events:
+// the two kernels' causal tails overlap instead of adding up (the reference launches its three
+// backward kernels serially, flash_bwd_launch_template.h:49-88).  FLASH_ATTN_MI355X_BWD_OVERLAP=0
+// (read once) or flash_attn_bwd_overlap(0) keeps both on the caller's stream.
+namespace {
+struct SideStream {
+  hipStream_t s = nullptr;
+  hipEvent_t fork = nullptr, join = nullptr;
+};
+std::mutex g_side_mu;
+SideStream g_side[64];
+int g_overlap = -1;
+}  // namespace
+
+void bwd_overlap_enable(int on) {
+  std::lock_guard<std::mutex> lk(g_side_mu);
+  g_overlap = on ? 1 : 0;
+}
+
 template <bool BF16, int D, bool CAUSAL, bool DROPOUT>
 static void run_bwd(const BwdParams& p, hipStream_t stream) {
   const int nheads_grid = p.gqa_reduce ? p.s.hk : p.s.h;
   const bool masked = p.s.mask != nullptr || p.s.fm_lts != nullptr;
-  {
+  auto dkdv = [&](hipStream_t st) {
     dim3 grid(p.s.b * nheads_grid * p.num_n_blocks);   // 1-D, xcd_order
-    prof_begin(kTimeBwdMain, stream);
+    prof_begin(kTimeBwdMain, st);
     if (masked)
-      hipLaunchKernelGGL((bwd_dkdv_kernel<BF16, D, CAUSAL, DROPOUT, true>), grid, dim3(DkdvTile<D>::NW * 64), 0, stream, p);
+      hipLaunchKernelGGL((bwd_dkdv_kernel<BF16, D, CAUSAL, DROPOUT, true>), grid, dim3(DkdvTile<D>::NW * 64), 0, st, p);
     else
-      hipLaunchKernelGGL((bwd_dkdv_kernel<BF16, D, CAUSAL, DROPOUT, false>), grid, dim3(DkdvTile<D>::NW * 64), 0, stream, p);
-    prof_end(kTimeBwdMain, stream);
-  }
-  {
+      hipLaunchKernelGGL((bwd_dkdv_kernel<BF16, D, CAUSAL, DROPOUT, false>), grid, dim3(DkdvTile<D>::NW * 64), 0, st, p);
+    prof_end(kTimeBwdMain, st);
+  };
+  auto dq = [&](hipStream_t st) {
     dim3 grid(p.s.b * p.s.h * ((p.s.seqlen_q + DqTile<D>::BM - 1) / DqTile<D>::BM));
-    prof_begin(kTimeBwdDq, stream);
+    prof_begin(kTimeBwdDq, st);
     if (masked)
-      hipLaunchKernelGGL((bwd_dq_kernel<BF16, D, CAUSAL, DROPOUT, true>), grid, dim3(DqTile<D>::NW * 64), 0, stream, p);
+      hipLaunchKernelGGL((bwd_dq_kernel<BF16, D, CAUSAL, DROPOUT, true>), grid, dim3(DqTile<D>::NW * 64), 0, st, p);
     else
-      hipLaunchKernelGGL((bwd_dq_kernel<BF16, D, CAUSAL, DROPOUT, false>), grid, dim3(DqTile<D>::NW * 64), 0, stream, p);
-    prof_end(kTimeBwdDq, stream);
+      hipLaunchKernelGGL((bwd_dq_kernel<BF16, D, CAUSAL, DROPOUT, false>), grid, dim3(DqTile<D>::NW * 64), 0, st, p);
+    prof_end(kTimeBwdDq, st);
+  };
+  std::unique_lock<std::mutex> lk(g_side_mu);
+  if (g_overlap < 0) {
+    const char* e = std::getenv("FLASH_ATTN_MI355X_BWD_OVERLAP");
+    g_overlap = (e != nullptr && e[0] == '0') ? 0 : 1;
   }
+  int dev = 0;
+  SideStream* ss = nullptr;
+  if (g_overlap && hipGetDevice(&dev) == hipSuccess && dev >= 0 && dev < 64) {
+    ss = &g_side[dev];
+    if (ss->s == nullptr) {
+      if (hipStreamCreateWithFlags(&ss->s, hipStreamNonBlocking) != hipSuccess ||
+          hipEventCreateWithFlags(&ss->fork, hipEventDisableTiming) != hipSuccess ||
+          hipEventCreateWithFlags(&ss->join, hipEventDisableTiming) != hipSuccess)
+        throw std::runtime_error("flash_attn_bwd: creating the dQ stream failed");
+    }
+  }
+  prof_begin(kTimeBwdBoth, stream);
+  if (ss == nullptr) {
+    lk.unlock();
+    dkdv(stream);
+    dq(stream);
+  } else {
+    // fork: dQ waits for everything queued on the caller's stream so far (bwd_pre_kernel)
+    if (hipEventRecord(ss->fork, stream) != hipSuccess || hipStreamWaitEvent(ss->s, ss->fork, 0) != hipSuccess)
+      throw std::runtime_error("flash_attn_bwd: stream fork failed");
+    dkdv(stream);
+    dq(ss->s);
+    // join: the caller's stream continues after dQ
+    if (hipEventRecord(ss->join, ss->s) != hipSuccess || hipStreamWaitEvent(stream, ss->join, 0) != hipSuccess)
+      throw std::runtime_error("flash_attn_bwd: stream join failed");
+  }
+  prof_end(kTimeBwdBoth, stream);
 }
 
 template <bool BF16, bool CAUSAL, bool DROPOUT>
@@ -1037,7 +1091,9 @@ static void dispatch_bwd_d(const BwdParams& p, hipStream_t stream) {
   else if (d <= 64) run_bwd<BF16, 64, CAUSAL, DROPOUT>(p, stream);
   else if (d <= 96) run_bwd<BF16, 96, CAUSAL, DROPOUT>(p, stream);
   else if (d <= 128) run_bwd<BF16, 128, CAUSAL, DROPOUT>(p, stream);
+  else if (d <= 160) run_bwd<BF16, 160, CAUSAL, DROPOUT>(p, stream);   // dedicated tiles (reference hdim160)
   else if (d <= 192) run_bwd<BF16, 192, CAUSAL, DROPOUT>(p, stream);
+  else if (d <= 224) run_bwd<BF16, 224, CAUSAL, DROPOUT>(p, stream);   // (reference hdim224)
   else if (d <= 256) run_bwd<BF16, 256, CAUSAL, DROPOUT>(p, stream);
   else throw std::runtime_error("flash_attn_bwd: head dim " + std::to_string(d) + " > 256");
 }

@@ -665,7 +665,9 @@ static void dispatch_d(const FwdParams& p, hipStream_t stream) {
   else if (d <= 64) run_fwd<BF16, 64, CAUSAL, DROPOUT>(p, stream);
   else if (d <= 96) run_fwd<BF16, 96, CAUSAL, DROPOUT>(p, stream);
   else if (d <= 128) run_fwd<BF16, 128, CAUSAL, DROPOUT>(p, stream);
+  else if (d <= 160) run_fwd<BF16, 160, CAUSAL, DROPOUT>(p, stream);   // dedicated tiles (reference hdim160)
   else if (d <= 192) run_fwd<BF16, 192, CAUSAL, DROPOUT>(p, stream);
+  else if (d <= 224) run_fwd<BF16, 224, CAUSAL, DROPOUT>(p, stream);   // (reference hdim224)
   else if (d <= 256) run_fwd<BF16, 256, CAUSAL, DROPOUT>(p, stream);
   else throw std::runtime_error("flash_attn_fwd: head dim " + std::to_string(d) + " > 256");
 }

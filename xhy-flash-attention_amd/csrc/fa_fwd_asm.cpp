@@ -114,9 +114,9 @@ bool launch_fwd_asm(const FwdParams& p, bool is_bf16, hipStream_t stream) {
   const AttnShape& s = p.s;
   {
     std::lock_guard<std::mutex> lk(g_mu);
-    if (g_enabled < 0) {   // FLASH_ATTN_MI355X_FWD_ASM=1 switches the path on (read once)
+    if (g_enabled < 0) {   // FLASH_ATTN_MI355X_FWD_ASM=0 switches the path off (read once)
       const char* e = std::getenv("FLASH_ATTN_MI355X_FWD_ASM");
-      g_enabled = (e != nullptr && e[0] == '1') ? 1 : 0;
+      g_enabled = (e != nullptr && e[0] == '0') ? 0 : 1;
     }
     if (!g_enabled) return false;
   }
@@ -178,3 +178,6 @@ bool launch_fwd_asm(const FwdParams& p, bool is_bf16, hipStream_t stream) {
 // Test / A-B hook: 0 routes every forward to fwd_kernel (HIP), 1 lets launch_fwd use the assembly
 // kernel where it applies (the default; FLASH_ATTN_MI355X_FWD_ASM=0 sets 0 at the first launch).
 extern "C" void flash_attn_fwd_use_asm(int on) { fa::fwd_asm_enable(on); }
+// Test / A-B hook: 0 runs the backward's dQ kernel after dK/dV on the caller's stream, 1 (default)
+// overlaps them on two streams (fa_bwd.hip run_bwd).
+extern "C" void flash_attn_bwd_overlap(int on) { fa::bwd_overlap_enable(on); }

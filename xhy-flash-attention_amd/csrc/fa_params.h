@@ -139,6 +139,7 @@ void launch_fwd(const FwdParams& p, bool is_bf16, hipStream_t stream);
 bool launch_fwd_asm(const FwdParams& p, bool is_bf16, hipStream_t stream);
 void fwd_asm_enable(int on);
 void launch_bwd(const BwdParams& p, bool is_bf16, hipStream_t stream);
+void bwd_overlap_enable(int on);   // fa_bwd.hip: dQ on a second stream (default on)
 void launch_reduced_scores(const ReducedParams& p, bool is_bf16, hipStream_t stream);
 void launch_rotary(const RotaryParams& p, bool interleaved, bool conj, bool is_bf16, hipStream_t stream);
 
@@ -147,7 +148,8 @@ void fwd_block_size(int d, int* block_m, int* block_n);
 void bwd_block_size(int d, int* block_m, int* block_n);
 
 // Optional HIP-event timing around each kernel launch (fa_timing.cpp).
-enum TimedKernel { kTimeFwd = 0, kTimeBwdPre = 1, kTimeBwdMain = 2 /* dK/dV */, kTimeBwdDq = 3, kNumTimedKernels = 4 };
+enum TimedKernel { kTimeFwd = 0, kTimeBwdPre = 1, kTimeBwdMain = 2 /* dK/dV */, kTimeBwdDq = 3,
+                   kTimeBwdBoth = 4 /* dK/dV + dQ window */, kNumTimedKernels = 5 };
 void prof_begin(int id, hipStream_t s);
 void prof_end(int id, hipStream_t s);
 

@@ -21,7 +21,7 @@ std::vector<Pending> g_pending;
 std::vector<hipEvent_t> g_pool;
 double g_ms[kNumTimedKernels] = {};
 long g_count[kNumTimedKernels] = {};
-thread_local hipEvent_t t_start = nullptr;
+thread_local hipEvent_t t_start[kNumTimedKernels] = {};   // per id: windows may overlap
 
 hipEvent_t take() {
   if (!g_pool.empty()) { hipEvent_t e = g_pool.back(); g_pool.pop_back(); return e; }
@@ -47,17 +47,18 @@ void prof_begin(int id, hipStream_t s) {
   (void)id;
   if (!g_on) return;
   std::lock_guard<std::mutex> lk(g_mu);
-  t_start = take();
-  (void)hipEventRecord(t_start, s);
+  if (id < 0 || id >= kNumTimedKernels) return;
+  t_start[id] = take();
+  (void)hipEventRecord(t_start[id], s);
 }
 
 void prof_end(int id, hipStream_t s) {
-  if (!g_on || t_start == nullptr) return;
+  if (!g_on || id < 0 || id >= kNumTimedKernels || t_start[id] == nullptr) return;
   std::lock_guard<std::mutex> lk(g_mu);
   hipEvent_t e = take();
   (void)hipEventRecord(e, s);
-  g_pending.push_back({t_start, e, id});
-  t_start = nullptr;
+  g_pending.push_back({t_start[id], e, id});
+  t_start[id] = nullptr;
   if (g_pending.size() > 4096) drain_locked();
 }
 
@@ -76,7 +77,8 @@ void flash_attn_timing_enable(int enable) {
 }
 
 // Total device milliseconds and launch count of kernel `id` since the last enable
-// (0 fwd, 1 bwd_pre, 2 bwd_dkdv, 3 bwd_dq).  Synchronises on the recorded events.
+// (0 fwd, 1 bwd_pre, 2 bwd_dkdv, 3 bwd_dq, 4 the dK/dV + dQ window: both kernels, which overlap on
+// two streams).  Synchronises on the recorded events.
 void flash_attn_timing_read(int id, double* total_ms, long* count) {
   std::lock_guard<std::mutex> lk(fa::g_mu);
   fa::drain_locked();
