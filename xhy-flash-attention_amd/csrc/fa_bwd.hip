@@ -1008,14 +1008,16 @@ __global__ void __launch_bounds__(DqTile<D>::NW * 64, DqTile<D>::MINB) bwd_dq_ke
 }
 
 // ------------------------------------------------------------------------------------------------
-// dK/dV and dQ are independent once bwd_pre_kernel has written D and -LSE/scale, so dQ runs on a
-// second stream of the device, forked from and joined back into the caller's stream with events:
-// the two kernels' causal tails overlap instead of adding up (the reference launches its three
-// backward kernels serially, flash_bwd_launch_template.h:49-88).  FLASH_ATTN_MI355X_BWD_OVERLAP=0
-// (read once) or flash_attn_bwd_overlap(0) keeps both on the caller's stream.
+// dK/dV and dQ are independent once bwd_pre_kernel has written D and -LSE/scale, so they can run
+// on two streams of the device, forked from and joined back into the caller's stream with events,
+// and the two kernels' causal tails overlap instead of adding up (the reference launches its three
+// backward kernels serially, flash_bwd_launch_template.h:49-88).  Modes (FLASH_ATTN_MI355X_BWD_OVERLAP,
+// read once, or flash_attn_bwd_overlap(mode)): 0 both on the caller's stream (default: measured
+// faster at C3, DESIGN.md "dQ overlap"), 1 dQ on a second stream of the same priority, 2 dQ on a
+// lowest-priority stream, 3 dK/dV on a highest-priority stream and dQ on the caller's.
 namespace {
 struct SideStream {
-  hipStream_t s = nullptr;
+  hipStream_t s[3] = {nullptr, nullptr, nullptr};   // per mode 1..3
   hipEvent_t fork = nullptr, join = nullptr;
 };
 std::mutex g_side_mu;
@@ -1023,9 +1025,9 @@ SideStream g_side[64];
 int g_overlap = -1;
 }  // namespace
 
-void bwd_overlap_enable(int on) {
+void bwd_overlap_enable(int mode) {
   std::lock_guard<std::mutex> lk(g_side_mu);
-  g_overlap = on ? 1 : 0;
+  g_overlap = (mode >= 0 && mode <= 3) ? mode : 0;
 }
 
 template <bool BF16, int D, bool CAUSAL, bool DROPOUT>
@@ -1053,32 +1055,46 @@ static void run_bwd(const BwdParams& p, hipStream_t stream) {
   std::unique_lock<std::mutex> lk(g_side_mu);
   if (g_overlap < 0) {
     const char* e = std::getenv("FLASH_ATTN_MI355X_BWD_OVERLAP");
-    g_overlap = (e != nullptr && e[0] == '0') ? 0 : 1;
+    g_overlap = (e != nullptr && e[0] >= '1' && e[0] <= '3' && e[1] == 0) ? e[0] - '0' : 0;
   }
+  const int mode = g_overlap;
   int dev = 0;
+  hipStream_t side = nullptr;
   SideStream* ss = nullptr;
-  if (g_overlap && hipGetDevice(&dev) == hipSuccess && dev >= 0 && dev < 64) {
+  if (mode > 0 && hipGetDevice(&dev) == hipSuccess && dev >= 0 && dev < 64) {
     ss = &g_side[dev];
-    if (ss->s == nullptr) {
-      if (hipStreamCreateWithFlags(&ss->s, hipStreamNonBlocking) != hipSuccess ||
-          hipEventCreateWithFlags(&ss->fork, hipEventDisableTiming) != hipSuccess ||
-          hipEventCreateWithFlags(&ss->join, hipEventDisableTiming) != hipSuccess)
-        throw std::runtime_error("flash_attn_bwd: creating the dQ stream failed");
+    if (ss->fork == nullptr &&
+        (hipEventCreateWithFlags(&ss->fork, hipEventDisableTiming) != hipSuccess ||
+         hipEventCreateWithFlags(&ss->join, hipEventDisableTiming) != hipSuccess))
+      throw std::runtime_error("flash_attn_bwd: creating the fork/join events failed");
+    if (ss->s[mode - 1] == nullptr) {
+      int least = 0, greatest = 0;
+      if (hipDeviceGetStreamPriorityRange(&least, &greatest) != hipSuccess)
+        throw std::runtime_error("flash_attn_bwd: stream priority range query failed");
+      const int prio = mode == 1 ? 0 : mode == 2 ? least : greatest;
+      if (hipStreamCreateWithPriority(&ss->s[mode - 1], hipStreamNonBlocking, prio) != hipSuccess)
+        throw std::runtime_error("flash_attn_bwd: creating the side stream failed");
     }
+    side = ss->s[mode - 1];
   }
   prof_begin(kTimeBwdBoth, stream);
-  if (ss == nullptr) {
+  if (side == nullptr) {
     lk.unlock();
     dkdv(stream);
     dq(stream);
   } else {
-    // fork: dQ waits for everything queued on the caller's stream so far (bwd_pre_kernel)
-    if (hipEventRecord(ss->fork, stream) != hipSuccess || hipStreamWaitEvent(ss->s, ss->fork, 0) != hipSuccess)
+    // fork: the side stream waits for everything queued on the caller's stream so far (bwd_pre_kernel)
+    if (hipEventRecord(ss->fork, stream) != hipSuccess || hipStreamWaitEvent(side, ss->fork, 0) != hipSuccess)
       throw std::runtime_error("flash_attn_bwd: stream fork failed");
-    dkdv(stream);
-    dq(ss->s);
-    // join: the caller's stream continues after dQ
-    if (hipEventRecord(ss->join, ss->s) != hipSuccess || hipStreamWaitEvent(stream, ss->join, 0) != hipSuccess)
+    if (mode == 3) {
+      dkdv(side);
+      dq(stream);
+    } else {
+      dkdv(stream);
+      dq(side);
+    }
+    // join: the caller's stream continues after the side stream's kernel
+    if (hipEventRecord(ss->join, side) != hipSuccess || hipStreamWaitEvent(stream, ss->join, 0) != hipSuccess)
       throw std::runtime_error("flash_attn_bwd: stream join failed");
   }
   prof_end(kTimeBwdBoth, stream);

@@ -178,6 +178,6 @@ bool launch_fwd_asm(const FwdParams& p, bool is_bf16, hipStream_t stream) {
 // Test / A-B hook: 0 routes every forward to fwd_kernel (HIP), 1 lets launch_fwd use the assembly
 // kernel where it applies (the default; FLASH_ATTN_MI355X_FWD_ASM=0 sets 0 at the first launch).
 extern "C" void flash_attn_fwd_use_asm(int on) { fa::fwd_asm_enable(on); }
-// Test / A-B hook: 0 runs the backward's dQ kernel after dK/dV on the caller's stream, 1 (default)
-// overlaps them on two streams (fa_bwd.hip run_bwd).
-extern "C" void flash_attn_bwd_overlap(int on) { fa::bwd_overlap_enable(on); }
+// Test / A-B hook: 0 (default) runs the backward's dQ kernel after dK/dV on the caller's stream,
+// 1..3 overlap them on two streams (fa_bwd.hip run_bwd lists the modes).
+extern "C" void flash_attn_bwd_overlap(int mode) { fa::bwd_overlap_enable(mode); }
