@@ -412,9 +412,24 @@ void flash_attn_block_size(int head_size, int is_backward, int * block_m, int * 
 
 /* Per-kernel device timing with HIP events on the launch stream (benchmarking only; not under
  * graph capture).  enable != 0 clears the totals and starts recording.  Kernel ids: 0 forward,
- * 1 backward preprocess (D = rowsum(dO*O)), 2 backward dK/dV, 3 backward dQ. */
+ * 1 backward preprocess (D = rowsum(dO*O)), 2 backward dK/dV, 3 backward dQ, 4 the window from
+ * the dK/dV launch to the end of dQ (the two may overlap on two streams). */
 void flash_attn_timing_enable(int enable);
 void flash_attn_timing_read(int kernel_id, double * total_ms, long * count);
+
+/* Test / A-B switches (no reference counterpart).  Knob ids: 0 never split K/V in the forward
+ * (FLASH_ATTN_MI355X_NO_SPLITKV), 1 head-fastest work order (FLASH_ATTN_MI355X_NO_XCD_GROUP),
+ * 2 XCD head-grouping threshold in MiB of streamed K/V (FLASH_ATTN_MI355X_XCD_GROUP_MIN_MIB,
+ * default 256).  Each is read from its environment variable once, at first use. */
+void flash_attn_set_knob(int id, int value);
+int flash_attn_get_knob(int id);
+/* 0 routes every forward to the HIP kernel, 1 (default) lets head dim 128 take the assembly
+ * kernel (FLASH_ATTN_MI355X_FWD_ASM=0 sets 0). */
+void flash_attn_fwd_use_asm(int on);
+/* Backward dQ / dK-dV stream overlap: 0 (default) serial on the caller's stream, 1 dQ on a second
+ * stream, 2 dQ on a lowest-priority stream, 3 dK/dV on a highest-priority stream
+ * (FLASH_ATTN_MI355X_BWD_OVERLAP). */
+void flash_attn_bwd_overlap(int mode);
 
 #ifdef __cplusplus
 }

@@ -1,0 +1,31 @@
+"""Launcher switches of the library (include/flash_attn.h flash_attn_set_knob), for the GPU tests
+that compare a launch path with its alternative (the library reads them from the environment once;
+a test sets and restores them through the C entry point instead)."""
+import contextlib
+import ctypes
+
+NO_SPLITKV, NO_XCD_GROUP, XCD_GROUP_MIN_MIB = 0, 1, 2
+
+
+def _lib():
+    import flash_attn_2_cuda as m
+    lib = m._lib
+    lib.flash_attn_set_knob.argtypes = [ctypes.c_int, ctypes.c_int]
+    lib.flash_attn_get_knob.argtypes = [ctypes.c_int]
+    lib.flash_attn_get_knob.restype = ctypes.c_int
+    return lib
+
+
+@contextlib.contextmanager
+def knob(kid, value):
+    lib = _lib()
+    old = lib.flash_attn_get_knob(kid)
+    lib.flash_attn_set_knob(kid, value)
+    try:
+        yield
+    finally:
+        lib.flash_attn_set_knob(kid, old)
+
+
+def no_splitkv():
+    return knob(NO_SPLITKV, 1)

@@ -96,17 +96,19 @@ SEQ_PAIRS = [(113, 203), (128, 217), (113, 211), (108, 256), (256, 512), (512, 2
              (1024, 1024), (1023, 1024), (1024, 1023)]
 
 
-@pytest.mark.parametrize("kvpacked", [False, True])
+# (mha_type, kvpacked): the kvpacked layout is covered on GQA only (no skip-only combinations)
+LAYOUTS = [("mha", False), ("mqa", False), ("gqa", False), ("gqa", True)]
+LAYOUT_IDS = ["mha", "mqa", "gqa", "gqa-kvpacked"]
+
+
 @pytest.mark.parametrize("dtype", DTYPES)
-@pytest.mark.parametrize("mha_type", ["mha", "mqa", "gqa"])
+@pytest.mark.parametrize("mha_type,kvpacked", LAYOUTS, ids=LAYOUT_IDS)
 @pytest.mark.parametrize("causal", [False, True])
 @pytest.mark.parametrize("d", [32, 40, 59, 64, 80, 96, 111, 128, 160, 192, 224, 256])
 @pytest.mark.parametrize("seqlen_q,seqlen_k", SEQ_PAIRS)
-def test_flash_attn_output(seqlen_q, seqlen_k, d, causal, mha_type, dtype, kvpacked):
+def test_flash_attn_output(seqlen_q, seqlen_k, d, causal, mha_type, kvpacked, dtype):
     from flash_attn import flash_attn_func, flash_attn_kvpacked_func
 
-    if kvpacked and mha_type != "gqa":
-        pytest.skip("kvpacked covered on the gqa layout")
     torch.manual_seed(0)
     batch_size, nheads = 2, 6
     nheads_k = nheads if mha_type == "mha" else (1 if mha_type == "mqa" else 3)
@@ -164,17 +166,14 @@ def test_flash_attn_qkvpacked(seqlen, d, causal, dtype):
     _assert_bound("dqkv", dqkv, dref, dpt)
 
 
-@pytest.mark.parametrize("kvpacked", [False, True])
 @pytest.mark.parametrize("dtype", DTYPES)
-@pytest.mark.parametrize("mha_type", ["mha", "mqa", "gqa"])
+@pytest.mark.parametrize("mha_type,kvpacked", LAYOUTS, ids=LAYOUT_IDS)
 @pytest.mark.parametrize("causal", [False, True])
 @pytest.mark.parametrize("d", [32, 64, 96, 128, 160, 256])
 @pytest.mark.parametrize("seqlen_q,seqlen_k", [(113, 203), (128, 217), (256, 512), (512, 256), (1023, 1024)])
-def test_flash_attn_varlen_output(seqlen_q, seqlen_k, d, causal, mha_type, dtype, kvpacked):
+def test_flash_attn_varlen_output(seqlen_q, seqlen_k, d, causal, mha_type, kvpacked, dtype):
     from flash_attn import flash_attn_varlen_func, flash_attn_varlen_kvpacked_func
 
-    if kvpacked and mha_type != "gqa":
-        pytest.skip("kvpacked covered on the gqa layout")
     torch.manual_seed(0)
     batch_size, nheads = 4, 6
     nheads_k = nheads if mha_type == "mha" else (1 if mha_type == "mqa" else 3)
@@ -490,10 +489,11 @@ def test_fwd_deferred_max_forced(mode, causal, dtype):
 # ------------------------------------------------------------------------------------------------
 # XCD-grouped work order (fa_common.h xcd_order_grouped): launches whose K/V stream exceeds the
 # 256 MiB Infinity Cache run a head-grouped order; the result must be bitwise the head-fastest one
-# (FLASH_ATTN_MI355X_NO_XCD_GROUP=1, read per launch, forces that order).
+# (the NO_XCD_GROUP switch, tests/knobs.py, forces that order).
 # ------------------------------------------------------------------------------------------------
-def test_xcd_grouped_order_is_bitwise_head_fastest(monkeypatch):
+def test_xcd_grouped_order_is_bitwise_head_fastest():
     from flash_attn import flash_attn_func
+    from knobs import NO_XCD_GROUP, knob
 
     torch.manual_seed(0)
     # K + V = 402 MB > 256 MiB: grouped order for the forward and dQ kernels
@@ -503,10 +503,10 @@ def test_xcd_grouped_order_is_bitwise_head_fastest(monkeypatch):
     g = torch.randn_like(q)
     res = {}
     for flag in ("0", "1"):
-        monkeypatch.setenv("FLASH_ATTN_MI355X_NO_XCD_GROUP", flag)
-        out, lse, _ = flash_attn_func(q, k, v, causal=True, return_attn_probs=True)
-        dq, dk, dv = torch.autograd.grad(out, (q, k, v), g)
-        torch.cuda.synchronize()
+        with knob(NO_XCD_GROUP, int(flag)):
+            out, lse, _ = flash_attn_func(q, k, v, causal=True, return_attn_probs=True)
+            dq, dk, dv = torch.autograd.grad(out, (q, k, v), g)
+            torch.cuda.synchronize()
         res[flag] = (out, lse, dq, dk, dv)
     for name, a, b in zip(("out", "lse", "dq", "dk", "dv"), res["0"], res["1"]):
         assert torch.isfinite(a.float()).all(), name

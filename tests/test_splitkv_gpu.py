@@ -1,11 +1,12 @@
 """GPU tests of the split-KV forward (decode-time split-KV): launch_fwd splits the
 keys of decode-shaped, non-causal calls (fewer workgroups than CUs) across workgroups and merges
 the fp32 partials.  Checked against the fp32 oracle under the reference's 2x rule, LSE against
-the fp32 logsumexp, and against the unsplit kernel (FLASH_ATTN_MI355X_NO_SPLITKV=1, read per
-launch) to fp32-summation-order tolerance; the backward consumes the merged LSE unchanged."""
+the fp32 logsumexp, and against the unsplit kernel (the NO_SPLITKV switch, tests/knobs.py) to
+fp32-summation-order tolerance; the backward consumes the merged LSE unchanged."""
 import pytest
 import torch
 
+from knobs import no_splitkv
 from oracle.attention_ref import attention_ref, check_within_bound
 
 pytestmark = pytest.mark.gpu
@@ -22,7 +23,7 @@ def _need_gpu():
 @pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float16])
 @pytest.mark.parametrize("d", [64, 128, 256])
 @pytest.mark.parametrize("sq,sk,h,hk", [(1, 4096 + 17, 4, 2), (3, 2000, 2, 2), (64, 8192, 4, 1), (300, 1500, 1, 1)])
-def test_splitkv_forward(sq, sk, h, hk, d, dtype, monkeypatch):
+def test_splitkv_forward(sq, sk, h, hk, d, dtype):
     from flash_attn import flash_attn_func
     from flash_attn.flash_attn_interface import _flash_attn_forward
 
@@ -39,12 +40,11 @@ def test_splitkv_forward(sq, sk, h, hk, d, dtype, monkeypatch):
     kr = k.float().repeat_interleave(h // hk, dim=2)
     s = torch.einsum("bqhd,bkhd->bhqk", q.float(), kr) * d ** -0.5
     torch.testing.assert_close(lse, torch.logsumexp(s, -1), atol=1e-3, rtol=0)
-    monkeypatch.setenv("FLASH_ATTN_MI355X_NO_SPLITKV", "1")
-    out1, _, _, _, _, lse1, _, _ = _flash_attn_forward(q, k, v, 0.0, d ** -0.5, False, False)
+    with no_splitkv():
+        out1, _, _, _, _, lse1, _, _ = _flash_attn_forward(q, k, v, 0.0, d ** -0.5, False, False)
     torch.testing.assert_close(lse, lse1, atol=2e-5, rtol=0)
     tol = 2 ** -7 if dtype == torch.bfloat16 else 2 ** -10
     torch.testing.assert_close(out.float(), out1.float(), atol=tol, rtol=tol)
-    monkeypatch.delenv("FLASH_ATTN_MI355X_NO_SPLITKV")
     # backward through the split forward's LSE
     qg, kg, vg = (x.clone().requires_grad_() for x in (q, k, v))
     o = flash_attn_func(qg, kg, vg)
@@ -62,7 +62,7 @@ def test_splitkv_forward(sq, sk, h, hk, d, dtype, monkeypatch):
 
 
 @pytest.mark.parametrize("d", [64, 128])
-def test_gqa_packing_without_split(d, monkeypatch):
+def test_gqa_packing_without_split(d):
     """Many sequences (no split) with grouped heads: the packed launch alone (n_split = 1)."""
     from flash_attn.flash_attn_interface import _flash_attn_forward
 
@@ -76,7 +76,7 @@ def test_gqa_packing_without_split(d, monkeypatch):
     pt, _ = attention_ref(q, k, v, upcast=False, reorder_ops=True)
     ok, err, bound = check_within_bound(out, ref, pt)
     assert ok, (err, bound)
-    monkeypatch.setenv("FLASH_ATTN_MI355X_NO_SPLITKV", "1")
-    out1, _, _, _, _, lse1, _, _ = _flash_attn_forward(q, k, v, 0.0, d ** -0.5, False, False)
+    with no_splitkv():
+        out1, _, _, _, _, lse1, _, _ = _flash_attn_forward(q, k, v, 0.0, d ** -0.5, False, False)
     torch.testing.assert_close(lse, lse1, atol=2e-5, rtol=0)
     torch.testing.assert_close(out.float(), out1.float(), atol=2 ** -7, rtol=2 ** -7)

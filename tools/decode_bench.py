@@ -15,6 +15,8 @@ import torch
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, os.path.join(ROOT, "xhy-flash-attention_amd"))
 from flash_attn.flash_attn_interface import _flash_attn_forward  # noqa: E402
+sys.path.insert(0, os.path.join(ROOT, "tests"))
+from knobs import no_splitkv  # noqa: E402
 
 
 def time_fwd(q, k, v, iters=20):
@@ -37,9 +39,8 @@ def main():
         k = torch.randn(b, sk, hk, d, device="cuda", dtype=torch.bfloat16)
         v = torch.randn(b, sk, hk, d, device="cuda", dtype=torch.bfloat16)
         gb = 2 * b * sk * hk * d * 2 / 1e9
-        os.environ["FLASH_ATTN_MI355X_NO_SPLITKV"] = "1"
-        t0 = time_fwd(q, k, v)
-        os.environ.pop("FLASH_ATTN_MI355X_NO_SPLITKV")
+        with no_splitkv():
+            t0 = time_fwd(q, k, v)
         t1 = time_fwd(q, k, v)
         print(f"b={b} sq={sq} sk={sk} h={h} hk={hk}: unsplit {t0:.3f} ms ({gb / t0 * 1e3:.0f} GB/s), "
               f"split {t1:.3f} ms ({gb / t1 * 1e3:.0f} GB/s), speedup {t0 / t1:.2f}x")

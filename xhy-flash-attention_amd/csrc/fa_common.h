@@ -24,6 +24,8 @@
 
 #include <type_traits>
 
+#include "fa_params.h"
+
 namespace fa {
 
 typedef __attribute__((ext_vector_type(8))) __bf16 bf16x8_t;
@@ -443,14 +445,10 @@ inline void keep_pool_memory() {
 // (stream_bytes): below that the cache absorbs the re-reads of head-fastest order, which then keeps
 // the better causal balance (measured at C3, 256 MiB of K/V: grouping -1.5%; at C5, 1 GiB: +16% fwd,
 // +14% dQ).  causal = false: every block costs the same, one head per group.
-#ifndef FA_XCD_GROUP_MIN_BYTES   // dev switch (A/B): streams above this many bytes use grouping
-#define FA_XCD_GROUP_MIN_BYTES (256ll << 20)
-#endif
+// The threshold is the FLASH_ATTN_MI355X_XCD_GROUP_MIN_MIB knob (default 256), and
+// FLASH_ATTN_MI355X_NO_XCD_GROUP=1 forces head-fastest order (fa_params.h Knob: read once).
 inline int xcd_head_group(long long nbh, long long nblk, long long stream_bytes, bool causal) {
-  // test knob (read per launch): FLASH_ATTN_MI355X_NO_XCD_GROUP=1 -> head-fastest order
-  const char* e = std::getenv("FLASH_ATTN_MI355X_NO_XCD_GROUP");
-  const bool disabled = e != nullptr && e[0] == '1';
-  if (disabled || stream_bytes <= FA_XCD_GROUP_MIN_BYTES) return 0;
+  if (knob(kKnobNoXcdGroup) == 1 || stream_bytes <= ((long long)knob(kKnobXcdGroupMinMiB) << 20)) return 0;
   if (nbh % 8 != 0 || nbh <= 0 || nblk <= 0) return 0;
   if (!causal) return 1;
   const long long h8 = nbh / 8;

@@ -714,13 +714,12 @@ void launch_fwd(const FwdParams& p_in, bool is_bf16, hipStream_t stream) {
     int bm, bn;
     fwd_block_size(p.s.d, &bm, &bn);
     const int nblk = (p.s.seqlen_k + bn - 1) / bn;
-    const char* env = getenv("FLASH_ATTN_MI355X_NO_SPLITKV");
     const bool plain = !p.s.causal && !p.s.dropout && p.s.mask == nullptr && p.s.fm_lts == nullptr &&
                        p.p_out == nullptr && p.s.cu_seqlens_q == nullptr && p.s.cu_seqlens_k == nullptr;
     const int G = p.s.h / p.s.hk;
     const bool pack = plain && G > 1 && (long long)p.s.seqlen_q * G <= bm;
     const long long wgs = pack ? (long long)p.s.b * p.s.hk : (long long)p.s.b * p.s.h * p.num_m_blocks;
-    if (plain && !(env && env[0] == '1') && nblk > 0 && (pack || (wgs < 256 && nblk >= 8))) {
+    if (plain && knob(kKnobNoSplitKv) != 1 && nblk > 0 && (pack || (wgs < 256 && nblk >= 8))) {
       int ns = 1;
       if (wgs < 256 && nblk >= 8)
         ns = (int)std::min<long long>(64, std::min<long long>((512 + wgs - 1) / wgs, nblk / 4));

@@ -139,7 +139,7 @@ void launch_fwd(const FwdParams& p, bool is_bf16, hipStream_t stream);
 bool launch_fwd_asm(const FwdParams& p, bool is_bf16, hipStream_t stream);
 void fwd_asm_enable(int on);
 void launch_bwd(const BwdParams& p, bool is_bf16, hipStream_t stream);
-void bwd_overlap_enable(int on);   // fa_bwd.hip: dQ on a second stream (default on)
+void bwd_overlap_enable(int mode);   // fa_bwd.hip: dQ / dK-dV stream overlap mode (default 0: off)
 void launch_reduced_scores(const ReducedParams& p, bool is_bf16, hipStream_t stream);
 void launch_rotary(const RotaryParams& p, bool interleaved, bool conj, bool is_bf16, hipStream_t stream);
 
@@ -152,5 +152,14 @@ enum TimedKernel { kTimeFwd = 0, kTimeBwdPre = 1, kTimeBwdMain = 2 /* dK/dV */, 
                    kTimeBwdBoth = 4 /* dK/dV + dQ window */, kNumTimedKernels = 5 };
 void prof_begin(int id, hipStream_t s);
 void prof_end(int id, hipStream_t s);
+
+// Test / A-B switches of the launchers (fa_timing.cpp): each is read from its environment variable
+// once, at its first use, and can be set later through flash_attn_set_knob (not per launch).
+enum Knob { kKnobNoSplitKv = 0 /* FLASH_ATTN_MI355X_NO_SPLITKV: 1 = never split K/V */,
+            kKnobNoXcdGroup = 1 /* FLASH_ATTN_MI355X_NO_XCD_GROUP: 1 = head-fastest order */,
+            kKnobXcdGroupMinMiB = 2 /* FLASH_ATTN_MI355X_XCD_GROUP_MIN_MIB: grouping threshold */,
+            kNumKnobs = 3 };
+int knob(int id);
+void set_knob(int id, int value);
 
 }  // namespace fa

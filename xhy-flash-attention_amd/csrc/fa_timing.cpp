@@ -5,6 +5,9 @@
 // kernels themselves rather than from host wall time.  Not for use under graph capture.
 #include <hip/hip_runtime.h>
 
+#include <atomic>
+#include <climits>
+#include <cstdlib>
 #include <mutex>
 #include <vector>
 
@@ -88,3 +91,33 @@ void flash_attn_timing_read(int id, double* total_ms, long* count) {
 }
 
 }  // extern "C"
+
+// ---- launcher switches (fa_params.h Knob) ----
+namespace fa {
+namespace {
+struct KnobDef { const char* env; int dflt; };
+constexpr KnobDef kKnobs[kNumKnobs] = {{"FLASH_ATTN_MI355X_NO_SPLITKV", 0},
+                                       {"FLASH_ATTN_MI355X_NO_XCD_GROUP", 0},
+                                       {"FLASH_ATTN_MI355X_XCD_GROUP_MIN_MIB", 256}};
+std::atomic<int> g_knob[kNumKnobs] = {{INT_MIN}, {INT_MIN}, {INT_MIN}};
+}  // namespace
+
+int knob(int id) {
+  if (id < 0 || id >= kNumKnobs) return 0;
+  int v = g_knob[id].load(std::memory_order_relaxed);
+  if (v == INT_MIN) {
+    const char* e = std::getenv(kKnobs[id].env);
+    v = (e != nullptr && *e != 0) ? std::atoi(e) : kKnobs[id].dflt;
+    int expect = INT_MIN;
+    if (!g_knob[id].compare_exchange_strong(expect, v)) v = expect;
+  }
+  return v;
+}
+
+void set_knob(int id, int value) {
+  if (id >= 0 && id < kNumKnobs) g_knob[id].store(value);
+}
+}  // namespace fa
+
+extern "C" void flash_attn_set_knob(int id, int value) { fa::set_knob(id, value); }
+extern "C" int flash_attn_get_knob(int id) { return fa::knob(id); }
