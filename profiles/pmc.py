@@ -29,6 +29,8 @@ OURS = ("fwd_kernel", "bwd_pre_kernel", "bwd_dkdv_kernel", "bwd_dq_kernel", "spl
 def short(name):
     if name.startswith("fa_fwd_asm_"):   # the assembly forward (csrc/asm/gen_fwd.py) is the fwd_kernel slot
         return "fwd_kernel"
+    if name.startswith("fa_bwd_dkdv_asm_"):   # the assembly dK/dV kernel (gen_bwd.py)
+        return "bwd_dkdv_kernel"
     return name.split("(")[0].split("::")[-1].split("<")[0].strip()
 
 

@@ -128,6 +128,7 @@ class Wave:
         self.done = False
         self.at_barrier = False
         self.wid = wid
+        self.vm = []        # outstanding VMEM ops in issue order: LDS-DMA writes (dst, bytes) or None
 
 
 class Emu:
@@ -261,9 +262,23 @@ class Emu:
         I_ = lambda t: self.vsrc(w, t).view(np.int32)  # noqa: E731
         U = lambda t: self.vsrc(w, t)  # noqa: E731
         # ------------------------------------------------ scalar
-        if op == "s_nop" or op == "s_waitcnt" or op == "s_setprio":
+        if op == "s_waitcnt":
+            # LDS-DMA data lands as late as the program allows: at the wait that forces it
+            for t in a + [k for k in mods]:
+                if t.startswith("vmcnt("):
+                    n = int(t[6:-1])
+                    while len(w.vm) > n:
+                        e = w.vm.pop(0)
+                        if e is not None:
+                            lds[e[0]:e[0] + len(e[1])] = e[1]
+            return
+        if op == "s_nop" or op == "s_setprio":
             return
         if op == "s_endpgm":
+            for e in w.vm:
+                if e is not None:
+                    lds[e[0]:e[0] + len(e[1])] = e[1]
+            w.vm = []
             w.done = True
             return
         if op == "s_barrier":
@@ -498,7 +513,8 @@ class Emu:
             s[lo] = r
 
     def buffer(self, w, lds, op, a, mods):
-        n = {"buffer_load_dword": 1, "buffer_load_dwordx4": 4, "buffer_store_dword": 1, "buffer_store_dwordx4": 4}[op]
+        n = {"buffer_load_dword": 1, "buffer_load_dwordx4": 4, "buffer_store_dword": 1, "buffer_store_dwordx2": 2,
+             "buffer_store_dwordx4": 4}[op]
         if mods.get("lds"):       # buffer_load_* vaddr, srsrc, soffset ... lds (no data register)
             a = [None] + list(a)
         base, nrec = self.desc(w, a[2])
@@ -512,9 +528,10 @@ class Emu:
                 if ok[lane]:
                     data[lane] = self.mem_read(base + int(off[lane]), size).view(np.uint32)
             if mods.get("lds"):
-                for lane in range(64):
-                    dst = w.m0 + 16 * lane if n == 4 else w.m0 + 4 * lane
-                    lds[dst:dst + size] = data[lane].view(np.uint8)
+                # lands later (s_waitcnt vmcnt): a read before the wait sees the old LDS contents
+                dst = w.m0
+                w.vm.append((dst, np.ascontiguousarray(data).view(np.uint8).ravel().copy()))
+                return
             else:
                 ri, _ = self.regs(w, a[0])
                 w.r[ri:ri + n] = data.T
@@ -523,6 +540,8 @@ class Emu:
             for lane in range(64):
                 if ok[lane]:
                     self.heap.get(base + int(off[lane]), size)[:] = np.ascontiguousarray(w.r[ri:ri + n, lane]).view(np.uint8)
+        if not mods.get("lds"):
+            w.vm.append(None)
 
     def mfma(self, w, op, a):
         self.mfma_count += 1

@@ -1,0 +1,159 @@
+#!/usr/bin/env python3
+"""Runs the generated assembly dK / dV kernel (csrc/asm/gen_bwd.py) in the CPU emulator
+(tools/asm_emu.py) on small inputs and compares dK / dV with a float64 reference (dev / test tool).
+
+    python tools/emu_bwd.py [--b 1 --sq 200 --sk 200 --h 2 --hk 1 --full --fp16 --noreduce]
+"""
+import argparse
+import os
+import struct
+import subprocess
+import sys
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "tools"))
+from asm_emu import Emu, Heap, bf16_to_f32, f16_to_f32, f32_to_bf16, f32_to_f16  # noqa: E402
+
+GEN = os.path.join(ROOT, "xhy-flash-attention_amd", "csrc", "asm", "gen_bwd.py")
+D = 128
+BKN = 128
+
+
+def asm_text():
+    return subprocess.run([sys.executable, GEN], check=True, capture_output=True, text=True).stdout
+
+
+def sched_table(b, nh_grid, hk, h, nblk, reduce):
+    """workgroup -> (bidb | hx << 16, kvh | kblock << 16), heaviest key block first, XCD-grouped as
+    fa_common.h xcd_order"""
+    nbh = b * nh_grid
+    tab = np.zeros((nbh * nblk, 2), dtype=np.uint32)
+    g = h // hk
+    for L in range(nbh * nblk):
+        if nbh % 8 == 0:
+            i = L >> 3
+            hl, blk = divmod(i, nblk)
+            bh = hl * 8 + (L & 7)
+        else:
+            blk, bh = divmod(L, nbh)
+        bidb, hx = divmod(bh, nh_grid)
+        kvh = hx if reduce else hx // g
+        tab[L] = (bidb | (hx << 16), kvh | (blk << 16))
+    return tab
+
+
+def pack_args(**kw):
+    out = struct.pack("<10Q", kw["q"], kw["k"], kw["v"], kw["do"], kw["dk"], kw["dv"], kw["lsed"], kw["sched"],
+                      kw["cuq"], kw["cuk"])
+    out += struct.pack("<6q", kw["q_batch"], kw["k_batch"], kw["v_batch"], kw["do_batch"], kw["dk_batch"], kw["dv_batch"])
+    out += struct.pack("<6i", kw["q_row"], kw["k_row"], kw["v_row"], kw["do_row"], kw["dk_row"], kw["dv_row"])
+    out += struct.pack("<6i", kw["q_head"], kw["k_head"], kw["v_head"], kw["do_head"], kw["dk_head"], kw["dv_head"])
+    out += struct.pack("<6i", kw["sq"], kw["sk"], kw["h"], kw["ng"], kw["nh"], kw["group"])
+    out += struct.pack("<ffii", kw["c"], kw["scale"], kw["flags"], 0)
+    assert len(out) == 216, len(out)
+    return out
+
+
+def reference(q, k, v, do, causal, scale):
+    """float64 forward + backward; q, do (b, sq, h, d), k, v (b, sk, hk, d) -> lse (b, h, sq),
+    D (b, h, sq), dk, dv (b, sk, h, d) per query head (not yet reduced over the group)"""
+    b, sq, h, d = q.shape
+    sk, hk = k.shape[1], k.shape[2]
+    g = h // hk
+    lse = np.full((b, h, sq), np.inf)
+    dsum = np.zeros((b, h, sq))
+    dk = np.zeros((b, sk, h, d))
+    dv = np.zeros((b, sk, h, d))
+    for bi in range(b):
+        for hi in range(h):
+            s = q[bi, :, hi] @ k[bi, :, hi // g].T * scale
+            if causal:
+                s = np.where(np.arange(sk)[None, :] > np.arange(sq)[:, None], -np.inf, s)
+            m = np.max(s, axis=1, keepdims=True)
+            m = np.where(np.isfinite(m), m, 0)
+            p = np.exp(s - m)
+            l = p.sum(axis=1, keepdims=True)
+            with np.errstate(all="ignore"):
+                lse[bi, hi] = np.where(l[:, 0] > 0, (m + np.log(l))[:, 0], np.inf)
+                pn = np.where(l > 0, p / l, 0)
+            o = pn @ v[bi, :, hi // g]
+            dsum[bi, hi] = (do[bi, :, hi] * o).sum(axis=1)
+            dp = do[bi, :, hi] @ v[bi, :, hi // g].T
+            ds = pn * (dp - dsum[bi, hi][:, None])
+            dv[bi, :, hi] = pn.T @ do[bi, :, hi]
+            dk[bi, :, hi] = scale * ds.T @ q[bi, :, hi]
+    return lse, dsum, dk, dv
+
+
+def run(b=1, sq=200, sk=200, h=2, hk=1, causal=True, bf16=True, reduce=True, seed=0, text=None, verbose=True):
+    rng = np.random.default_rng(seed)
+    q = rng.standard_normal((b, sq, h, D)).astype(np.float32)
+    k = rng.standard_normal((b, sk, hk, D)).astype(np.float32)
+    v = rng.standard_normal((b, sk, hk, D)).astype(np.float32)
+    do = rng.standard_normal((b, sq, h, D)).astype(np.float32)
+    enc, dec = (f32_to_bf16, bf16_to_f32) if bf16 else (f32_to_f16, f16_to_f32)
+    q16, k16, v16, do16 = (enc(x).astype(np.uint16) for x in (q, k, v, do))
+    qf, kf, vf, dof = (dec(x).astype(np.float64) for x in (q16, k16, v16, do16))
+    scale = D ** -0.5
+    lse, dsum, dk_ref, dv_ref = reference(qf, kf, vf, dof, causal, scale)
+    g = h // hk
+    if reduce and g > 1:
+        dk_ref = dk_ref.reshape(b, sk, hk, g, D).sum(axis=3)
+        dv_ref = dv_ref.reshape(b, sk, hk, g, D).sum(axis=3)
+    nh_out = hk if (reduce and g > 1) else h
+    ng = (sq + 31) // 32 + 1
+    lsed = np.zeros((b, h, ng, 64), np.float32)
+    for bi in range(b):
+        for hi in range(h):
+            for r in range(sq):
+                lsed[bi, hi, r // 32, r % 32] = np.float32(-lse[bi, hi, r] / np.float32(scale))
+                lsed[bi, hi, r // 32, 32 + r % 32] = np.float32(-dsum[bi, hi, r])
+    heap = Heap(64 << 20)
+    aq, ak, av, ado = heap.put(q16), heap.put(k16), heap.put(v16), heap.put(do16)
+    adk = heap.alloc(b * sk * nh_out * D * 2)
+    adv = heap.alloc(b * sk * nh_out * D * 2)
+    heap.get(adk, b * sk * nh_out * D * 2)[:] = 0xAB
+    heap.get(adv, b * sk * nh_out * D * 2)[:] = 0xAB
+    alsed = heap.put(lsed)
+    nblk = (sk + BKN - 1) // BKN
+    red = reduce and g > 1
+    tab = sched_table(b, nh_out, hk, h, nblk, red)
+    asch = heap.put(tab)
+    kw = dict(q=aq, k=ak, v=av, do=ado, dk=adk, dv=adv, lsed=alsed, sched=asch, cuq=0, cuk=0,
+              q_batch=sq * h * D * 2, k_batch=sk * hk * D * 2, v_batch=sk * hk * D * 2, do_batch=sq * h * D * 2,
+              dk_batch=sk * nh_out * D * 2, dv_batch=sk * nh_out * D * 2,
+              q_row=h * D * 2, k_row=hk * D * 2, v_row=hk * D * 2, do_row=h * D * 2, dk_row=nh_out * D * 2,
+              dv_row=nh_out * D * 2, q_head=D * 2, k_head=D * 2, v_head=D * 2, do_head=D * 2, dk_head=D * 2,
+              dv_head=D * 2, sq=sq, sk=sk, h=h, ng=ng, nh=g if red else 1, group=g,
+              c=float(np.float32(scale * 1.4426950408889634)), scale=float(np.float32(scale)), flags=2 if red else 0)
+    akarg = heap.put(np.frombuffer(pack_args(**kw), dtype=np.uint8))
+    text = text or asm_text()
+    name = f"fa_bwd_dkdv_asm_d128_{'bf16' if bf16 else 'f16'}_{'causal' if causal else 'full'}"
+    emu = Emu(text, name, heap)
+    for L in range(len(tab)):
+        emu.run_wg(L, akarg)
+    dk = dec(heap.get(adk, b * sk * nh_out * D * 2).view(np.uint16)).reshape(b, sk, nh_out, D).astype(np.float64)
+    dv = dec(heap.get(adv, b * sk * nh_out * D * 2).view(np.uint16)).reshape(b, sk, nh_out, D).astype(np.float64)
+    ek = np.abs(dk - dk_ref).max() / max(np.abs(dk_ref).max(), 1e-9)
+    ev = np.abs(dv - dv_ref).max() / max(np.abs(dv_ref).max(), 1e-9)
+    if verbose:
+        print(f"b={b} sq={sq} sk={sk} h={h} hk={hk} causal={causal} bf16={bf16} reduce={red}: "
+              f"rel max|ddK| {ek:.3e} rel max|ddV| {ev:.3e} ({emu.count} instructions, {emu.mfma_count} MFMAs)")
+    return ek, ev, dk, dk_ref, dv, dv_ref
+
+
+if __name__ == "__main__":
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--b", type=int, default=1)
+    ap.add_argument("--sq", type=int, default=200)
+    ap.add_argument("--sk", type=int, default=200)
+    ap.add_argument("--h", type=int, default=2)
+    ap.add_argument("--hk", type=int, default=1)
+    ap.add_argument("--full", action="store_true")
+    ap.add_argument("--fp16", action="store_true")
+    ap.add_argument("--noreduce", action="store_true")
+    ap.add_argument("--seed", type=int, default=0)
+    a = ap.parse_args()
+    run(a.b, a.sq, a.sk, a.h, a.hk, not a.full, not a.fp16, not a.noreduce, a.seed)

@@ -126,7 +126,15 @@ __global__ void __launch_bounds__(256) bwd_pre_kernel(const BwdParams p) {
   const SeqGeom g = seq_geom(p, bidb);
   const int row = blockIdx.y * 16 + (threadIdx.x >> 4);
   const int l16 = threadIdx.x & 15;
-  if (row >= g.sq) return;
+  if (row >= g.sq) {
+    // assembly dK / dV path: the rows of the last 32-row group past seqlen_q read zero chain starts
+    if (p.lsed != nullptr && l16 == 0 && row < ((g.sq + 31) & ~31)) {
+      float* grp = p.lsed + (((int64_t)bidb * s.h + head) * p.lsed_ng + (row >> 5)) * 64 + (row & 31);
+      grp[0] = 0.f;
+      grp[32] = 0.f;
+    }
+    return;
+  }
   const u16* O = (const u16*)p.o + g.o_off + (int64_t)head * p.o_head + (int64_t)row * p.o_row;
   const u16* dO = (const u16*)p.dout + g.do_off + (int64_t)head * p.do_head + (int64_t)row * p.do_row;
   float acc = 0.f;
@@ -144,9 +152,17 @@ __global__ void __launch_bounds__(256) bwd_pre_kernel(const BwdParams p) {
   if (l16 == 0) {
     const int64_t bhi = (int64_t)bidb * s.h + head;
     // with dropout the reference keeps D scaled down by the keep probability (flash_bwd_kernel.h:178-182)
-    p.dsum[bhi * p.seqlen_q_rounded + row] = s.dropout ? acc * s.p_keep : acc;
+    const float dv = s.dropout ? acc * s.p_keep : acc;
+    p.dsum[bhi * p.seqlen_q_rounded + row] = dv;
     // -LSE / scale: the initial accumulator of the dK/dV kernel's S chain (scale != 0: launch_bwd)
-    p.lse_s[bhi * p.seqlen_q_rounded + row] = -p.lse[bhi * s.lse_pitch + row] / s.scale;
+    const float ls = -p.lse[bhi * s.lse_pitch + row] / s.scale;
+    if (p.lsed != nullptr) {   // assembly dK / dV: [-LSE / scale | -D] per 32-row group
+      float* grp = p.lsed + (bhi * p.lsed_ng + (row >> 5)) * 64 + (row & 31);
+      grp[0] = ls;
+      grp[32] = -dv;
+    } else {
+      p.lse_s[bhi * p.seqlen_q_rounded + row] = ls;
+    }
   }
 }
 
@@ -1037,7 +1053,9 @@ static void run_bwd(const BwdParams& p, hipStream_t stream) {
   auto dkdv = [&](hipStream_t st) {
     dim3 grid(p.s.b * nheads_grid * p.num_n_blocks);   // 1-D, xcd_order
     prof_begin(kTimeBwdMain, st);
-    if (masked)
+    if (p.lsed != nullptr)   // the assembly dK / dV kernel (launch_bwd chose it: fa_bwd_asm.cpp)
+      launch_bwd_dkdv_asm(p, BF16, st);
+    else if (masked)
       hipLaunchKernelGGL((bwd_dkdv_kernel<BF16, D, CAUSAL, DROPOUT, true>), grid, dim3(DkdvTile<D>::NW * 64), 0, st, p);
     else
       hipLaunchKernelGGL((bwd_dkdv_kernel<BF16, D, CAUSAL, DROPOUT, false>), grid, dim3(DkdvTile<D>::NW * 64), 0, st, p);
@@ -1123,7 +1141,9 @@ template <bool BF16>
 static void launch_bwd_t(const BwdParams& p, hipStream_t stream) {
   if (p.lse_s == nullptr) throw std::runtime_error("flash_attn_bwd: no scratch for the scaled LSE");
   {
-    dim3 grid(p.s.b * p.s.h, (p.s.seqlen_q + 15) / 16);
+    // (assembly dK / dV: also the zero rows up to the last 32-row group)
+    const int rows = p.lsed != nullptr ? 32 * p.lsed_ng : p.s.seqlen_q;
+    dim3 grid(p.s.b * p.s.h, (rows + 15) / 16);
     prof_begin(kTimeBwdPre, stream);
     hipLaunchKernelGGL((bwd_pre_kernel<BF16>), grid, dim3(256), 0, stream, p);
     prof_end(kTimeBwdPre, stream);
@@ -1153,15 +1173,26 @@ void launch_bwd(const BwdParams& p_in, bool is_bf16, hipStream_t stream) {
   // softmax_scale == 0 (uniform attention) would make -LSE / scale infinite: a tiny positive scale
   // gives the same P to fp32 precision (P deviates from uniform by 1e-30 |S|) and dQ, dK ~ 1e-30.
   if (p.s.scale == 0.f) { p.s.scale = 1e-30f; p.s.scale_log2 = 1e-30f * kLog2e; }
-  // scratch for -LSE / scale: the caller's dq_accum, else the stream-ordered allocator
+  // scratch for -LSE / scale (HIP dK/dV): the caller's dq_accum (at least (b, h, seqlen_q_rounded)
+  // fp32), else the stream-ordered allocator; the assembly dK/dV's [-LSE / scale | -D] groups
+  // (2 x 32-row-rounded rows) always come from the allocator (the caller's buffer size is unknown)
+  p.lsed = nullptr;
+  p.lsed_ng = (p.s.seqlen_q + 31) / 32;
+  const bool asm_dkdv = bwd_asm_applicable(p);
   void* ws = nullptr;
   p.lse_s = p.dq_accum;
-  if (p.lse_s == nullptr) {
+  if (p.lse_s == nullptr || asm_dkdv) {
     keep_pool_memory();
-    const size_t bytes = (size_t)p.s.b * p.s.h * p.seqlen_q_rounded * sizeof(float);
+    const size_t bytes = asm_dkdv ? (size_t)p.s.b * p.s.h * p.lsed_ng * 64 * sizeof(float)
+                                  : (size_t)p.s.b * p.s.h * p.seqlen_q_rounded * sizeof(float);
     if (hipMallocAsync(&ws, bytes, stream) != hipSuccess)
       throw std::runtime_error("flash_attn_bwd: hipMallocAsync of the LSE scratch failed");
-    p.lse_s = static_cast<float*>(ws);
+    if (asm_dkdv) {
+      p.lsed = static_cast<float*>(ws);
+      if (p.lse_s == nullptr) p.lse_s = p.lsed;   // (not read on this path)
+    } else {
+      p.lse_s = static_cast<float*>(ws);
+    }
   }
   if (is_bf16) launch_bwd_t<true>(p, stream); else launch_bwd_t<false>(p, stream);
   if (ws != nullptr) (void)hipFreeAsync(ws, stream);

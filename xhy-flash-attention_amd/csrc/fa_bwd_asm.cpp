@@ -1,0 +1,169 @@
+// Host side of the hand-scheduled assembly dK / dV kernel (csrc/asm/gen_bwd.py -> fa_bwd_asm.s,
+// assembled for gfx950 and embedded in this library as a code object).
+//
+// The kernel covers the headline backward: head dim 128, bf16 / fp16, causal or not, fixed length
+// or varlen, MHA / GQA (reduced in-kernel over the group, or expanded per query head), no dropout /
+// mask / FlashMask.  It replaces bwd_dkdv_kernel for those calls; bwd_pre_kernel then writes the
+// per-row chain starts it streams (-LSE / scale and -D, 32 rows per 256-byte group: the "lsed"
+// scratch), and the dQ kernel is unchanged.  Everything else -- and this path when it is switched
+// off (FLASH_ATTN_MI355X_BWD_ASM=0 or knob 3) -- runs bwd_dkdv_kernel (fa_bwd.hip).
+//
+// Work order: a per-shape table maps workgroup -> (batch, head, kv head, 128-key block) in the HIP
+// kernel's xcd_order (heaviest causal key block first, the blocks of one head on one XCD).
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+#include <cstring>
+#include <map>
+#include <mutex>
+#include <stdexcept>
+#include <string>
+#include <tuple>
+#include <vector>
+
+#include "fa_params.h"
+
+extern "C" const unsigned char fa_bwd_asm_co[];
+extern "C" const unsigned long fa_bwd_asm_co_size;
+
+namespace fa {
+namespace {
+
+// must match the kernarg loads of gen_bwd.py (K.prologue) and KARG_SIZE
+struct BwdAsmArgs {
+  const void* q; const void* k; const void* v; const void* dout; void* dk; void* dv;
+  const float* lsed; const uint32_t* sched; const int* cu_q; const int* cu_k;
+  int64_t q_batch, k_batch, v_batch, do_batch, dk_batch, dv_batch;     // bytes
+  int32_t q_row, k_row, v_row, do_row, dk_row, dv_row;                 // bytes
+  int32_t q_head, k_head, v_head, do_head, dk_head, dv_head;           // bytes
+  int32_t sq, sk, h, ng, nh, group;
+  float c, scale;
+  int32_t flags;    // bit 0: varlen_padded_input, bit 1: dK / dV reduced over the GQA group
+  int32_t pad;
+};
+static_assert(sizeof(BwdAsmArgs) == 216, "BwdAsmArgs layout");
+
+constexpr int kMaxDev = 64;
+constexpr int kBkn = 128;   // keys per workgroup
+struct DevModule {
+  hipModule_t mod = nullptr;
+  hipFunction_t fn[4] = {};   // [bf16 causal, bf16 full, f16 causal, f16 full]
+  std::map<std::tuple<int, int, int, int>, uint32_t*> tables;
+};
+std::mutex g_mu;
+DevModule g_dev[kMaxDev];
+
+const char* kNames[4] = {"fa_bwd_dkdv_asm_d128_bf16_causal", "fa_bwd_dkdv_asm_d128_bf16_full",
+                         "fa_bwd_dkdv_asm_d128_f16_causal", "fa_bwd_dkdv_asm_d128_f16_full"};
+
+void check(hipError_t e, const char* what) {
+  if (e != hipSuccess) throw std::runtime_error(std::string("flash_attn_bwd (asm dK/dV): ") + what + ": " + hipGetErrorString(e));
+}
+
+DevModule& module_for(int dev) {
+  if (dev < 0 || dev >= kMaxDev) throw std::runtime_error("flash_attn_bwd (asm dK/dV): device index out of range");
+  DevModule& m = g_dev[dev];
+  if (m.mod == nullptr) {
+    check(hipModuleLoadData(&m.mod, fa_bwd_asm_co), "hipModuleLoadData");
+    for (int i = 0; i < 4; ++i) check(hipModuleGetFunction(&m.fn[i], m.mod, kNames[i]), kNames[i]);
+  }
+  return m;
+}
+
+// workgroup -> (bidb | hx << 16, kvh | kblock << 16): fa_common.h xcd_order over nbh = b * heads
+// of dK / dV and nblk key blocks (block 0, the longest causal sweep, first)
+std::vector<uint32_t> build_table(int b, int nh_grid, int h, int hk, int nblk, bool reduce) {
+  const long long nbh = (long long)b * nh_grid;
+  const long long n = nbh * nblk;
+  std::vector<uint32_t> t((size_t)n * 2);
+  const int g = h / hk;
+  for (long long L = 0; L < n; ++L) {
+    long long bh, blk;
+    if ((nbh & 7) == 0) {
+      const long long i = L >> 3;
+      const long long hl = i / nblk;
+      blk = i - hl * nblk;
+      bh = hl * 8 + (L & 7);
+    } else {
+      blk = L / nbh;
+      bh = L - blk * nbh;
+    }
+    const int bidb = (int)(bh / nh_grid), hx = (int)(bh - (long long)bidb * nh_grid);
+    const int kvh = reduce ? hx : hx / g;
+    t[2 * L] = (uint32_t)bidb | ((uint32_t)hx << 16);
+    t[2 * L + 1] = (uint32_t)kvh | ((uint32_t)blk << 16);
+  }
+  return t;
+}
+
+bool fits32(int64_t x) { return x >= 0 && x < (1ll << 31); }
+
+}  // namespace
+
+bool bwd_asm_applicable(const BwdParams& p) {
+  const AttnShape& s = p.s;
+  if (knob(kKnobBwdAsm) == 0) return false;
+  if (s.d != 128 || s.dropout || s.mask != nullptr || s.fm_lts != nullptr) return false;
+  if (s.hk <= 0 || s.h % s.hk != 0 || s.b > 65535 || s.h > 65535) return false;
+  const int nblk = (s.seqlen_k + kBkn - 1) / kBkn;
+  if (nblk > 65535 || (long long)s.b * s.h * nblk > 0x7fffffffll) return false;
+  if ((32ll * ((s.seqlen_q + 31) / 32) + 15) / 16 > 65535) return false;   // bwd_pre_kernel's grid
+  for (int64_t x : {p.q_row, p.k_row, p.v_row, p.do_row, p.dk_row, p.dv_row,
+                    p.q_head, p.k_head, p.v_head, p.do_head, p.dk_head, p.dv_head})
+    if (!fits32(2 * x)) return false;
+  // records of one (sequence, head) and the 32-row cursor steps stay below 2^31 bytes
+  const int64_t sq = s.seqlen_q + 64, sk = s.seqlen_k + kBkn;
+  for (int64_t x : {sq * 2 * p.q_row, sq * 2 * p.do_row, sk * 2 * p.k_row, sk * 2 * p.v_row, sk * 2 * p.dk_row,
+                    sk * 2 * p.dv_row})
+    if (!fits32(x)) return false;
+  return true;
+}
+
+void launch_bwd_dkdv_asm(const BwdParams& p, bool is_bf16, hipStream_t stream) {
+  const AttnShape& s = p.s;
+  if (p.lsed == nullptr) throw std::runtime_error("flash_attn_bwd (asm dK/dV): no LSE / D scratch");
+  const int nh_grid = p.gqa_reduce ? s.hk : s.h;
+  const int nblk = (s.seqlen_k + kBkn - 1) / kBkn;
+  const long long nwg = (long long)s.b * nh_grid * nblk;
+  if (nwg <= 0) return;
+  int dev = 0;
+  check(hipGetDevice(&dev), "hipGetDevice");
+  hipFunction_t fn;
+  uint32_t* table;
+  {
+    std::lock_guard<std::mutex> lk(g_mu);
+    DevModule& m = module_for(dev);
+    fn = m.fn[(is_bf16 ? 0 : 2) + (s.causal ? 0 : 1)];
+    const int red = p.gqa_reduce ? 1 : 0;
+    auto key = std::make_tuple(s.b, nh_grid * 2 + red, s.h * 65536 + s.hk, nblk);
+    auto it = m.tables.find(key);
+    if (it == m.tables.end()) {
+      std::vector<uint32_t> t = build_table(s.b, nh_grid, s.h, s.hk, nblk, p.gqa_reduce);
+      uint32_t* d = nullptr;
+      check(hipMalloc(&d, t.size() * sizeof(uint32_t)), "hipMalloc (schedule table)");
+      check(hipMemcpy(d, t.data(), t.size() * sizeof(uint32_t), hipMemcpyHostToDevice), "hipMemcpy (schedule table)");
+      it = m.tables.emplace(key, d).first;
+    }
+    table = it->second;
+  }
+  BwdAsmArgs a;
+  std::memset(&a, 0, sizeof(a));
+  a.q = p.q; a.k = p.k; a.v = p.v; a.dout = p.dout; a.dk = p.dk; a.dv = p.dv;
+  a.lsed = p.lsed; a.sched = table; a.cu_q = s.cu_seqlens_q; a.cu_k = s.cu_seqlens_k;
+  a.q_batch = 2 * p.q_batch; a.k_batch = 2 * p.k_batch; a.v_batch = 2 * p.v_batch;
+  a.do_batch = 2 * p.do_batch; a.dk_batch = 2 * p.dk_batch; a.dv_batch = 2 * p.dv_batch;
+  a.q_row = (int32_t)(2 * p.q_row); a.k_row = (int32_t)(2 * p.k_row); a.v_row = (int32_t)(2 * p.v_row);
+  a.do_row = (int32_t)(2 * p.do_row); a.dk_row = (int32_t)(2 * p.dk_row); a.dv_row = (int32_t)(2 * p.dv_row);
+  a.q_head = (int32_t)(2 * p.q_head); a.k_head = (int32_t)(2 * p.k_head); a.v_head = (int32_t)(2 * p.v_head);
+  a.do_head = (int32_t)(2 * p.do_head); a.dk_head = (int32_t)(2 * p.dk_head); a.dv_head = (int32_t)(2 * p.dv_head);
+  a.sq = s.seqlen_q; a.sk = s.seqlen_k; a.h = s.h; a.ng = p.lsed_ng;
+  a.group = s.h / s.hk;
+  a.nh = p.gqa_reduce ? a.group : 1;
+  a.c = s.scale_log2; a.scale = s.scale;
+  a.flags = (s.varlen_padded_input ? 1 : 0) | (p.gqa_reduce ? 2 : 0);
+  size_t sz = sizeof(a);
+  void* cfg[] = {HIP_LAUNCH_PARAM_BUFFER_POINTER, &a, HIP_LAUNCH_PARAM_BUFFER_SIZE, &sz, HIP_LAUNCH_PARAM_END};
+  check(hipModuleLaunchKernel(fn, (unsigned)nwg, 1, 1, 256, 1, 1, 0, stream, nullptr, cfg), "hipModuleLaunchKernel");
+}
+
+}  // namespace fa

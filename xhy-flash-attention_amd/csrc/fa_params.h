@@ -104,6 +104,10 @@ struct BwdParams {
                           // false: dk/dv have h heads (reference "expanded" contract)
   int num_n_blocks;
   int dq_head_group;        // dQ kernel: xcd_order_grouped heads per group (0: head-fastest)
+  // assembly dK / dV path (fa_bwd_asm.cpp): (b, h, lsed_ng, 64) fp32 scratch of 32-row groups
+  // [-LSE / scale x 32 | -D x 32] written by bwd_pre_kernel instead of lse_s; nullptr: HIP path
+  float* lsed;
+  int lsed_ng;
 };
 
 // calc_reduced_attn_scores (fa_reduced.hip; reference reduced_scores::Params,
@@ -139,7 +143,9 @@ void launch_fwd(const FwdParams& p, bool is_bf16, hipStream_t stream);
 bool launch_fwd_asm(const FwdParams& p, bool is_bf16, hipStream_t stream);
 void fwd_asm_enable(int on);
 void launch_bwd(const BwdParams& p, bool is_bf16, hipStream_t stream);
-void bwd_overlap_enable(int mode);   // fa_bwd.hip: dQ / dK-dV stream overlap mode (default 0: off)
+void bwd_overlap_enable(int mode);
+bool bwd_asm_applicable(const BwdParams& p);                        // fa_bwd_asm.cpp
+void launch_bwd_dkdv_asm(const BwdParams& p, bool is_bf16, hipStream_t stream);   // fa_bwd.hip: dQ / dK-dV stream overlap mode (default 0: off)
 void launch_reduced_scores(const ReducedParams& p, bool is_bf16, hipStream_t stream);
 void launch_rotary(const RotaryParams& p, bool interleaved, bool conj, bool is_bf16, hipStream_t stream);
 
@@ -158,7 +164,8 @@ void prof_end(int id, hipStream_t s);
 enum Knob { kKnobNoSplitKv = 0 /* FLASH_ATTN_MI355X_NO_SPLITKV: 1 = never split K/V */,
             kKnobNoXcdGroup = 1 /* FLASH_ATTN_MI355X_NO_XCD_GROUP: 1 = head-fastest order */,
             kKnobXcdGroupMinMiB = 2 /* FLASH_ATTN_MI355X_XCD_GROUP_MIN_MIB: grouping threshold */,
-            kNumKnobs = 3 };
+            kKnobBwdAsm = 3 /* FLASH_ATTN_MI355X_BWD_ASM: 0 = HIP dK/dV kernel for every call */,
+            kNumKnobs = 4 };
 int knob(int id);
 void set_knob(int id, int value);
 
