@@ -31,6 +31,8 @@ def short(name):
         return "fwd_kernel"
     if name.startswith("fa_bwd_dkdv_asm_"):   # the assembly dK/dV kernel (gen_bwd.py)
         return "bwd_dkdv_kernel"
+    if name.startswith("fa_bwd_dq_asm_"):     # the assembly dQ kernel (gen_dq.py)
+        return "bwd_dq_kernel"
     return name.split("(")[0].split("::")[-1].split("<")[0].strip()
 
 

@@ -20,7 +20,22 @@ from bench import KernelTimer  # noqa: E402
 from flash_attn import flash_attn_func, flash_attn_varlen_func  # noqa: E402
 from knobs import knob  # noqa: E402
 
-BWD_ASM = 3
+BWD_ASM, DQ_ASM = 3, 4
+
+
+class both:
+    """both assembly backward kernels on (1) or off (0)"""
+
+    def __init__(self, on):
+        self.k = [knob(BWD_ASM, on), knob(DQ_ASM, on)]
+
+    def __enter__(self):
+        for k in self.k:
+            k.__enter__()
+
+    def __exit__(self, *a):
+        for k in reversed(self.k):
+            k.__exit__(*a)
 SHAPES = [  # b, sq, sk, h, hk, causal, dtype
     (1, 64, 128, 1, 1, True, torch.bfloat16),
     (2, 300, 300, 2, 2, True, torch.bfloat16),
@@ -55,9 +70,9 @@ def main():
         k = torch.randn(b, sk, hk, 128, device="cuda", dtype=dt, generator=g).requires_grad_()
         v = torch.randn(b, sk, hk, 128, device="cuda", dtype=dt, generator=g).requires_grad_()
         do = torch.randn(b, sq, h, 128, device="cuda", dtype=dt, generator=g)
-        with knob(BWD_ASM, 0):
+        with both(0):
             ref = grads(q, k, v, do, causal)
-        with knob(BWD_ASM, 1):
+        with both(1):
             got = grads(q, k, v, do, causal)
         torch.cuda.synchronize()
         msg = []
@@ -81,7 +96,7 @@ def main():
         do = torch.randn(900, 4, 128, device="cuda", dtype=torch.bfloat16, generator=g)
         res = {}
         for on in (0, 1):
-            with knob(BWD_ASM, on):
+            with both(on):
                 out = flash_attn_varlen_func(q, k, v, cu, cu, 543, 543, causal=causal)
                 res[on] = torch.autograd.grad(out, (q, k, v), do)
         msg = []
@@ -103,7 +118,7 @@ def main():
         res = {0: [], 1: []}
         for _ in range(4):
             for on in (1, 0):
-                with knob(BWD_ASM, on):
+                with both(on):
                     for _ in range(2):
                         torch.autograd.grad(out, (q, k, v), do, retain_graph=True)
                     torch.cuda.synchronize()
@@ -111,10 +126,13 @@ def main():
                     for _ in range(10):
                         torch.autograd.grad(out, (q, k, v), do, retain_graph=True)
                     torch.cuda.synchronize()
-                    res[on].append(timer.stop()["bwd_dkdv_kernel"]["avg_ms"])
+                    t = timer.stop()
+                    res[on].append((t["bwd_dkdv_kernel"]["avg_ms"], t["bwd_dq_kernel"]["avg_ms"]))
         for on in (1, 0):
-            ms = min(res[on])
-            print(f"C3 dK/dV {'asm' if on else 'HIP'}: {ms:.4f} ms ({2 * f / ms / 1e9:.0f} TF)", flush=True)
+            ms = min(x[0] for x in res[on])
+            mq = min(x[1] for x in res[on])
+            print(f"C3 {'asm' if on else 'HIP'}: dK/dV {ms:.4f} ms ({2 * f / ms / 1e9:.0f} TF), "
+                  f"dQ {mq:.4f} ms ({1.5 * f / mq / 1e9:.0f} TF)", flush=True)
 
 
 if __name__ == "__main__":

@@ -1,0 +1,115 @@
+#!/usr/bin/env python3
+"""Runs the generated assembly dQ kernel (csrc/asm/gen_dq.py) in the CPU emulator (tools/asm_emu.py)
+on small inputs and compares dQ with a float64 reference (dev / test tool).
+
+    python tools/emu_dq.py [--b 1 --sq 300 --sk 300 --h 2 --hk 1 --full --fp16]
+"""
+import argparse
+import os
+import struct
+import subprocess
+import sys
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "tools"))
+from asm_emu import Emu, Heap, bf16_to_f32, f16_to_f32, f32_to_bf16, f32_to_f16  # noqa: E402
+from emu_bwd import reference as bwd_reference  # noqa: E402
+from emu_fwd import sched_table  # noqa: E402
+
+GEN = os.path.join(ROOT, "xhy-flash-attention_amd", "csrc", "asm", "gen_dq.py")
+D = 128
+BM = 256
+
+
+def asm_text():
+    return subprocess.run([sys.executable, GEN], check=True, capture_output=True, text=True).stdout
+
+
+def pack_args(**kw):
+    out = struct.pack("<10Q", kw["q"], kw["k"], kw["v"], kw["do"], kw["dq"], kw["lse"], kw["dsum"], kw["sched"],
+                      kw["cuq"], kw["cuk"])
+    out += struct.pack("<4q", kw["q_batch"], kw["kv_batch"], kw["do_batch"], kw["dq_batch"])
+    out += struct.pack("<4i", kw["q_row"], kw["kv_row"], kw["do_row"], kw["dq_row"])
+    out += struct.pack("<5i", kw["q_head"], kw["k_head"], kw["v_head"], kw["do_head"], kw["dq_head"])
+    out += struct.pack("<7i", kw["sq"], kw["sk"], kw["lse_pitch"], kw["dsum_pitch"], kw["h"], kw["hk"], kw["flags"])
+    out += struct.pack("<ff", kw["c"], kw["scale"])
+    assert len(out) == 184, len(out)
+    return out
+
+
+def reference_dq(q, k, v, do, causal, scale):
+    b, sq, h, d = q.shape
+    sk, hk = k.shape[1], k.shape[2]
+    g = h // hk
+    lse, dsum, _, _ = bwd_reference(q, k, v, do, causal, scale)
+    dq = np.zeros_like(q)
+    for bi in range(b):
+        for hi in range(h):
+            s = q[bi, :, hi] @ k[bi, :, hi // g].T * scale
+            if causal:
+                s = np.where(np.arange(sk)[None, :] > np.arange(sq)[:, None], -np.inf, s)
+            with np.errstate(all="ignore"):
+                p = np.where(np.isfinite(lse[bi, hi])[:, None], np.exp(s - lse[bi, hi][:, None]), 0)
+            dp = do[bi, :, hi] @ v[bi, :, hi // g].T
+            ds = p * (dp - dsum[bi, hi][:, None])
+            dq[bi, :, hi] = scale * ds @ k[bi, :, hi // g]
+    return lse, dsum, dq
+
+
+def run(b=1, sq=300, sk=300, h=2, hk=1, causal=True, bf16=True, seed=0, text=None, verbose=True):
+    rng = np.random.default_rng(seed)
+    q = rng.standard_normal((b, sq, h, D)).astype(np.float32)
+    k = rng.standard_normal((b, sk, hk, D)).astype(np.float32)
+    v = rng.standard_normal((b, sk, hk, D)).astype(np.float32)
+    do = rng.standard_normal((b, sq, h, D)).astype(np.float32)
+    enc, dec = (f32_to_bf16, bf16_to_f32) if bf16 else (f32_to_f16, f16_to_f32)
+    q16, k16, v16, do16 = (enc(x).astype(np.uint16) for x in (q, k, v, do))
+    qf, kf, vf, dof = (dec(x).astype(np.float64) for x in (q16, k16, v16, do16))
+    scale = D ** -0.5
+    lse, dsum, dq_ref = reference_dq(qf, kf, vf, dof, causal, scale)
+    sqr = (sq + 127) // 128 * 128
+    lse32 = lse.astype(np.float32)
+    ds32 = np.zeros((b, h, sqr), np.float32)
+    ds32[:, :, :sq] = dsum
+    heap = Heap(64 << 20)
+    aq, ak, av, ado = heap.put(q16), heap.put(k16), heap.put(v16), heap.put(do16)
+    adq = heap.alloc(b * sq * h * D * 2)
+    heap.get(adq, b * sq * h * D * 2)[:] = 0xAB
+    alse, ads = heap.put(lse32), heap.put(ds32)
+    nmb = (sq + BM - 1) // BM
+    tab = sched_table(b, h, hk, nmb)
+    asch = heap.put(tab)
+    kw = dict(q=aq, k=ak, v=av, do=ado, dq=adq, lse=alse, dsum=ads, sched=asch, cuq=0, cuk=0,
+              q_batch=sq * h * D * 2, kv_batch=sk * hk * D * 2, do_batch=sq * h * D * 2, dq_batch=sq * h * D * 2,
+              q_row=h * D * 2, kv_row=hk * D * 2, do_row=h * D * 2, dq_row=h * D * 2,
+              q_head=D * 2, k_head=D * 2, v_head=D * 2, do_head=D * 2, dq_head=D * 2,
+              sq=sq, sk=sk, lse_pitch=sq, dsum_pitch=sqr, h=h, hk=hk, flags=0,
+              c=float(np.float32(scale * 1.4426950408889634)), scale=float(np.float32(scale)))
+    akarg = heap.put(np.frombuffer(pack_args(**kw), dtype=np.uint8))
+    text = text or asm_text()
+    name = f"fa_bwd_dq_asm_d128_{'bf16' if bf16 else 'f16'}_{'causal' if causal else 'full'}"
+    emu = Emu(text, name, heap)
+    for L in range(len(tab)):
+        emu.run_wg(L, akarg)
+    dq = dec(heap.get(adq, b * sq * h * D * 2).view(np.uint16)).reshape(b, sq, h, D).astype(np.float64)
+    e = np.abs(dq - dq_ref).max() / max(np.abs(dq_ref).max(), 1e-9)
+    if verbose:
+        print(f"b={b} sq={sq} sk={sk} h={h} hk={hk} causal={causal} bf16={bf16}: rel max|ddQ| {e:.3e} "
+              f"({emu.count} instructions, {emu.mfma_count} MFMAs)")
+    return e, dq, dq_ref
+
+
+if __name__ == "__main__":
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--b", type=int, default=1)
+    ap.add_argument("--sq", type=int, default=300)
+    ap.add_argument("--sk", type=int, default=300)
+    ap.add_argument("--h", type=int, default=2)
+    ap.add_argument("--hk", type=int, default=1)
+    ap.add_argument("--full", action="store_true")
+    ap.add_argument("--fp16", action="store_true")
+    ap.add_argument("--seed", type=int, default=0)
+    a = ap.parse_args()
+    run(a.b, a.sq, a.sk, a.h, a.hk, not a.full, not a.fp16, a.seed)

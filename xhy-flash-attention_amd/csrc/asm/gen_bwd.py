@@ -40,7 +40,7 @@ import os
 import sys
 
 sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
-from isa import (ACCR, ACCW, BARRIER, BRANCH, DMA, LABEL, LDS, MFMA, RFL, SALU, SMEM, SOPP,  # noqa: E402
+from isa import (ACCR, ACCW, BARRIER, BRANCH, DMA, LABEL, LDS, MFMA, PERM, RFL, SALU, SMEM, SOPP,  # noqa: E402
                  TRANS, VALU, VLOAD, VSTORE, WAIT, Inst, add_waits, ar, fix_hazards, label, nop, rtxt,
                  schedule, sr, vr)
 
@@ -131,6 +131,10 @@ S_TMP = 49                           # 49..55 (the prologue keeps kernargs in 56
 NSGPR = 102
 
 KARG_SIZE = 216
+
+# dev A/B switches, read when the .s is generated (tools/asm_variant.sh)
+OPT_WIN = int(os.environ.get("FA_GBW_WIN", "16"))     # an A fragment may be read up to WIN MFMAs ahead
+OPT_LEAD = int(os.environ.get("FA_GBW_LEAD", "2"))    # ... and at least LEAD MFMAs ahead
 
 
 class K:
@@ -305,8 +309,8 @@ class K:
         for m, (_, t, i) in enumerate(mf):
             if m < 3 and first_pref:
                 continue
-            fill += self.frag_reads(m, t, i, key=-100 + m, earliest=max(m - 16, -1) if m >= 16 else None,
-                                    deadline=max(m - 2, 0))
+            fill += self.frag_reads(m, t, i, key=-100 + m, earliest=max(m - OPT_WIN, -1) if m >= OPT_WIN else None,
+                                    deadline=max(m - OPT_LEAD, 0))
         if valu:
             fill += self.valu_ops(par, masked, q0_add)
             fill += self.init_reads(par)
@@ -501,8 +505,11 @@ class K:
         # ---- K / V fragments of this wave's 32 keys (B operands), loaded once into AGPRs ----
         REM = T6
         ins += [I(f"s_sub_i32 s{REM}, s{SK}, s{KW0}", SALU, rd=sr(SK) + sr(KW0), wr=sr(REM))]
-        ins += desc_at(S_QD, Pk, KOFF, KVH, Hk, KW0, Rk, REM)      # (the Q / dO cursor registers, borrowed)
-        ins += desc_at(S_OD, Pv, VOFF, KVH, Hv, KW0, Rv, REM)
+        # descriptors in the varlen kernargs' registers (dead now, never rewritten): the fragment loads
+        # stay in flight while the Q / dO / LSE DMA of the prologue is issued
+        KD, VD = 72, 76
+        ins += desc_at(KD, Pk, KOFF, KVH, Hk, KW0, Rk, REM)
+        ins += desc_at(VD, Pv, VOFF, KVH, Hv, KW0, Rv, REM)
         r_, hh = V_TMP, V_TMP + 1
         ins += [I(f"v_and_b32_e32 v{r_}, 31, v{V_LANE}", VALU, rd=vr(V_LANE), wr=vr(r_)),
                 I(f"v_lshrrev_b32_e32 v{hh}, 5, v{V_LANE}", VALU, rd=vr(V_LANE), wr=vr(hh)),
@@ -511,11 +518,11 @@ class K:
                 I(f"v_mul_lo_u32 v{V_TMP + 3}, v{r_}, s{Rv}", VALU, rd=vr(r_) + sr(Rv), wr=vr(V_TMP + 3)),
                 I(f"v_lshl_add_u32 v{V_TMP + 3}, v{hh}, 4, v{V_TMP + 3}", VALU, rd=vr(hh) + vr(V_TMP + 3), wr=vr(V_TMP + 3))]
         for ks in range(KS):
-            ins.append(I(f"buffer_load_dwordx4 {rtxt('a', KF + 4 * ks, 4)}, v{V_TMP + 2}, s[{S_QD}:{S_QD + 3}], 0 offen offset:{32 * ks}",
-                         VLOAD, rd=vr(V_TMP + 2) + sr(S_QD, 4), wr=ar(KF + 4 * ks, 4)))
+            ins.append(I(f"buffer_load_dwordx4 {rtxt('a', KF + 4 * ks, 4)}, v{V_TMP + 2}, s[{KD}:{KD + 3}], 0 offen offset:{32 * ks}",
+                         VLOAD, rd=vr(V_TMP + 2) + sr(KD, 4), wr=ar(KF + 4 * ks, 4)))
         for ks in range(KS):
-            ins.append(I(f"buffer_load_dwordx4 {rtxt('a', VF + 4 * ks, 4)}, v{V_TMP + 3}, s[{S_OD}:{S_OD + 3}], 0 offen offset:{32 * ks}",
-                         VLOAD, rd=vr(V_TMP + 3) + sr(S_OD, 4), wr=ar(VF + 4 * ks, 4)))
+            ins.append(I(f"buffer_load_dwordx4 {rtxt('a', VF + 4 * ks, 4)}, v{V_TMP + 3}, s[{VD}:{VD + 3}], 0 offen offset:{32 * ks}",
+                         VLOAD, rd=vr(V_TMP + 3) + sr(VD, 4), wr=ar(VF + 4 * ks, 4)))
         # ---- per-lane values (while the fragments load) ----
         # DMA voffsets: wave w, half f: row = 16 f + lane / 4, col = 64 w + 16 ((lane & 3) ^ ((lane >> 4) & 3))
         x = V_TMP + 2
@@ -598,8 +605,7 @@ class K:
                 I(f"s_and_b32 s{S_LD + 1}, s{S_LH + 1}, 0xffff", SALU, rd=sr(S_LH + 1), wr=sr(S_LD + 1)),
                 I(f"s_mov_b32 s{S_LD + 2}, s{S_LREC0}", SALU, rd=sr(S_LREC0), wr=sr(S_LD + 2)),
                 I(f"s_mov_b32 s{S_LD + 3}, 0x20000", SALU, wr=sr(S_LD + 3))]
-        # ---- Q / dO cursors at (head HB, row q_first); their registers held the K / V descriptors ----
-        ins += [I("s_waitcnt vmcnt(0)", WAIT)]
+        # ---- Q / dO cursors at (head HB, row q_first) ----
         ins += desc_at(S_QD, Pq, QOFF, HB, Hq, QF, Rq, ROWS)
         ins += desc_at(S_OD, Pdo, DOOFF, HB, Hdo, QF, Rdo, ROWS)
         ins += [I(f"s_mov_b32 s{S_QREC0}, s{S_QD + 2}", SALU, rd=sr(S_QD + 2), wr=sr(S_QREC0)),
@@ -665,6 +671,9 @@ class K:
         def sa(op, d, a, b, extra_rd=()):
             return I(f"{op} s{d}, s{a}, s{b}", SALU, rd=sr(a) + sr(b) + list(extra_rd), wr=sr(d) + [("scc", 0)])
 
+        # the last steps' DMA (zero records past the sweep) must have landed before the workgroup's LDS
+        # is released
+        ins += [I("s_waitcnt vmcnt(0)", WAIT)]
         ins += [rf(KW0v, T4), rf(HDv, T5), rf(SKv, T6)]
         for dst, ptr, off, rowv, headv, acc, scale in ((S_QD, PDV, DVO, RDV, HDV, DV, False),
                                                         (S_OD, PDK, DKO, RDK, HDK, DK, True)):
@@ -681,24 +690,31 @@ class K:
                     I(f"s_max_i32 s{T3}, s{T3}, 0", SALU, rd=sr(T3), wr=sr(T3)),
                     sa("s_mul_i32", dst + 2, T3, T2),
                     I(f"s_mov_b32 s{dst + 3}, 0x20000", SALU, wr=sr(dst + 3)),
-                    # lane offset: r row + 8 hh
+                    # lane offset: r row + 16 hh (lane halves store alternate 8-column groups)
                     I(f"v_and_b32_e32 v{V_TMP}, 31, v{V_LANE}", VALU, rd=vr(V_LANE), wr=vr(V_TMP)),
                     I(f"v_mul_lo_u32 v{V_TMP}, v{V_TMP}, s{T2}", VALU, rd=vr(V_TMP) + sr(T2), wr=vr(V_TMP)),
                     I(f"v_lshrrev_b32_e32 v{V_TMP + 1}, 5, v{V_LANE}", VALU, rd=vr(V_LANE), wr=vr(V_TMP + 1)),
-                    I(f"v_lshl_add_u32 v{V_TMP + 2}, v{V_TMP + 1}, 3, v{V_TMP}", VALU, rd=vr(V_TMP, 2), wr=vr(V_TMP + 2))]
+                    I(f"v_lshl_add_u32 v{V_TMP + 2}, v{V_TMP + 1}, 4, v{V_TMP}", VALU, rd=vr(V_TMP, 2), wr=vr(V_TMP + 2))]
+            # per (d-tile, u pair): lane half 0 writes columns 8 u0 .. +7 (its 4 + its partner's 4),
+            # half 1 writes 8 (u0 + 1) .. +7, one dwordx4 each (v_permlane32_swap joins the halves)
             x = 0
             for dt in range(NP):
-                for u in range(4):
-                    a = acc + 16 * dt + 4 * u
-                    ins += [I(f"v_accvgpr_read_b32 v{x + k}, a{a + k}", ACCR, rd=ar(a + k), wr=vr(x + k)) for k in range(4)]
-                    if scale:
-                        ins += [I(f"v_mul_f32_e32 v{x + k}, s{S_SCALE}, v{x + k}", VALU, rd=sr(S_SCALE) + vr(x + k), wr=vr(x + k))
-                                for k in range(4)]
-                    ins += [self.cvt(x + 4, x, x + 1), self.cvt(x + 5, x + 2, x + 3)]
-                    ins.append(I(f"buffer_store_dwordx2 v[{x + 4}:{x + 5}], v{V_TMP + 2}, s[{dst}:{dst + 3}], 0 offen offset:{64 * dt + 16 * u}",
-                                 VSTORE, rd=vr(x + 4, 2) + vr(V_TMP + 2) + sr(dst, 4)))
-                    x = (x + 8) % 64
-        ins += [I("s_waitcnt vmcnt(0)", WAIT)]
+                for u0 in (0, 2):
+                    w = x + 8
+                    for uu in range(2):
+                        a = acc + 16 * dt + 4 * (u0 + uu)
+                        xs = x + 4 * uu
+                        ins += [I(f"v_accvgpr_read_b32 v{xs + k}, a{a + k}", ACCR, rd=ar(a + k), wr=vr(xs + k)) for k in range(4)]
+                        if scale:
+                            ins += [I(f"v_mul_f32_e32 v{xs + k}, s{S_SCALE}, v{xs + k}", VALU, rd=sr(S_SCALE) + vr(xs + k), wr=vr(xs + k))
+                                    for k in range(4)]
+                        ins += [self.cvt(w + 2 * uu, xs, xs + 1), self.cvt(w + 2 * uu + 1, xs + 2, xs + 3)]
+                    ins += [I(f"v_permlane32_swap_b32_e32 v{w}, v{w + 2}", PERM, rd=vr(w) + vr(w + 2), wr=vr(w) + vr(w + 2)),
+                            I(f"v_permlane32_swap_b32_e32 v{w + 1}, v{w + 3}", PERM, rd=vr(w + 1) + vr(w + 3), wr=vr(w + 1) + vr(w + 3))]
+                    ins.append(I(f"buffer_store_dwordx4 v[{w}:{w + 3}], v{V_TMP + 2}, s[{dst}:{dst + 3}], 0 offen offset:{64 * dt + 16 * u0}",
+                                 VSTORE, rd=vr(w, 4) + vr(V_TMP + 2) + sr(dst, 4)))
+                    x = (x + 12) % 60
+        # (no wait: the stores complete after the wave ends; the DMAs were drained before them)
         return ins
 
     # ------------------------------------------------------------------ whole kernel

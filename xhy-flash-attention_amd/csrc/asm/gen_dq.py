@@ -1,0 +1,687 @@
+#!/usr/bin/env python3
+"""Generates fa_dq_asm.s: the gfx950 FlashAttention-2 dQ kernel for head dim 128, written as a
+hand-scheduled assembly kernel (one wave per SIMD).
+
+    python3 gen_dq.py > fa_dq_asm.s
+
+Algorithm: the dQ half of the reference's backward (csrc/flash_attn/src/flash_bwd_kernel.h:
+compute_dq_dk_dv_1colblock, dS :897-906, dQ :948-1008) for one block of query rows, swept over every
+key it can see:
+    S^T = K Q^T,  P^T = exp2(c S^T - log2e LSE)   (-inf where the causal mask hides the key)
+    dP^T = V dO^T,  dS^T = P^T o (dP^T - D)
+    dQ^T += K^T dS^T                              (dQ = scale dQ^T^T at the end)
+with LSE and D = rowsum(dO o O) per query row -- per lane: the query is the MFMA column.
+
+MI355X structure: gen_bwd.py's (the dK / dV kernel) with the roles of the operands swapped:
+  * workgroup = 4 waves x 64 query rows (q-blocks a and b of 32) = a 256-row block; each wave keeps
+    its rows' operands and results in its 512 registers for the whole sweep:
+      a[0:127] dQ^T (2 q-blocks x 4 d-tiles x 16), a[128:191] Q fragments, a[192:255] dO fragments
+      (B operands of S^T = K Q^T and dP^T = V dO^T);
+      v[0:127] S^T / dP^T tiles (two buffers x two q-blocks), v[128:159] packed dS^T (two buffers:
+      the B operands of dQ^T), v[160:223] a ring of 16 A-operand fragments read from LDS;
+  * the keys stream through LDS in 32-key subtiles (K and V, 16 KiB, a 9-slot ring) by LDS-DMA,
+    6 subtiles ahead, one s_waitcnt + s_barrier per step of two subtiles;
+  * phase p (48 MFMAs):  S^T, dP^T(p+1)  ||  dQ^T += ..(p-1)  and, in the gaps, the VALU of subtile p
+    (P, dS and the dS pack of both q-blocks) and the LDS reads (K / V rows with ds_read_b128, K^T with
+    ds_read_b64_tr_b16): each A fragment feeds the MFMAs of both q-blocks;
+  * causal: the subtiles that reach past the block's first row run a MASKED step variant; keys past
+    the causal end or seqlen_k read zero K / V (range-checked descriptors) and contribute nothing.
+"""
+import os
+import sys
+
+sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+from isa import (ACCR, ACCW, BARRIER, BRANCH, DMA, LABEL, LDS, MFMA, PERM, RFL, SALU, SMEM, SOPP,  # noqa: E402
+                 TRANS, VALU, VLOAD, VSTORE, WAIT, Inst, add_waits, ar, fix_hazards, label, nop, rtxt,
+                 schedule, sr, vr)
+
+D = 128
+KS = D // 16            # k-steps of S^T / dP^T
+NP = D // 32            # d-tiles of dQ^T
+SUB = 32                # keys per subtile
+BM = 256                # query rows per workgroup
+KT = SUB * D * 2        # bytes of a K (or V) subtile = 8 KiB
+SLOT = 2 * KT           # K | V
+NS = 9
+RING = NS * SLOT        # 147456
+LDS_BYTES = RING
+KQ = 6                  # K / V subtile s is DMA'd in step (s - KQ) / 2
+# the end of step n-1 waits for the rows of subtiles <= 2n+3 (step n reads them, its last phase
+# prefetching the first fragments of 2n+3); younger than K/V(2n+3) (issued in step n-2): the 8 of step n-1
+VMCNT_STEP = 8
+
+OPT_WIN = int(os.environ.get("FA_GDQ_WIN", "16"))
+OPT_LEAD = int(os.environ.get("FA_GDQ_LEAD", "2"))
+
+# ---- AGPRs ----
+def DQ(j, dt):
+    return 64 * j + 16 * dt
+
+
+def QF(j, ks):
+    return 128 + 32 * j + 4 * ks
+
+
+def OF(j, ks):
+    return 192 + 32 * j + 4 * ks
+
+
+# ---- VGPRs ----
+def SB(par, j):
+    return 32 * par + 16 * j
+
+
+def DPB(par, j):
+    return 64 + 32 * par + 16 * j
+
+
+def DSP(par, j):
+    return 128 + 16 * par + 8 * j
+
+
+RG = 160
+
+
+def ring(f):
+    return RG + 4 * (f % 16)
+
+
+V_RB0, V_RB1, V_TB0, V_TB1 = 224, 225, 226, 227
+V_KB0, V_KB1, V_VB0, V_VB1 = 228, 229, 230, 231
+V_KV0, V_KV1 = 232, 233        # DMA voffsets (K and V share them: k_row == v_row), halves 0 / 1
+V_NLC = (234, 235)             # -log2e LSE per q-block
+V_D = (236, 237)               # D per q-block
+V_LIM = (238, 239)             # causal mask limit base per q-block: q - 4 hh
+V_LM = 240
+V_NINF = 241
+V_LANE = 242
+V_QOFF = (243, 244)            # Q / dO row offsets (prologue), then dQ row offsets (epilogue)
+V_OOFF = (245, 246)
+V_TMP = 247                    # 247..255
+NVGPR = 256
+
+# ---- SGPRs ----
+S_KD, S_VD = 4, 8              # K / V DMA cursors
+S_QD, S_OD = 12, 16            # Q / dO (prologue), dQ (epilogue)
+S_C = 20                       # scale log2 e
+S_SCALE = 21
+S_SROW, S_STR, S_SDMA = 22, 23, 24
+S_W2K = 25
+S_N, S_NLAST = 26, 27
+S_MASK0 = 28                   # first masked step (causal), else a large value
+S_KV32 = 29                    # 32 rows of K / V (bytes)
+S_WAVE = 30
+S_TMP = 31                     # 31..39
+NSGPR = 102
+
+KARG_SIZE = 184
+
+
+class K:
+    def __init__(self, bf16, causal):
+        self.bf16 = bf16
+        self.causal = causal
+        self.ty = "bf16" if bf16 else "f16"
+        self.name = f"fa_bwd_dq_asm_d{D}_{self.ty}_{'causal' if causal else 'full'}"
+        self.uid = 0
+
+    def lab(self, s):
+        self.uid += 1
+        return f".L{self.name}_{s}_{self.uid}"
+
+    # ------------------------------------------------------------------ MFMAs of a phase
+    def mf(self, dst, a, b, first=False):
+        dk, dr = dst
+        regs = {"v": vr, "a": ar}
+        c = "0" if first else rtxt(dk, dr, 16)
+        t = (f"v_mfma_f32_32x32x16_{self.ty} {rtxt(dk, dr, 16)}, {rtxt(a[0], a[1], 4)}, {rtxt(b[0], b[1], 4)}, {c}")
+        d = regs[dk](dr, 16)
+        rd = regs[a[0]](a[1], 4) + regs[b[0]](b[1], 4) + ([] if first else d)
+        return Inst(t, MFMA, rd=rd, wr=d, rd_c=[] if first else d)
+
+    def phase_frags(self, sdp, dq):
+        """the A fragments of a phase in MFMA order: (kind, index)"""
+        if sdp and dq:
+            return [(t, i) for i in range(8) for t in ("S", "dQ", "dP")]
+        if sdp:
+            return [(t, i) for i in range(8) for t in ("S", "dP")]
+        return [("dQ", i) for i in range(8)]
+
+    def phase_mfmas(self, par, sdp, dq):
+        """MFMA list (two per fragment: q-blocks a, b) and the fragment list; par = parity of the VALU
+        subtile p: S^T / dP^T(p+1) write buffers 1 - par, dQ(p-1) reads packs 1 - par"""
+        nb = 1 - par
+        frags = self.phase_frags(sdp, dq)
+        out = []
+        for f, (t, i) in enumerate(frags):
+            for j in range(2):
+                if t == "S":
+                    out.append(self.mf(("v", SB(nb, j)), ("v", ring(f)), ("a", QF(j, i)), first=(i == 0)))
+                elif t == "dP":
+                    out.append(self.mf(("v", DPB(nb, j)), ("v", ring(f)), ("a", OF(j, i)), first=(i == 0)))
+                else:
+                    dt, kk = i // 2, i % 2
+                    out.append(self.mf(("a", DQ(j, dt)), ("v", ring(f)), ("v", DSP(nb, j) + 4 * kk)))
+        return out, frags
+
+    def frag_reads(self, f, t, i, **kw):
+        dst = ring(f)
+        if t in ("S", "dP"):
+            base = V_KB0 if i % 2 == 0 else V_KB1
+            off = (i // 2) * 2048 + (KT if t == "dP" else 0)
+            return [Inst(f"ds_read_b128 {rtxt('v', dst, 4)}, v{base} offset:{off}", LDS, rd=vr(base), wr=vr(dst, 4), **kw)]
+        dt, kk = i // 2, i % 2
+        out = []
+        for h in range(2):
+            base = V_VB0 if h == 0 else V_VB1
+            off = dt * 2048 + kk * 1024 + h * 512
+            out.append(Inst(f"ds_read_b64_tr_b16 {rtxt('v', dst + 2 * h, 2)}, v{base} offset:{off}", LDS,
+                            rd=vr(base), wr=vr(dst + 2 * h, 2), **kw))
+        return out
+
+    def cvt(self, dst, s0, s1, **kw):
+        return Inst(f"v_cvt_pk_{self.ty}_f32 v{dst}, v{s0}, v{s1}", VALU, rd=vr(s0) + vr(s1), wr=vr(dst), **kw)
+
+    # ------------------------------------------------------------------ VALU of one subtile
+    def valu_ops(self, par, masked, n0_add):
+        """P^T and dS^T of subtile p (buffers par) for both q-blocks -> dS packs par.  Key base of the
+        subtile = S_N * 64 + n0_add"""
+        ops = []
+        for j in range(2):
+            S, DP, PK = SB(par, j), DPB(par, j), DSP(par, j)
+            k0 = 200 * j
+            if masked:
+                # limit = q - 4 hh - key base; element g masked iff (g & 3) + 8 (g >> 2) > limit
+                ops.append(Inst(f"s_lshl_b32 s{S_TMP + 8}, s{S_N}, 6", SALU, rd=sr(S_N), wr=sr(S_TMP + 8), key=k0))
+                ops.append(Inst(f"v_subrev_u32 v{V_LM}, s{S_TMP + 8}, v{V_LIM[j]}", VALU, rd=sr(S_TMP + 8) + vr(V_LIM[j]),
+                                wr=vr(V_LM), key=k0))
+                if n0_add:
+                    ops.append(Inst(f"v_subrev_u32 v{V_LM}, {n0_add}, v{V_LM}", VALU, rd=vr(V_LM), wr=vr(V_LM), key=k0))
+            for g in range(16):
+                ops.append(Inst(f"v_fma_f32 v{S + g}, v{S + g}, s{S_C}, v{V_NLC[j]}", VALU,
+                                rd=vr(S + g) + sr(S_C) + vr(V_NLC[j]), wr=vr(S + g), key=k0 + 4 * g))
+                if masked:
+                    const = (g & 3) + 8 * (g >> 2)
+                    ops.append(Inst(f"v_cmp_gt_i32_e32 vcc, {const}, v{V_LM}", VALU, rd=vr(V_LM), wr=[("vcc", 0)], key=k0 + 4 * g))
+                    ops.append(Inst(f"v_cndmask_b32_e32 v{S + g}, v{S + g}, v{V_NINF}, vcc", VALU,
+                                    rd=vr(S + g) + vr(V_NINF) + [("vcc", 0)], wr=vr(S + g), key=k0 + 4 * g))
+                ops.append(Inst(f"v_exp_f32_e32 v{S + g}, v{S + g}", TRANS, rd=vr(S + g), wr=vr(S + g), key=k0 + 4 * g + 1))
+                ops.append(Inst(f"v_sub_f32_e32 v{DP + g}, v{DP + g}, v{V_D[j]}", VALU, rd=vr(DP + g) + vr(V_D[j]),
+                                wr=vr(DP + g), key=k0 + 4 * g + 2))
+                ops.append(Inst(f"v_mul_f32_e32 v{DP + g}, v{S + g}, v{DP + g}", VALU, rd=vr(S + g) + vr(DP + g),
+                                wr=vr(DP + g), key=k0 + 4 * g + 3))
+                if g % 2 == 1:
+                    ops.append(self.cvt(PK + g // 2, DP + g - 1, DP + g, key=k0 + 4 * g + 3))
+        return ops
+
+    # ------------------------------------------------------------------ DMA of one subtile
+    def dma_subtile(self, key=-50, eg=None):
+        t = S_TMP
+        I = Inst
+        ops = [I(f"s_add_u32 s{t}, s{S_SDMA}, s{S_W2K}", SALU, rd=sr(S_SDMA) + sr(S_W2K), wr=sr(t) + [("scc", 0)], key=key)]
+        for jx, (voff, desc, add) in enumerate(((V_KV0, S_KD, 0), (V_KV1, S_KD, 1024), (V_KV0, S_VD, KT),
+                                                (V_KV1, S_VD, KT + 1024))):
+            e = None if eg is None else eg + 2 * jx
+            ops.append(I(f"s_add_u32 m0, s{t}, {add}", SALU, rd=sr(t), wr=[("m0", 0), ("scc", 0)], key=key, earliest=e))
+            ops.append(I(f"buffer_load_dwordx4 v{voff}, s[{desc}:{desc + 3}], 0 offen lds", DMA,
+                         rd=vr(voff) + sr(desc, 4) + [("m0", 0)], key=key, earliest=e))
+        for desc in (S_KD, S_VD):
+            ops += [I(f"s_add_u32 s{desc}, s{desc}, s{S_KV32}", SALU, rd=sr(desc) + sr(S_KV32), wr=sr(desc) + [("scc", 0)], key=key + 1),
+                    I(f"s_addc_u32 s{desc + 1}, s{desc + 1}, 0", SALU, rd=sr(desc + 1) + [("scc", 0)], wr=sr(desc + 1) + [("scc", 0)], key=key + 1),
+                    I(f"s_sub_u32 s{t + 1}, s{desc + 2}, s{S_KV32}", SALU, rd=sr(desc + 2) + sr(S_KV32), wr=sr(t + 1) + [("scc", 0)], key=key + 1),
+                    I(f"s_cselect_b32 s{desc + 2}, 0, s{t + 1}", SALU, rd=sr(t + 1) + [("scc", 0)], wr=sr(desc + 2), key=key + 1)]
+        ops += self.slot_advance(S_SDMA, key + 1)
+        return ops
+
+    def slot_advance(self, reg, key=0):
+        """reg = (reg + SLOT) mod RING"""
+        t, u = S_TMP + 2, S_TMP + 3
+        I = Inst
+        return [I(f"s_add_u32 s{u}, s{reg}, {SLOT}", SALU, rd=sr(reg), wr=sr(u) + [("scc", 0)], key=key),
+                I(f"s_sub_u32 s{t}, s{reg}, {RING - SLOT}", SALU, rd=sr(reg), wr=sr(t) + [("scc", 0)], key=key),
+                I(f"s_cselect_b32 s{reg}, s{u}, s{t}", SALU, rd=sr(u) + sr(t) + [("scc", 0)], wr=sr(reg), key=key)]
+
+    # ------------------------------------------------------------------ one phase
+    def phase(self, par, sdp, dq, valu, masked, n0_add, dma, next_kind, tail_ops=None):
+        mf, frags = self.phase_mfmas(par, sdp, dq)
+        n = len(mf)
+        fill = []
+        for f, (t, i) in enumerate(frags):
+            if f < 3:
+                continue        # prefetched by the predecessor
+            eg = 2 * (f - 16) + 1 if f >= 16 else (2 * (f - OPT_WIN) + 1 if f >= OPT_WIN else None)
+            fill += self.frag_reads(f, t, i, key=-100 + f, earliest=eg, deadline=max(2 * f - OPT_LEAD, 0))
+        if valu:
+            fill += self.valu_ops(par, masked, n0_add)
+        if dma:
+            fill += self.dma_subtile(key=-40, eg=2)
+        nxt = self.slot_advance(S_SROW, key=400) + self.slot_advance(S_STR, key=400)
+        nxt += [Inst(f"v_add_u32_e32 v{V_KB0}, s{S_SROW}, v{V_RB0}", VALU, rd=sr(S_SROW) + vr(V_RB0), wr=vr(V_KB0), key=401),
+                Inst(f"v_add_u32_e32 v{V_KB1}, s{S_SROW}, v{V_RB1}", VALU, rd=sr(S_SROW) + vr(V_RB1), wr=vr(V_KB1), key=401),
+                Inst(f"v_add_u32_e32 v{V_VB0}, s{S_STR}, v{V_TB0}", VALU, rd=sr(S_STR) + vr(V_TB0), wr=vr(V_VB0), key=401),
+                Inst(f"v_add_u32_e32 v{V_VB1}, s{S_STR}, v{V_TB1}", VALU, rd=sr(S_STR) + vr(V_TB1), wr=vr(V_VB1), key=401)]
+        fill += nxt
+        if next_kind is not None:
+            nfr = self.phase_frags(next_kind in ("full", "sdp"), next_kind in ("full", "dq"))
+            for f in range(3):
+                t, i = nfr[f]
+                users = [k for k in range(len(frags)) if k % 16 == f % 16]
+                eg = 2 * max(users) + 1 if users else None
+                fill += self.frag_reads(f, t, i, key=600 + f, earliest=eg)
+        if tail_ops:
+            fill += tail_ops
+        return schedule(mf, fill)
+
+    def step(self, first, last, masked):
+        a = self.phase(0, sdp=True, dq=not first, valu=True, masked=masked, n0_add=0, dma=True,
+                       next_kind="dq" if last else "full")
+        tail = [Inst(f"s_add_u32 s{S_N}, s{S_N}, 1", SALU, rd=sr(S_N), wr=sr(S_N) + [("scc", 0)], key=900)]
+        b = self.phase(1, sdp=not last, dq=True, valu=True, masked=masked, n0_add=SUB, dma=True,
+                       next_kind="dq" if last else "full", tail_ops=tail)
+        return a + b
+
+    def step_end(self):
+        return [Inst(f"s_waitcnt vmcnt({VMCNT_STEP}) lgkmcnt(0)", WAIT), Inst("s_barrier", BARRIER)]
+
+    def tail(self):
+        mf, frags = self.phase_mfmas(0, False, True)     # par 0 -> packs 1 (subtile N-1 is odd)
+        fill = []
+        for f, (t, i) in enumerate(frags):
+            if f < 3:
+                continue
+            fill += self.frag_reads(f, t, i, key=-100 + f, deadline=max(2 * f - OPT_LEAD, 0))
+        return schedule(mf, fill)
+
+    # ------------------------------------------------------------------ prologue
+    def prologue(self, l_epi):
+        I = Inst
+        ins = []
+        # kernargs (DqAsmArgs, fa_bwd_asm.cpp) -> s56..s99
+        ka = 56
+        ins += [I(f"s_load_dwordx16 s[{ka}:{ka + 15}], s[0:1], 0x0", SMEM, rd=sr(0, 2), wr=sr(ka, 16)),
+                I(f"s_load_dwordx16 s[{ka + 16}:{ka + 31}], s[0:1], 0x40", SMEM, rd=sr(0, 2), wr=sr(ka + 16, 16)),
+                I(f"s_load_dwordx8 s[{ka + 32}:{ka + 39}], s[0:1], 0x80", SMEM, rd=sr(0, 2), wr=sr(ka + 32, 8)),
+                I(f"s_load_dwordx4 s[{ka + 40}:{ka + 43}], s[0:1], 0xa0", SMEM, rd=sr(0, 2), wr=sr(ka + 40, 4)),
+                I("s_waitcnt lgkmcnt(0)", WAIT)]
+        P = lambda i: ka + i   # noqa: E731
+        # dwords: 0 q, 2 k, 4 v, 6 dout, 8 dq, 10 lse, 12 dsum, 14 sched, 16 cu_q, 18 cu_k,
+        # 20 q_batch, 22 kv_batch, 24 do_batch, 26 dq_batch (i64 bytes),
+        # 28 q_row, 29 kv_row, 30 do_row, 31 dq_row, 32 q_head, 33 k_head, 34 v_head, 35 do_head, 36 dq_head,
+        # 37 sq, 38 sk, 39 lse_pitch, 40 dsum_pitch, 41 h, 42 hk, 43 flags | c, scale follow at 0xb0
+        Pq, Pk, Pv, Pdo, Pdq, Pl, Pds, Psch, Pcq, Pck = (P(2 * i) for i in range(10))
+        Bq, Bkv, Bdo, Bdq = (P(20 + 2 * i) for i in range(4))
+        Rq, Rkv, Rdo, Rdq, Hq, Hk, Hv, Hdo, Hdq = (P(28 + i) for i in range(9))
+        SQ, SK, LP, DPt, NH, NHK, FLG = (P(37 + i) for i in range(7))
+        T = [S_TMP + i for i in range(9)]
+        ins += [I(f"s_load_dwordx2 s[{S_C}:{S_SCALE}], s[0:1], 0xb0", SMEM, rd=sr(0, 2), wr=sr(S_C, 2)),
+                I("v_lshrrev_b32_e32 v1, 6, v0", VALU, rd=vr(0), wr=vr(1)),
+                I(f"v_readfirstlane_b32 s{S_WAVE}, v1", RFL, rd=vr(1), wr=sr(S_WAVE)),
+                I(f"v_and_b32_e32 v{V_LANE}, 63, v0", VALU, rd=vr(0), wr=vr(V_LANE)),
+                I(f"s_lshl_b32 s{T[0]}, s2, 3", SALU, rd=sr(2), wr=sr(T[0])),
+                I(f"s_load_dwordx2 s[{T[1]}:{T[2]}], s[{Psch}:{Psch + 1}], s{T[0]}", SMEM, rd=sr(Psch, 2) + sr(T[0]), wr=sr(T[1], 2)),
+                I("s_waitcnt lgkmcnt(0)", WAIT)]
+        BIDB, HEAD, KVH, MB = S_N, S_NLAST, S_MASK0, S_KV32     # temporaries until the loop state
+        ins += [I(f"s_and_b32 s{BIDB}, s{T[1]}, 0xffff", SALU, rd=sr(T[1]), wr=sr(BIDB)),
+                I(f"s_lshr_b32 s{HEAD}, s{T[1]}, 16", SALU, rd=sr(T[1]), wr=sr(HEAD)),
+                I(f"s_and_b32 s{KVH}, s{T[2]}, 0xffff", SALU, rd=sr(T[2]), wr=sr(KVH)),
+                I(f"s_lshr_b32 s{MB}, s{T[2]}, 16", SALU, rd=sr(T[2]), wr=sr(MB))]
+        # varlen geometry (block_info.h:14-31): byte offsets of row 0 of this sequence (Q-side: Q, dO,
+        # dQ; K-side: K and V share it, k_row == v_row and the batch strides are equal)
+        QOFF, DOOFF, DQOFF, KOFF = (40, 41), (42, 43), (44, 45), (46, 47)
+
+        def mul64(dst, a32, b32):
+            return [I(f"s_mul_i32 s{dst[0]}, s{a32}, s{b32}", SALU, rd=sr(a32) + sr(b32), wr=sr(dst[0])),
+                    I(f"s_mul_hi_u32 s{dst[1]}, s{a32}, s{b32}", SALU, rd=sr(a32) + sr(b32), wr=sr(dst[1]))]
+
+        def mul64_i64(dst, a32, b64):
+            return [I(f"s_mul_i32 s{dst[0]}, s{a32}, s{b64}", SALU, rd=sr(a32) + sr(b64), wr=sr(dst[0])),
+                    I(f"s_mul_hi_u32 s{dst[1]}, s{a32}, s{b64}", SALU, rd=sr(a32) + sr(b64), wr=sr(dst[1])),
+                    I(f"s_mul_i32 s{T[0]}, s{a32}, s{b64 + 1}", SALU, rd=sr(a32) + sr(b64 + 1), wr=sr(T[0])),
+                    I(f"s_add_u32 s{dst[1]}, s{dst[1]}, s{T[0]}", SALU, rd=sr(dst[1]) + sr(T[0]), wr=sr(dst[1]))]
+
+        for cu, bstride, rstride, off, seq in ((Pcq, Bq, Rq, QOFF, SQ), (Pcq, Bdo, Rdo, DOOFF, None),
+                                                (Pcq, Bdq, Rdq, DQOFF, None), (Pck, Bkv, Rkv, KOFF, SK)):
+            lf, ld = self.lab("fixed"), self.lab("done")
+            ins += [I(f"s_cmp_eq_u64 s[{cu}:{cu + 1}], 0", SALU, rd=sr(cu, 2), wr=[("scc", 0)]),
+                    I(f"s_cbranch_scc1 {lf}", BRANCH),
+                    I(f"s_lshl_b32 s{T[1]}, s{BIDB}, 2", SALU, rd=sr(BIDB), wr=sr(T[1])),
+                    I(f"s_load_dwordx2 s[{off[0]}:{off[1]}], s[{cu}:{cu + 1}], s{T[1]}", SMEM, rd=sr(cu, 2) + sr(T[1]), wr=sr(off[0], 2)),
+                    I("s_waitcnt lgkmcnt(0)", WAIT)]
+            if seq is not None:
+                ins += [I(f"s_sub_u32 s{seq}, s{off[1]}, s{off[0]}", SALU, rd=sr(off[0], 2), wr=sr(seq))]
+            ins += [I(f"s_bitcmp1_b32 s{FLG}, 0", SALU, rd=sr(FLG), wr=[("scc", 0)]),
+                    I(f"s_cbranch_scc1 {lf}", BRANCH),
+                    I(f"s_mov_b32 s{T[1]}, s{off[0]}", SALU, rd=sr(off[0]), wr=sr(T[1]))]
+            ins += mul64(off, T[1], rstride)
+            ins += [I(f"s_branch {ld}", BRANCH), label(lf)]
+            ins += mul64_i64(off, BIDB, bstride)
+            ins += [label(ld)]
+        # m0 = 256 mb; exit when m0 >= sq
+        M0R, NROW = T[4], T[5]
+        ins += [I(f"s_lshl_b32 s{M0R}, s{MB}, 8", SALU, rd=sr(MB), wr=sr(M0R)),
+                I(f"s_cmp_ge_i32 s{M0R}, s{SQ}", SALU, rd=sr(M0R) + sr(SQ), wr=[("scc", 0)]),
+                I(f"s_cbranch_scc1 {self.lab_end}", BRANCH),
+                I(f"s_sub_u32 s{NROW}, s{SQ}, s{M0R}", SALU, rd=sr(SQ) + sr(M0R), wr=sr(NROW)),
+                I(f"s_min_u32 s{NROW}, s{NROW}, {BM}", SALU, rd=sr(NROW), wr=sr(NROW))]
+
+        def desc(dst4, ptr, off64, head, hstride, rows, rstride, nrec):
+            """dst4 = descriptor of ptr + off64 + head hstride + rows rstride; nrec: list of records ops"""
+            o = [I(f"s_mul_i32 s{T[0]}, s{head}, s{hstride}", SALU, rd=sr(head) + sr(hstride), wr=sr(T[0])),
+                 I(f"s_mul_hi_u32 s{T[1]}, s{head}, s{hstride}", SALU, rd=sr(head) + sr(hstride), wr=sr(T[1])),
+                 I(f"s_add_u32 s{dst4}, s{ptr}, s{T[0]}", SALU, rd=sr(ptr) + sr(T[0]), wr=sr(dst4) + [("scc", 0)]),
+                 I(f"s_addc_u32 s{dst4 + 1}, s{ptr + 1}, s{T[1]}", SALU, rd=sr(ptr + 1) + sr(T[1]) + [("scc", 0)], wr=sr(dst4 + 1)),
+                 I(f"s_add_u32 s{dst4}, s{dst4}, s{off64[0]}", SALU, rd=sr(dst4) + sr(off64[0]), wr=sr(dst4) + [("scc", 0)]),
+                 I(f"s_addc_u32 s{dst4 + 1}, s{dst4 + 1}, s{off64[1]}", SALU, rd=sr(dst4 + 1) + sr(off64[1]) + [("scc", 0)], wr=sr(dst4 + 1))]
+            if rows is not None:
+                o += [I(f"s_mul_i32 s{T[0]}, s{rows}, s{rstride}", SALU, rd=sr(rows) + sr(rstride), wr=sr(T[0])),
+                      I(f"s_mul_hi_u32 s{T[1]}, s{rows}, s{rstride}", SALU, rd=sr(rows) + sr(rstride), wr=sr(T[1])),
+                      I(f"s_add_u32 s{dst4}, s{dst4}, s{T[0]}", SALU, rd=sr(dst4) + sr(T[0]), wr=sr(dst4) + [("scc", 0)]),
+                      I(f"s_addc_u32 s{dst4 + 1}, s{dst4 + 1}, s{T[1]}", SALU, rd=sr(dst4 + 1) + sr(T[1]) + [("scc", 0)], wr=sr(dst4 + 1))]
+            o += [I(f"s_and_b32 s{dst4 + 1}, s{dst4 + 1}, 0xffff", SALU, rd=sr(dst4 + 1), wr=sr(dst4 + 1))]
+            o += nrec
+            o += [I(f"s_mov_b32 s{dst4 + 3}, 0x20000", SALU, wr=sr(dst4 + 3))]
+            return o
+
+        # Q / dO: rows [m0, m0 + nrow) of this sequence and head
+        ins += desc(S_QD, Pq, QOFF, HEAD, Hq, M0R, Rq, [I(f"s_mul_i32 s{S_QD + 2}, s{NROW}, s{Rq}", SALU, rd=sr(NROW) + sr(Rq), wr=sr(S_QD + 2))])
+        ins += desc(S_OD, Pdo, DOOFF, HEAD, Hdo, M0R, Rdo, [I(f"s_mul_i32 s{S_OD + 2}, s{NROW}, s{Rdo}", SALU, rd=sr(NROW) + sr(Rdo), wr=sr(S_OD + 2))])
+        # keys of the sweep: n_end = causal ? min(sk, m0 + 256) : sk (K / V read zero past it)
+        NEND = T[6]
+        if self.causal:
+            ins += [I(f"s_add_u32 s{NEND}, s{M0R}, {BM}", SALU, rd=sr(M0R), wr=sr(NEND)),
+                    I(f"s_min_i32 s{NEND}, s{NEND}, s{SK}", SALU, rd=sr(NEND) + sr(SK), wr=sr(NEND))]
+        else:
+            ins += [I(f"s_mov_b32 s{NEND}, s{SK}", SALU, rd=sr(SK), wr=sr(NEND))]
+        ins += [I(f"s_max_i32 s{NEND}, s{NEND}, 0", SALU, rd=sr(NEND), wr=sr(NEND))]
+        ZERO = T[7]
+        ins += [I(f"s_mov_b32 s{ZERO}, 0", SALU, wr=sr(ZERO))]
+        ins += desc(S_KD, Pk, KOFF, KVH, Hk, None, None, [I(f"s_mul_i32 s{S_KD + 2}, s{NEND}, s{Rkv}", SALU, rd=sr(NEND) + sr(Rkv), wr=sr(S_KD + 2))])
+        ins += desc(S_VD, Pv, KOFF, KVH, Hv, None, None, [I(f"s_mul_i32 s{S_VD + 2}, s{NEND}, s{Rkv}", SALU, rd=sr(NEND) + sr(Rkv), wr=sr(S_VD + 2))])
+        # steps: subtiles ns = ceil(n_end / 32) rounded up to even; N / 2 steps
+        ins += [I(f"s_add_u32 s{T[0]}, s{NEND}, {2 * SUB - 1}", SALU, rd=sr(NEND), wr=sr(T[0])),
+                I(f"s_lshr_b32 s{T[0]}, s{T[0]}, 6", SALU, rd=sr(T[0]), wr=sr(T[0])),          # steps
+                I(f"s_sub_i32 s{T[8]}, s{T[0]}, 1", SALU, rd=sr(T[0]), wr=sr(T[8]))]           # last step
+        # first masked step (causal): the first subtile with keys past the block's first row: m0 / 64
+        if self.causal:
+            ins += [I(f"s_lshr_b32 s{T[3]}, s{M0R}, 6", SALU, rd=sr(M0R), wr=sr(T[3]))]
+        else:
+            ins += [I(f"s_mov_b32 s{T[3]}, 0x7fffffff", SALU, wr=sr(T[3]))]
+        # ---- per-lane values: rows, LSE / D, offsets ----
+        r_, hh = V_TMP, V_TMP + 1
+        x = V_TMP + 2
+        ins += [I(f"v_and_b32_e32 v{r_}, 31, v{V_LANE}", VALU, rd=vr(V_LANE), wr=vr(r_)),
+                I(f"v_lshrrev_b32_e32 v{hh}, 5, v{V_LANE}", VALU, rd=vr(V_LANE), wr=vr(hh))]
+        # LSE / D descriptors: lse + ((bidb h + head) lse_pitch + m0) * 4 (records 4 nrow), the same for D
+        LD, DD = 48, 52          # borrowed from the kernarg block (dead by now): q_batch.. / kv_batch..
+        for dd, ptr, pitch in ((LD, Pl, LP), (DD, Pds, DPt)):
+            ins += [I(f"s_mul_i32 s{T[0]}, s{BIDB}, s{NH}", SALU, rd=sr(BIDB) + sr(NH), wr=sr(T[0])),
+                    I(f"s_add_u32 s{T[0]}, s{T[0]}, s{HEAD}", SALU, rd=sr(T[0]) + sr(HEAD), wr=sr(T[0])),
+                    I(f"s_mul_i32 s{T[1]}, s{T[0]}, s{pitch}", SALU, rd=sr(T[0]) + sr(pitch), wr=sr(T[1])),
+                    I(f"s_mul_hi_u32 s{T[2]}, s{T[0]}, s{pitch}", SALU, rd=sr(T[0]) + sr(pitch), wr=sr(T[2])),
+                    I(f"s_add_u32 s{T[1]}, s{T[1]}, s{M0R}", SALU, rd=sr(T[1]) + sr(M0R), wr=sr(T[1]) + [("scc", 0)]),
+                    I(f"s_addc_u32 s{T[2]}, s{T[2]}, 0", SALU, rd=sr(T[2]) + [("scc", 0)], wr=sr(T[2])),
+                    I(f"s_lshl_b64 s[{T[1]}:{T[2]}], s[{T[1]}:{T[2]}], 2", SALU, rd=sr(T[1], 2), wr=sr(T[1], 2)),
+                    I(f"s_add_u32 s{dd}, s{ptr}, s{T[1]}", SALU, rd=sr(ptr) + sr(T[1]), wr=sr(dd) + [("scc", 0)]),
+                    I(f"s_addc_u32 s{dd + 1}, s{ptr + 1}, s{T[2]}", SALU, rd=sr(ptr + 1) + sr(T[2]) + [("scc", 0)], wr=sr(dd + 1)),
+                    I(f"s_and_b32 s{dd + 1}, s{dd + 1}, 0xffff", SALU, rd=sr(dd + 1), wr=sr(dd + 1)),
+                    I(f"s_lshl_b32 s{dd + 2}, s{NROW}, 2", SALU, rd=sr(NROW), wr=sr(dd + 2)),
+                    I(f"s_mov_b32 s{dd + 3}, 0x20000", SALU, wr=sr(dd + 3))]
+        # rows of the wave: 64 w + 32 j + r
+        for j in range(2):
+            ins += [I(f"v_lshl_add_u32 v{x}, v1, 6, v{r_}", VALU, rd=vr(1) + vr(r_), wr=vr(x)),
+                    I(f"v_add_u32_e32 v{x}, {32 * j}, v{x}", VALU, rd=vr(x), wr=vr(x)),
+                    I(f"v_lshlrev_b32_e32 v{x + 1}, 2, v{x}", VALU, rd=vr(x), wr=vr(x + 1)),
+                    I(f"buffer_load_dword v{V_NLC[j]}, v{x + 1}, s[{LD}:{LD + 3}], 0 offen", VLOAD,
+                      rd=vr(x + 1) + sr(LD, 4), wr=vr(V_NLC[j])),
+                    I(f"buffer_load_dword v{V_D[j]}, v{x + 1}, s[{DD}:{DD + 3}], 0 offen", VLOAD,
+                      rd=vr(x + 1) + sr(DD, 4), wr=vr(V_D[j])),
+                    # Q / dO row offsets: row * row_stride + 16 hh
+                    I(f"v_mul_lo_u32 v{V_QOFF[j]}, v{x}, s{Rq}", VALU, rd=vr(x) + sr(Rq), wr=vr(V_QOFF[j])),
+                    I(f"v_lshl_add_u32 v{V_QOFF[j]}, v{hh}, 4, v{V_QOFF[j]}", VALU, rd=vr(hh) + vr(V_QOFF[j]), wr=vr(V_QOFF[j])),
+                    I(f"v_mul_lo_u32 v{V_OOFF[j]}, v{x}, s{Rdo}", VALU, rd=vr(x) + sr(Rdo), wr=vr(V_OOFF[j])),
+                    I(f"v_lshl_add_u32 v{V_OOFF[j]}, v{hh}, 4, v{V_OOFF[j]}", VALU, rd=vr(hh) + vr(V_OOFF[j]), wr=vr(V_OOFF[j])),
+                    # causal mask limit base: q - 4 hh (q = m0 + row)
+                    I(f"v_add_u32_e32 v{V_LIM[j]}, s{M0R}, v{x}", VALU, rd=sr(M0R) + vr(x), wr=vr(V_LIM[j])),
+                    I(f"v_lshlrev_b32_e32 v{x + 2}, 2, v{hh}", VALU, rd=vr(hh), wr=vr(x + 2)),
+                    I(f"v_sub_u32_e32 v{V_LIM[j]}, v{V_LIM[j]}, v{x + 2}", VALU, rd=vr(V_LIM[j]) + vr(x + 2), wr=vr(V_LIM[j]))]
+        # Q / dO fragments into AGPRs: lane holds row[16 ks + 8 hh .. +7]
+        for j in range(2):
+            for ks in range(KS):
+                ins.append(I(f"buffer_load_dwordx4 {rtxt('a', QF(j, ks), 4)}, v{V_QOFF[j]}, s[{S_QD}:{S_QD + 3}], 0 offen offset:{32 * ks}",
+                             VLOAD, rd=vr(V_QOFF[j]) + sr(S_QD, 4), wr=ar(QF(j, ks), 4)))
+        for j in range(2):
+            for ks in range(KS):
+                ins.append(I(f"buffer_load_dwordx4 {rtxt('a', OF(j, ks), 4)}, v{V_OOFF[j]}, s[{S_OD}:{S_OD + 3}], 0 offen offset:{32 * ks}",
+                             VLOAD, rd=vr(V_OOFF[j]) + sr(S_OD, 4), wr=ar(OF(j, ks), 4)))
+        # dQ row offsets (epilogue) replace the Q / dO ones once those loads are issued
+        for j in range(2):
+            ins += [I(f"v_lshl_add_u32 v{x}, v1, 6, v{r_}", VALU, rd=vr(1) + vr(r_), wr=vr(x)),
+                    I(f"v_add_u32_e32 v{x}, {32 * j}, v{x}", VALU, rd=vr(x), wr=vr(x)),
+                    I(f"v_mul_lo_u32 v{x + 3}, v{x}, s{Rdq}", VALU, rd=vr(x) + sr(Rdq), wr=vr(x + 3)),
+                    I(f"v_lshl_add_u32 v{V_QOFF[j]}, v{hh}, 4, v{x + 3}", VALU, rd=vr(hh) + vr(x + 3), wr=vr(V_QOFF[j]))]
+        # dQ descriptor (S_QD is still read by the loads above: the epilogue builds it in S_OD... kept
+        # in SGPRs nothing rewrites: 92..95)
+        ins += desc(92, Pdq, DQOFF, HEAD, Hdq, M0R, Rdq, [I(f"s_mul_i32 s94, s{NROW}, s{Rdq}", SALU, rd=sr(NROW) + sr(Rdq), wr=sr(94))])
+        # LDS lane bases (as gen_fwd.py)
+        ins += [I(f"v_bfe_u32 v{x}, v{r_}, 2, 2", VALU, rd=vr(r_), wr=vr(x)),
+                I(f"v_xor_b32_e32 v{x + 1}, v{hh}, v{x}", VALU, rd=vr(hh) + vr(x), wr=vr(x + 1)),
+                I(f"v_lshlrev_b32_e32 v{x + 2}, 6, v{r_}", VALU, rd=vr(r_), wr=vr(x + 2)),
+                I(f"v_lshl_add_u32 v{V_RB0}, v{x + 1}, 4, v{x + 2}", VALU, rd=vr(x + 1) + vr(x + 2), wr=vr(V_RB0)),
+                I(f"v_add_u32_e32 v{x + 1}, 2, v{hh}", VALU, rd=vr(hh), wr=vr(x + 1)),
+                I(f"v_xor_b32_e32 v{x + 1}, v{x + 1}, v{x}", VALU, rd=vr(x + 1) + vr(x), wr=vr(x + 1)),
+                I(f"v_lshl_add_u32 v{V_RB1}, v{x + 1}, 4, v{x + 2}", VALU, rd=vr(x + 1) + vr(x + 2), wr=vr(V_RB1))]
+        ins += [I(f"v_and_b32_e32 v{x}, 15, v{V_LANE}", VALU, rd=vr(V_LANE), wr=vr(x)),             # i
+                I(f"v_lshrrev_b32_e32 v{x + 1}, 2, v{x}", VALU, rd=vr(x), wr=vr(x + 1)),            # q
+                I(f"v_and_b32_e32 v{x + 2}, 3, v{x}", VALU, rd=vr(x), wr=vr(x + 2)),                # pp
+                I(f"v_lshrrev_b32_e32 v{x + 3}, 4, v{r_}", VALU, rd=vr(r_), wr=vr(x + 3)),          # r >> 4
+                I(f"v_lshrrev_b32_e32 v{x + 4}, 1, v{x + 2}", VALU, rd=vr(x + 2), wr=vr(x + 4)),    # pp >> 1
+                I(f"v_lshl_add_u32 v{x + 3}, v{x + 3}, 1, v{x + 4}", VALU, rd=vr(x + 3) + vr(x + 4), wr=vr(x + 3)),   # trc
+                I(f"v_lshl_add_u32 v{x + 4}, v{hh}, 2, v{x + 1}", VALU, rd=vr(hh) + vr(x + 1), wr=vr(x + 4)),      # 4 hh + q
+                I(f"v_lshlrev_b32_e32 v{x + 4}, 6, v{x + 4}", VALU, rd=vr(x + 4), wr=vr(x + 4)),
+                I(f"v_and_b32_e32 v{x + 5}, 1, v{x + 2}", VALU, rd=vr(x + 2), wr=vr(x + 5)),
+                I(f"v_lshl_add_u32 v{x + 4}, v{x + 5}, 3, v{x + 4}", VALU, rd=vr(x + 5) + vr(x + 4), wr=vr(x + 4)),
+                I(f"v_xor_b32_e32 v{x + 5}, v{x + 3}, v{hh}", VALU, rd=vr(x + 3) + vr(hh), wr=vr(x + 5)),
+                I(f"v_lshl_add_u32 v{V_TB0}, v{x + 5}, 4, v{x + 4}", VALU, rd=vr(x + 5) + vr(x + 4), wr=vr(V_TB0)),
+                I(f"v_add_u32_e32 v{x + 5}, 2, v{hh}", VALU, rd=vr(hh), wr=vr(x + 5)),
+                I(f"v_xor_b32_e32 v{x + 5}, v{x + 3}, v{x + 5}", VALU, rd=vr(x + 3) + vr(x + 5), wr=vr(x + 5)),
+                I(f"v_lshl_add_u32 v{V_TB1}, v{x + 5}, 4, v{x + 4}", VALU, rd=vr(x + 5) + vr(x + 4), wr=vr(V_TB1))]
+        # DMA voffsets: wave w, half f: row = 16 f + lane / 4, col = 64 w + 16 ((lane & 3) ^ ((lane >> 4) & 3))
+        ins += [I(f"v_lshrrev_b32_e32 v{x}, 2, v{V_LANE}", VALU, rd=vr(V_LANE), wr=vr(x)),
+                I(f"v_bfe_u32 v{x + 1}, v{V_LANE}, 4, 2", VALU, rd=vr(V_LANE), wr=vr(x + 1)),
+                I(f"v_and_b32_e32 v{x + 2}, 3, v{V_LANE}", VALU, rd=vr(V_LANE), wr=vr(x + 2)),
+                I(f"v_xor_b32_e32 v{x + 1}, v{x + 1}, v{x + 2}", VALU, rd=vr(x + 1, 2), wr=vr(x + 1)),
+                I(f"v_lshlrev_b32_e32 v{x + 1}, 4, v{x + 1}", VALU, rd=vr(x + 1), wr=vr(x + 1)),
+                I(f"s_lshl_b32 s{T[0]}, s{S_WAVE}, 6", SALU, rd=sr(S_WAVE), wr=sr(T[0])),
+                I(f"v_add_u32_e32 v{x + 1}, s{T[0]}, v{x + 1}", VALU, rd=sr(T[0]) + vr(x + 1), wr=vr(x + 1)),
+                I(f"v_mul_lo_u32 v{V_KV0}, v{x}, s{Rkv}", VALU, rd=vr(x) + sr(Rkv), wr=vr(V_KV0)),
+                I(f"v_add_u32_e32 v{V_KV0}, v{V_KV0}, v{x + 1}", VALU, rd=vr(V_KV0) + vr(x + 1), wr=vr(V_KV0)),
+                I(f"s_lshl_b32 s{T[0]}, s{Rkv}, 4", SALU, rd=sr(Rkv), wr=sr(T[0])),
+                I(f"v_add_u32_e32 v{V_KV1}, s{T[0]}, v{V_KV0}", VALU, rd=sr(T[0]) + vr(V_KV0), wr=vr(V_KV1)),
+                I(f"v_mov_b32_e32 v{V_NINF}, 0xff800000", VALU, wr=vr(V_NINF))]
+        # ---- loop state ----
+        ins += [I(f"s_lshl_b32 s{S_W2K}, s{S_WAVE}, 11", SALU, rd=sr(S_WAVE), wr=sr(S_W2K)),
+                I(f"s_mov_b32 s{S_SDMA}, 0", SALU, wr=sr(S_SDMA)),
+                I(f"s_mov_b32 s{S_NLAST}, s{T[8]}", SALU, rd=sr(T[8]), wr=sr(S_NLAST)),
+                I(f"s_mov_b32 s{S_MASK0}, s{T[3]}", SALU, rd=sr(T[3]), wr=sr(S_MASK0)),
+                I(f"s_lshl_b32 s{S_KV32}, s{Rkv}, 5", SALU, rd=sr(Rkv), wr=sr(S_KV32)),
+                I(f"s_mov_b32 s{S_N}, 0", SALU, wr=sr(S_N))]
+        for i in range(128):
+            ins.append(I(f"v_accvgpr_write_b32 a{i}, 0", ACCW, wr=ar(i)))
+        # no keys: epilogue (dQ = 0)
+        ins += [I(f"s_cmp_lt_i32 s{S_NLAST}, 0", SALU, rd=sr(S_NLAST), wr=[("scc", 0)]),
+                I(f"s_cbranch_scc1 {l_epi}", BRANCH)]
+        return ins
+
+    def epilogue(self):
+        """dQ = scale dQ^T^T in bf16 / f16, rows < seqlen_q (range-checked; rows on lanes as gen_fwd.py)"""
+        I = Inst
+        ins = [I("s_waitcnt vmcnt(0)", WAIT)]
+        t = 0
+        for j in range(2):
+            for dt in range(NP):
+                for u in (0, 2):
+                    w = t + 4 + 4 * ((dt * 2 + u // 2) % 4)
+                    o = DQ(j, dt) + 4 * u
+                    x = t + 20
+                    ins += [I(f"v_accvgpr_read_b32 v{x + k}, a{o + k}", ACCR, rd=ar(o + k), wr=vr(x + k)) for k in range(8)]
+                    ins += [I(f"v_mul_f32_e32 v{x + k}, s{S_SCALE}, v{x + k}", VALU, rd=sr(S_SCALE) + vr(x + k), wr=vr(x + k))
+                            for k in range(8)]
+                    ins += [self.cvt(w + 0, x + 0, x + 1), self.cvt(w + 1, x + 2, x + 3),
+                            self.cvt(w + 2, x + 4, x + 5), self.cvt(w + 3, x + 6, x + 7)]
+                    ins += [I(f"v_permlane32_swap_b32_e32 v{w}, v{w + 2}", PERM, rd=vr(w) + vr(w + 2), wr=vr(w) + vr(w + 2)),
+                            I(f"v_permlane32_swap_b32_e32 v{w + 1}, v{w + 3}", PERM, rd=vr(w + 1) + vr(w + 3), wr=vr(w + 1) + vr(w + 3))]
+                    ins.append(I(f"buffer_store_dwordx4 v[{w}:{w + 3}], v{V_QOFF[j]}, s[92:95], 0 offen offset:{64 * dt + 16 * u}",
+                                 VSTORE, rd=vr(w, 4) + vr(V_QOFF[j]) + sr(92, 4)))
+        return ins
+
+    # ------------------------------------------------------------------ whole kernel
+    def build(self):
+        self.lab_end = self.lab("end")
+        l_epi = self.lab("epi")
+        code = []
+
+        def emit(insts, pre=()):
+            out, _ = add_waits(insts)
+            out, _ = fix_hazards(out, pre=pre)
+            code.extend(out)
+
+        pro = self.prologue(l_epi)
+        for _ in range(KQ):
+            pro += self.dma_subtile()
+        # K / V(0) and (1) landed (phase -1 reads 0, its tail prefetches 1): 16 younger DMAs
+        pro += [Inst("s_waitcnt vmcnt(16)", WAIT), Inst("s_barrier", BARRIER)]
+        emit(pro)
+        # phase -1: S^T / dP^T(0) -> buffers 0
+        # -LSE log2 e (LSE = +inf -> -inf: P = 0); the loads landed with the prologue's wait
+        ph = [Inst(f"v_mul_f32_e32 v{V_NLC[j]}, 0xbfb8aa3b, v{V_NLC[j]}", VALU, rd=vr(V_NLC[j]), wr=vr(V_NLC[j]), key=-500)
+              for j in range(2)]
+        ph += [Inst(f"s_mov_b32 s{S_SROW}, 0", SALU, wr=sr(S_SROW)),
+              Inst(f"s_mov_b32 s{S_STR}, {RING - 2 * SLOT}", SALU, wr=sr(S_STR)),
+              Inst(f"v_add_u32_e32 v{V_KB0}, 0, v{V_RB0}", VALU, rd=vr(V_RB0), wr=vr(V_KB0)),
+              Inst(f"v_add_u32_e32 v{V_KB1}, 0, v{V_RB1}", VALU, rd=vr(V_RB1), wr=vr(V_KB1))]
+        mf, frags = self.phase_mfmas(1, True, False)
+        fill = []
+        for f, (t, i) in enumerate(frags):
+            fill += self.frag_reads(f, t, i, key=-100 + f, deadline=max(2 * f - OPT_LEAD, 0))
+        fill += self.slot_advance(S_SROW, key=400) + self.slot_advance(S_STR, key=400)
+        fill += [Inst(f"v_add_u32_e32 v{V_KB0}, s{S_SROW}, v{V_RB0}", VALU, rd=sr(S_SROW) + vr(V_RB0), wr=vr(V_KB0), key=401),
+                 Inst(f"v_add_u32_e32 v{V_KB1}, s{S_SROW}, v{V_RB1}", VALU, rd=sr(S_SROW) + vr(V_RB1), wr=vr(V_KB1), key=401),
+                 Inst(f"v_add_u32_e32 v{V_VB0}, s{S_STR}, v{V_TB0}", VALU, rd=sr(S_STR) + vr(V_TB0), wr=vr(V_VB0), key=401),
+                 Inst(f"v_add_u32_e32 v{V_VB1}, s{S_STR}, v{V_TB1}", VALU, rd=sr(S_STR) + vr(V_TB1), wr=vr(V_VB1), key=401)]
+        nfr = self.phase_frags(True, False)
+        for f in range(3):
+            t, i = nfr[f]
+            fill += self.frag_reads(f, t, i, key=600 + f, earliest=2 * f + 1)
+        sch = schedule(mf, ph + fill)
+        sch += [Inst(f"s_waitcnt vmcnt({VMCNT_STEP}) lgkmcnt(0)", WAIT), Inst("s_barrier", BARRIER)]
+        emit(sch, pre=[nop(15)])
+        L = {}
+        variants = [(f, l, m) for f in (True, False) for l in (True, False) for m in ((True, False) if self.causal else (False,))]
+        for v in variants:
+            L[v] = self.lab("step_" + ("".join(c for c, on in zip("FLM", v) if on) or "R"))
+        l_tail = self.lab("tail")
+        l_disp = self.lab("dispatch")
+        l_notlast = self.lab("notlast")
+        l_first = self.lab("first")
+        # entry: the first step (masked when causal and m0 == 0)
+        code.append(label(l_first))
+        code += [Inst(f"s_cmp_eq_u32 s{S_NLAST}, 0", SALU), Inst(f"s_cbranch_scc1 {l_first}_last", BRANCH)]
+        if self.causal:
+            code += [Inst(f"s_cmp_eq_u32 s{S_MASK0}, 0", SALU), Inst(f"s_cbranch_scc1 {L[(True, False, True)]}", BRANCH)]
+        code += [Inst(f"s_branch {L[(True, False, False)]}", BRANCH), label(f"{l_first}_last")]
+        if self.causal:
+            code += [Inst(f"s_cmp_eq_u32 s{S_MASK0}, 0", SALU), Inst(f"s_cbranch_scc1 {L[(True, True, True)]}", BRANCH)]
+        code += [Inst(f"s_branch {L[(True, True, False)]}", BRANCH)]
+        # dispatch: done? last? masked (S_N >= S_MASK0)?
+        code += [label(l_disp), Inst(f"s_cmp_gt_u32 s{S_N}, s{S_NLAST}", SALU), Inst(f"s_cbranch_scc1 {l_tail}", BRANCH),
+                 Inst(f"s_cmp_lt_u32 s{S_N}, s{S_NLAST}", SALU), Inst(f"s_cbranch_scc1 {l_notlast}", BRANCH)]
+        if self.causal:
+            code += [Inst(f"s_cmp_ge_u32 s{S_N}, s{S_MASK0}", SALU), Inst(f"s_cbranch_scc1 {L[(False, True, True)]}", BRANCH)]
+        code += [Inst(f"s_branch {L[(False, True, False)]}", BRANCH), label(l_notlast)]
+        if self.causal:
+            code += [Inst(f"s_cmp_ge_u32 s{S_N}, s{S_MASK0}", SALU), Inst(f"s_cbranch_scc1 {L[(False, False, True)]}", BRANCH)]
+        code += [Inst(f"s_branch {L[(False, False, False)]}", BRANCH)]
+        pad = [nop(15)]
+        for v in variants:
+            f, l, m = v
+            code.append(label(L[v]))
+            emit(self.step(f, l, m) + self.step_end(), pre=pad)
+            code.append(Inst(f"s_branch {l_disp}", BRANCH))
+        code.append(label(l_tail))
+        emit(self.tail(), pre=pad)
+        code.append(label(l_epi))
+        emit([nop(15)] + self.epilogue(), pre=pad)
+        code.append(label(self.lab_end))
+        code.append(Inst("s_endpgm", SOPP))
+        return code
+
+    def render(self):
+        code = self.build()
+        out = [f"\t.globl {self.name}", "\t.p2align 8", f"\t.type {self.name},@function", f"{self.name}:"]
+        for ins in code:
+            out.append(ins.text if ins.kind == LABEL else "\t" + ins.text)
+        out.append(f".L{self.name}_fend:")
+        out.append(f"\t.size {self.name}, .L{self.name}_fend-{self.name}")
+        return "\n".join(out)
+
+    def descriptor(self):
+        return f"""
+	.rodata
+	.p2align 6
+	.amdhsa_kernel {self.name}
+		.amdhsa_group_segment_fixed_size {LDS_BYTES}
+		.amdhsa_private_segment_fixed_size 0
+		.amdhsa_kernarg_size {KARG_SIZE}
+		.amdhsa_user_sgpr_count 2
+		.amdhsa_user_sgpr_kernarg_segment_ptr 1
+		.amdhsa_system_sgpr_workgroup_id_x 1
+		.amdhsa_system_vgpr_workitem_id 0
+		.amdhsa_next_free_vgpr 512
+		.amdhsa_next_free_sgpr {NSGPR}
+		.amdhsa_accum_offset 256
+		.amdhsa_reserve_vcc 1
+		.amdhsa_float_denorm_mode_32 3
+		.amdhsa_float_denorm_mode_16_64 3
+		.amdhsa_dx10_clamp 1
+		.amdhsa_ieee_mode 0
+	.end_amdhsa_kernel
+	.text
+"""
+
+    def metadata(self):
+        return f"""  - .agpr_count: 256
+    .args:
+      - .offset: 0
+        .size: {KARG_SIZE}
+        .value_kind: by_value
+    .group_segment_fixed_size: {LDS_BYTES}
+    .kernarg_segment_align: 8
+    .kernarg_segment_size: {KARG_SIZE}
+    .max_flat_workgroup_size: 256
+    .name: {self.name}
+    .private_segment_fixed_size: 0
+    .sgpr_count: {NSGPR + 2}
+    .sgpr_spill_count: 0
+    .symbol: {self.name}.kd
+    .uniform_work_group_size: 1
+    .vgpr_count: 512
+    .vgpr_spill_count: 0
+    .wavefront_size: 64
+"""
+
+
+def main():
+    kernels = [K(bf, ca) for bf in (True, False) for ca in (True, False)]
+    out = ['\t.amdgcn_target "amdgcn-amd-amdhsa--gfx950"', "\t.amdhsa_code_object_version 5", "\t.text"]
+    for k in kernels:
+        out.append(k.render())
+        out.append(k.descriptor())
+    out.append("\t.amdgpu_metadata\n---\namdhsa.kernels:")
+    for k in kernels:
+        out.append(k.metadata().rstrip("\n"))
+    out.append("amdhsa.target: amdgcn-amd-amdhsa--gfx950\namdhsa.version:\n  - 1\n  - 2\n...\n\t.end_amdgpu_metadata")
+    sys.stdout.write("\n".join(out) + "\n")
+
+
+if __name__ == "__main__":
+    main()

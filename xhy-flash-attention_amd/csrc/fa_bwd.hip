@@ -1064,7 +1064,9 @@ static void run_bwd(const BwdParams& p, hipStream_t stream) {
   auto dq = [&](hipStream_t st) {
     dim3 grid(p.s.b * p.s.h * ((p.s.seqlen_q + DqTile<D>::BM - 1) / DqTile<D>::BM));
     prof_begin(kTimeBwdDq, st);
-    if (masked)
+    if (D == 128 && !DROPOUT && !masked && dq_asm_applicable(p))   // the assembly dQ kernel (fa_bwd_asm.cpp)
+      launch_bwd_dq_asm(p, BF16, st);
+    else if (masked)
       hipLaunchKernelGGL((bwd_dq_kernel<BF16, D, CAUSAL, DROPOUT, true>), grid, dim3(DqTile<D>::NW * 64), 0, st, p);
     else
       hipLaunchKernelGGL((bwd_dq_kernel<BF16, D, CAUSAL, DROPOUT, false>), grid, dim3(DqTile<D>::NW * 64), 0, st, p);

@@ -1,5 +1,6 @@
-// Host side of the hand-scheduled assembly dK / dV kernel (csrc/asm/gen_bwd.py -> fa_bwd_asm.s,
-// assembled for gfx950 and embedded in this library as a code object).
+// Host side of the hand-scheduled assembly backward kernels (csrc/asm/gen_bwd.py -> fa_bwd_asm.s for
+// dK / dV, csrc/asm/gen_dq.py -> fa_dq_asm.s for dQ; assembled for gfx950 and embedded in this
+// library as code objects).
 //
 // The kernel covers the headline backward: head dim 128, bf16 / fp16, causal or not, fixed length
 // or varlen, MHA / GQA (reduced in-kernel over the group, or expanded per query head), no dropout /
@@ -10,6 +11,11 @@
 //
 // Work order: a per-shape table maps workgroup -> (batch, head, kv head, 128-key block) in the HIP
 // kernel's xcd_order (heaviest causal key block first, the blocks of one head on one XCD).
+//
+// The dQ kernel (same operand coverage; K and V must share their row and batch strides) replaces
+// bwd_dq_kernel: 256-row query blocks in the forward's work order (xcd_order_grouped with the
+// launcher's dq_head_group), reading LSE and D (softmax_d) directly.  FLASH_ATTN_MI355X_DQ_ASM=0 (or
+// knob 4) keeps bwd_dq_kernel.
 #include <hip/hip_runtime.h>
 
 #include <cstdint>
@@ -25,6 +31,8 @@
 
 extern "C" const unsigned char fa_bwd_asm_co[];
 extern "C" const unsigned long fa_bwd_asm_co_size;
+extern "C" const unsigned char fa_dq_asm_co[];
+extern "C" const unsigned long fa_dq_asm_co_size;
 
 namespace fa {
 namespace {
@@ -43,18 +51,35 @@ struct BwdAsmArgs {
 };
 static_assert(sizeof(BwdAsmArgs) == 216, "BwdAsmArgs layout");
 
+// must match the kernarg loads of gen_dq.py (K.prologue) and KARG_SIZE
+struct DqAsmArgs {
+  const void* q; const void* k; const void* v; const void* dout; void* dq;
+  const float* lse; const float* dsum; const uint32_t* sched; const int* cu_q; const int* cu_k;
+  int64_t q_batch, kv_batch, do_batch, dq_batch;                    // bytes
+  int32_t q_row, kv_row, do_row, dq_row;                            // bytes
+  int32_t q_head, k_head, v_head, do_head, dq_head;                 // bytes
+  int32_t sq, sk, lse_pitch, dsum_pitch, h, hk;
+  int32_t flags;    // bit 0: varlen_padded_input
+  float c, scale;
+};
+static_assert(sizeof(DqAsmArgs) == 184, "DqAsmArgs layout");
+
 constexpr int kMaxDev = 64;
 constexpr int kBkn = 128;   // keys per workgroup
 struct DevModule {
-  hipModule_t mod = nullptr;
-  hipFunction_t fn[4] = {};   // [bf16 causal, bf16 full, f16 causal, f16 full]
+  hipModule_t mod = nullptr, mod_dq = nullptr;
+  hipFunction_t fn[4] = {};      // dK/dV [bf16 causal, bf16 full, f16 causal, f16 full]
+  hipFunction_t fn_dq[4] = {};   // dQ, the same order
   std::map<std::tuple<int, int, int, int>, uint32_t*> tables;
+  std::map<std::tuple<int, int, int, int, int>, uint32_t*> dq_tables;
 };
 std::mutex g_mu;
 DevModule g_dev[kMaxDev];
 
 const char* kNames[4] = {"fa_bwd_dkdv_asm_d128_bf16_causal", "fa_bwd_dkdv_asm_d128_bf16_full",
                          "fa_bwd_dkdv_asm_d128_f16_causal", "fa_bwd_dkdv_asm_d128_f16_full"};
+const char* kDqNames[4] = {"fa_bwd_dq_asm_d128_bf16_causal", "fa_bwd_dq_asm_d128_bf16_full",
+                           "fa_bwd_dq_asm_d128_f16_causal", "fa_bwd_dq_asm_d128_f16_full"};
 
 void check(hipError_t e, const char* what) {
   if (e != hipSuccess) throw std::runtime_error(std::string("flash_attn_bwd (asm dK/dV): ") + what + ": " + hipGetErrorString(e));
@@ -66,8 +91,39 @@ DevModule& module_for(int dev) {
   if (m.mod == nullptr) {
     check(hipModuleLoadData(&m.mod, fa_bwd_asm_co), "hipModuleLoadData");
     for (int i = 0; i < 4; ++i) check(hipModuleGetFunction(&m.fn[i], m.mod, kNames[i]), kNames[i]);
+    check(hipModuleLoadData(&m.mod_dq, fa_dq_asm_co), "hipModuleLoadData (dQ)");
+    for (int i = 0; i < 4; ++i) check(hipModuleGetFunction(&m.fn_dq[i], m.mod_dq, kDqNames[i]), kDqNames[i]);
   }
   return m;
+}
+
+// workgroup -> (bidb | head << 16, kvh | m_block << 16): the forward's order (fa_common.h
+// xcd_order_grouped, heaviest causal query block first)
+std::vector<uint32_t> build_dq_table(int b, int h, int hk, int nmb, int hp) {
+  const int nbh = b * h;
+  const long long n = (long long)nbh * nmb;
+  std::vector<uint32_t> t((size_t)n * 2);
+  const int g = h / hk;
+  for (long long L = 0; L < n; ++L) {
+    int bh, blk;
+    if ((nbh & 7) == 0 && hp > 0 && ((nbh >> 3) % hp) == 0) {
+      const long long i = L >> 3;
+      const long long per_group = (long long)hp * nmb;
+      const long long gi = i / per_group;
+      const long long r = i - gi * per_group;
+      blk = (int)(r / hp);
+      const long long hl = gi * hp + (r - (long long)blk * hp);
+      bh = (int)(hl * 8 + (L & 7));
+    } else {
+      blk = (int)(L / nbh);
+      bh = (int)(L - (long long)blk * nbh);
+    }
+    const int mb = nmb - 1 - blk;
+    const int bidb = bh / h, head = bh - bidb * h;
+    t[2 * L] = (uint32_t)bidb | ((uint32_t)head << 16);
+    t[2 * L + 1] = (uint32_t)(head / g) | ((uint32_t)mb << 16);
+  }
+  return t;
 }
 
 // workgroup -> (bidb | hx << 16, kvh | kblock << 16): fa_common.h xcd_order over nbh = b * heads
@@ -164,6 +220,65 @@ void launch_bwd_dkdv_asm(const BwdParams& p, bool is_bf16, hipStream_t stream) {
   size_t sz = sizeof(a);
   void* cfg[] = {HIP_LAUNCH_PARAM_BUFFER_POINTER, &a, HIP_LAUNCH_PARAM_BUFFER_SIZE, &sz, HIP_LAUNCH_PARAM_END};
   check(hipModuleLaunchKernel(fn, (unsigned)nwg, 1, 1, 256, 1, 1, 0, stream, nullptr, cfg), "hipModuleLaunchKernel");
+}
+
+bool dq_asm_applicable(const BwdParams& p) {
+  const AttnShape& s = p.s;
+  if (knob(kKnobDqAsm) == 0) return false;
+  if (s.d != 128 || s.dropout || s.mask != nullptr || s.fm_lts != nullptr) return false;
+  if (s.hk <= 0 || s.h % s.hk != 0 || s.b > 65535 || s.h > 65535) return false;
+  if (p.k_row != p.v_row || p.k_batch != p.v_batch) return false;   // K / V share the DMA offsets
+  const int nmb = (s.seqlen_q + 255) / 256;
+  if (nmb > 65535 || (long long)s.b * s.h * nmb > 0x7fffffffll) return false;
+  for (int64_t x : {p.q_row, p.k_row, p.do_row, p.dq_row, p.q_head, p.k_head, p.v_head, p.do_head, p.dq_head})
+    if (!fits32(2 * x)) return false;
+  const int64_t sq = s.seqlen_q + 256, sk = s.seqlen_k + 64;
+  for (int64_t x : {256 * 2 * p.q_row, 256 * 2 * p.do_row, 256 * 2 * p.dq_row, sk * 2 * p.k_row})
+    if (!fits32(x)) return false;
+  (void)sq;
+  return true;
+}
+
+void launch_bwd_dq_asm(const BwdParams& p, bool is_bf16, hipStream_t stream) {
+  const AttnShape& s = p.s;
+  const int nmb = (s.seqlen_q + 255) / 256;
+  const long long nwg = (long long)s.b * s.h * nmb;
+  if (nwg <= 0) return;
+  int dev = 0;
+  check(hipGetDevice(&dev), "hipGetDevice");
+  hipFunction_t fn;
+  uint32_t* table;
+  {
+    std::lock_guard<std::mutex> lk(g_mu);
+    DevModule& m = module_for(dev);
+    fn = m.fn_dq[(is_bf16 ? 0 : 2) + (s.causal ? 0 : 1)];
+    auto key = std::make_tuple(s.b, s.h, s.hk, nmb, p.dq_head_group);
+    auto it = m.dq_tables.find(key);
+    if (it == m.dq_tables.end()) {
+      std::vector<uint32_t> t = build_dq_table(s.b, s.h, s.hk, nmb, p.dq_head_group);
+      uint32_t* d = nullptr;
+      check(hipMalloc(&d, t.size() * sizeof(uint32_t)), "hipMalloc (dQ schedule table)");
+      check(hipMemcpy(d, t.data(), t.size() * sizeof(uint32_t), hipMemcpyHostToDevice), "hipMemcpy (dQ schedule table)");
+      it = m.dq_tables.emplace(key, d).first;
+    }
+    table = it->second;
+  }
+  DqAsmArgs a;
+  std::memset(&a, 0, sizeof(a));
+  a.q = p.q; a.k = p.k; a.v = p.v; a.dout = p.dout; a.dq = p.dq;
+  a.lse = p.lse; a.dsum = p.dsum; a.sched = table; a.cu_q = s.cu_seqlens_q; a.cu_k = s.cu_seqlens_k;
+  a.q_batch = 2 * p.q_batch; a.kv_batch = 2 * p.k_batch; a.do_batch = 2 * p.do_batch; a.dq_batch = 2 * p.dq_batch;
+  a.q_row = (int32_t)(2 * p.q_row); a.kv_row = (int32_t)(2 * p.k_row); a.do_row = (int32_t)(2 * p.do_row);
+  a.dq_row = (int32_t)(2 * p.dq_row);
+  a.q_head = (int32_t)(2 * p.q_head); a.k_head = (int32_t)(2 * p.k_head); a.v_head = (int32_t)(2 * p.v_head);
+  a.do_head = (int32_t)(2 * p.do_head); a.dq_head = (int32_t)(2 * p.dq_head);
+  a.sq = s.seqlen_q; a.sk = s.seqlen_k; a.lse_pitch = s.lse_pitch; a.dsum_pitch = p.seqlen_q_rounded;
+  a.h = s.h; a.hk = s.hk;
+  a.flags = s.varlen_padded_input ? 1 : 0;
+  a.c = s.scale_log2; a.scale = s.scale;
+  size_t sz = sizeof(a);
+  void* cfg[] = {HIP_LAUNCH_PARAM_BUFFER_POINTER, &a, HIP_LAUNCH_PARAM_BUFFER_SIZE, &sz, HIP_LAUNCH_PARAM_END};
+  check(hipModuleLaunchKernel(fn, (unsigned)nwg, 1, 1, 256, 1, 1, 0, stream, nullptr, cfg), "hipModuleLaunchKernel (dQ)");
 }
 
 }  // namespace fa

@@ -145,7 +145,9 @@ void fwd_asm_enable(int on);
 void launch_bwd(const BwdParams& p, bool is_bf16, hipStream_t stream);
 void bwd_overlap_enable(int mode);
 bool bwd_asm_applicable(const BwdParams& p);                        // fa_bwd_asm.cpp
-void launch_bwd_dkdv_asm(const BwdParams& p, bool is_bf16, hipStream_t stream);   // fa_bwd.hip: dQ / dK-dV stream overlap mode (default 0: off)
+void launch_bwd_dkdv_asm(const BwdParams& p, bool is_bf16, hipStream_t stream);
+bool dq_asm_applicable(const BwdParams& p);                         // fa_bwd_asm.cpp
+void launch_bwd_dq_asm(const BwdParams& p, bool is_bf16, hipStream_t stream);   // fa_bwd.hip: dQ / dK-dV stream overlap mode (default 0: off)
 void launch_reduced_scores(const ReducedParams& p, bool is_bf16, hipStream_t stream);
 void launch_rotary(const RotaryParams& p, bool interleaved, bool conj, bool is_bf16, hipStream_t stream);
 
@@ -165,7 +167,8 @@ enum Knob { kKnobNoSplitKv = 0 /* FLASH_ATTN_MI355X_NO_SPLITKV: 1 = never split 
             kKnobNoXcdGroup = 1 /* FLASH_ATTN_MI355X_NO_XCD_GROUP: 1 = head-fastest order */,
             kKnobXcdGroupMinMiB = 2 /* FLASH_ATTN_MI355X_XCD_GROUP_MIN_MIB: grouping threshold */,
             kKnobBwdAsm = 3 /* FLASH_ATTN_MI355X_BWD_ASM: 0 = HIP dK/dV kernel for every call */,
-            kNumKnobs = 4 };
+            kKnobDqAsm = 4 /* FLASH_ATTN_MI355X_DQ_ASM: 0 = HIP dQ kernel for every call */,
+            kNumKnobs = 5 };
 int knob(int id);
 void set_knob(int id, int value);
 
