@@ -62,3 +62,38 @@ def test_generated_dkdv_kernels_are_hazard_free():
             prev = lines[i - 1]
             assert not (prev.startswith("v_") and not prev.startswith("v_readfirstlane")
                         and prev.split()[1].rstrip(",") == src), (i, prev)
+
+
+# ------------------------------------------------------------------------------------------------
+# the assembly dQ kernel (csrc/asm/gen_dq.py), against the float64 dQ of tools/emu_dq.py
+# ------------------------------------------------------------------------------------------------
+@pytest.fixture(scope="module")
+def dq_text():
+    import emu_dq
+    return emu_dq.asm_text()
+
+
+@pytest.mark.timeout(900)
+@pytest.mark.parametrize("b,sq,sk,h,hk,causal,bf16", [
+    (1, 64, 64, 1, 1, True, True),              # one step: first + last + masked
+    (1, 300, 300, 1, 1, True, True),            # fast -> masked, ragged both
+    (1, 330, 200, 2, 1, True, True),            # GQA, sq > sk (rows past every key)
+    (1, 257, 129, 1, 1, False, True),           # full attention, odd subtile count (padded)
+    (1, 96, 300, 3, 1, True, False),            # fp16, sq < sk
+])
+def test_asm_dq_in_emulator(dq_text, b, sq, sk, h, hk, causal, bf16):
+    import emu_dq
+    e, *_ = emu_dq.run(b, sq, sk, h, hk, causal, bf16, seed=0, text=dq_text, verbose=False)
+    assert e <= (1e-2 if bf16 else 2e-3), e
+
+
+def test_generated_dq_kernels_assemble_shape():
+    text = subprocess.run([sys.executable, os.path.join(ROOT, "xhy-flash-attention_amd", "csrc", "asm", "gen_dq.py")],
+                          check=True, capture_output=True, text=True).stdout
+    assert text.count(".amdhsa_kernel ") == 4
+    assert ".amdhsa_group_segment_fixed_size 147456" in text
+    lines = [x.strip() for x in text.splitlines()]
+    for i, x in enumerate(lines):
+        if x.startswith("buffer_load_dword") and x.endswith(" lds"):
+            prev = lines[i - 1]
+            assert not prev.startswith("s_add_u32 m0") and not prev.startswith("s_mov_b32 m0"), (i, prev)

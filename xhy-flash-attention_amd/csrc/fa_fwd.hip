@@ -74,12 +74,16 @@ __global__ void __launch_bounds__(FwdTile<D>::NW * 64, FwdTile<D>::MINB) fwd_ker
   // every SIMD one wave opens its step with the softmax VALU while its partner opens with PV MFMAs
   // (MI355X_MICROARCH.md "Two waves per SIMD", item 9).  The late PV reads V(nb-1) while the DMA of
   // V(nb+3) is in flight, hence a 5-deep V ring next to the 4-deep K ring.
+  // (With dropout at d <= 64 the 5th V slot and the NW * NT KiB of random-byte scratch make the
+  // workgroup 88 KiB, one per CU.  Unstaggered with a 4-deep V ring it is 80 KiB, two per CU, but
+  // measured 7 % slower (d64 causal dropout forward, tools/ab.py: 2.205 vs 2.060 ms): kept staggered.)
   constexpr bool STAGGER = NW == 8;
   constexpr int VBUFS = STAGGER ? 5 : 4;
   constexpr int VBASE = kFwdBufs * TILE;
   constexpr int SCRATCH = VBASE + VBUFS * TILE;
+  constexpr int LDS_BYTES = SCRATCH + (DROPOUT ? NW * NT * 1024 : 0);
   // [K ring][V ring], then (dropout) NT 1-KiB random-byte scratch blocks per wave
-  __shared__ __attribute__((aligned(16))) char smem[SCRATCH + (DROPOUT ? NW * NT * 1024 : 0)];
+  __shared__ __attribute__((aligned(16))) char smem[LDS_BYTES];
   auto kslot = [&](int nb) { return (nb % kFwdBufs) * TILE; };
   auto vslot = [&](int nb) { return VBASE + (nb % VBUFS) * TILE; };
 
