@@ -8,7 +8,8 @@ ROOT=$(cd "$(dirname "$0")/.." && pwd)
 CS=$ROOT/xhy-flash-attention_amd/csrc
 W=/tmp/fa_asmv/$NAME
 rm -rf "$W"; mkdir -p "$W" "$ROOT/variants"
-make -s -C "$CS" >/dev/null
+# (the in-tree build must not see the dev switches)
+env $(env | grep -o '^FA_G[A-Z_]*' | sed 's/^/-u /') make -s -C "$CS" >/dev/null
 for k in fwd bwd dq; do
   python3 "$CS/asm/gen_$k.py" > "$W/fa_${k}_asm.s"
   /opt/rocm/lib/llvm/bin/clang -x assembler -target amdgcn-amd-amdhsa -mcpu=gfx950 -c "$W/fa_${k}_asm.s" -o "$W/fa_${k}_asm.o"

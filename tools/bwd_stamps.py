@@ -1,0 +1,69 @@
+#!/usr/bin/env python3
+"""Workgroup timeline of the assembly dK/dV kernel (dev tool): with a library whose kernel was
+generated with FA_GBW_STAMP=1 (tools/asm_variant.sh), every workgroup stores its start / end
+s_memtime and CU; per CU the workgroups are sorted by start and the gaps between them, the busy
+share and the tail are reported.
+
+    FA_GBW_STAMP=1 bash tools/asm_variant.sh stamp && python tools/bwd_stamps.py variants/libfa_stamp.so
+"""
+import ctypes
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "xhy-flash-attention_amd"))
+sys.path.insert(0, os.path.join(ROOT, "tools"))
+sys.path.insert(0, ROOT)
+
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+
+import flash_attn_2_cuda as m  # noqa: E402
+from ab import load  # noqa: E402
+
+
+def main(path, b=4, s=8192, h=16):
+    lib = load(path)
+    lib.flash_attn_debug_bwd_stamps.argtypes = [ctypes.c_void_p]
+    m._lib = lib
+    nwg = b * h * (s // 128)
+    buf = torch.zeros(nwg * 8, dtype=torch.int32, device="cuda")
+    q, k, v, do = (torch.randn(b, s, h, 128, device="cuda", dtype=torch.bfloat16) for _ in range(4))
+    scale = 128 ** -0.5
+    res = m.fwd(q, k, v, None, 0.0, scale, True, False, None)
+    for it in range(3):
+        lib.flash_attn_debug_bwd_stamps(ctypes.c_void_p(buf.data_ptr() if it == 2 else 0))
+        m.bwd(do, q, k, v, res[0], res[5], None, None, None, 0.0, scale, True, None, res[7])
+        torch.cuda.synchronize()
+    lib.flash_attn_debug_bwd_stamps(ctypes.c_void_p(0))
+    a = buf.cpu().numpy().view(np.uint32).reshape(nwg, 8)
+    start = a[:, 0].astype(np.int64) | (a[:, 1].astype(np.int64) << 32)
+    end = a[:, 5].astype(np.int64) | (a[:, 6].astype(np.int64) << 32)
+    hwid, xcc = a[:, 2], a[:, 3]
+    cu = (xcc.astype(np.int64) << 16) | ((hwid >> 8) & 0xFF)
+    t0 = start.min()
+    span = end.max() - t0
+    print(f"{nwg} workgroups, span {span} ticks (s_memtime), mean WG duration {np.mean(end - start):.0f}")
+    gaps, busy, tails, heads = [], [], [], []
+    for c in np.unique(cu):
+        idx = np.where(cu == c)[0]
+        o = idx[np.argsort(start[idx])]
+        st, en = start[o], end[o]
+        gaps += list(st[1:] - en[:-1])
+        busy.append((en - st).sum() / span)
+        heads.append(st[0] - t0)
+        tails.append(end.max() - en[-1])
+    gaps = np.array(gaps)
+    print(f"CUs {len(busy)}; WGs per CU {nwg / len(busy):.1f}; busy share mean {np.mean(busy):.3f} min {np.min(busy):.3f}")
+    print(f"gap between consecutive WGs on a CU: median {np.median(gaps):.0f} mean {gaps.mean():.0f} p90 {np.percentile(gaps, 90):.0f}"
+          f" ticks ({gaps.sum() / len(busy) / span:.3f} of the span per CU)")
+    print(f"first WG start after t0: median {np.median(heads):.0f}; tail after last WG end: median {np.median(tails):.0f} "
+          f"mean {np.mean(tails):.0f} ({np.mean(tails) / span:.3f} of the span)")
+    # durations of the heaviest / lightest key blocks (kblock from the WG's table order is unknown here:
+    # report the distribution)
+    d = end - start
+    print("WG duration percentiles (ticks): " + ", ".join(f"p{p} {np.percentile(d, p):.0f}" for p in (1, 10, 50, 90, 99)))
+
+
+if __name__ == "__main__":
+    main(sys.argv[1])

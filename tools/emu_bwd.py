@@ -51,8 +51,8 @@ def pack_args(**kw):
     out += struct.pack("<6i", kw["q_row"], kw["k_row"], kw["v_row"], kw["do_row"], kw["dk_row"], kw["dv_row"])
     out += struct.pack("<6i", kw["q_head"], kw["k_head"], kw["v_head"], kw["do_head"], kw["dk_head"], kw["dv_head"])
     out += struct.pack("<6i", kw["sq"], kw["sk"], kw["h"], kw["ng"], kw["nh"], kw["group"])
-    out += struct.pack("<ffii", kw["c"], kw["scale"], kw["flags"], 0)
-    assert len(out) == 216, len(out)
+    out += struct.pack("<ffiiQ", kw["c"], kw["scale"], kw["flags"], 0, 0)
+    assert len(out) == 224, len(out)
     return out
 
 

@@ -130,11 +130,15 @@ S_WAVE = 48
 S_TMP = 49                           # 49..55 (the prologue keeps kernargs in 56..101)
 NSGPR = 102
 
-KARG_SIZE = 216
+KARG_SIZE = 224
 
 # dev A/B switches, read when the .s is generated (tools/asm_variant.sh)
 OPT_WIN = int(os.environ.get("FA_GBW_WIN", "16"))     # an A fragment may be read up to WIN MFMAs ahead
 OPT_LEAD = int(os.environ.get("FA_GBW_LEAD", "2"))    # ... and at least LEAD MFMAs ahead
+# dev timeline: every workgroup stores {start, end} s_memtime, HW_ID, XCC_ID, id at the `stamps`
+# kernarg address + 32 id (tools/bwd_stamps.py)
+OPT_STAMP = os.environ.get("FA_GBW_STAMP") == "1"
+V_STAMP = 164          # 164..167: start lo / hi, HW_ID, XCC_ID (with OPT_STAMP)
 
 
 class K:
@@ -415,6 +419,13 @@ class K:
                 I(f"s_load_dwordx2 s[{S_C}:{S_SCALE}], s[0:1], 0xc8", SMEM, rd=sr(0, 2), wr=sr(S_C, 2)),
                 I("s_load_dword s3, s[0:1], 0xd0", SMEM, rd=sr(0, 2), wr=sr(3)),
                 I("s_waitcnt lgkmcnt(0)", WAIT)]
+        if OPT_STAMP:
+            ins += [I(f"s_memtime s[{S_TMP + 1}:{S_TMP + 2}]", SMEM, wr=sr(S_TMP + 1, 2)),
+                    I(f"s_getreg_b32 s{S_TMP + 3}, hwreg(HW_REG_HW_ID)", SALU, wr=sr(S_TMP + 3)),
+                    I(f"s_getreg_b32 s{S_TMP + 4}, hwreg(HW_REG_XCC_ID)", SALU, wr=sr(S_TMP + 4)),
+                    I("s_waitcnt lgkmcnt(0)", WAIT)]
+            ins += [I(f"v_mov_b32_e32 v{V_STAMP + i}, s{S_TMP + 1 + i}", VALU, rd=sr(S_TMP + 1 + i), wr=vr(V_STAMP + i)) for i in range(4)]
+            ins += [I(f"v_mov_b32_e32 v{V_STAMP + 4}, s2", VALU, rd=sr(2), wr=vr(V_STAMP + 4))]
         P = lambda i: ka + i   # noqa: E731
         Pq, Pk, Pv, Pdo, Pdk, Pdv, Pl, Psch, Pcq, Pck = (P(2 * i) for i in range(10))
         Bq, Bk, Bv, Bdo, Bdk, Bdv = (P(20 + 2 * i) for i in range(6))
@@ -798,6 +809,22 @@ class K:
         code.append(label(l_epi))
         emit([nop(15)] + self.epilogue(), pre=pad)
         code.append(label(self.lab_end))
+        if OPT_STAMP:
+            I = Inst
+            st = [I("s_waitcnt vmcnt(0)", WAIT),
+                  I(f"s_memtime s[{S_TMP + 1}:{S_TMP + 2}]", SMEM), I("s_load_dwordx2 s[52:53], s[0:1], 0xd8", SMEM),
+                  I("s_waitcnt lgkmcnt(0)", WAIT),
+                  I(f"v_mov_b32_e32 v{V_STAMP + 5}, s{S_TMP + 1}", VALU), I(f"v_mov_b32_e32 v{V_STAMP + 6}, s{S_TMP + 2}", VALU),
+                  I(f"v_mov_b32_e32 v{V_STAMP + 7}, s{S_WAVE}", VALU),
+                  # a NULL buffer (stamps off) gets zero records: the stores are dropped
+                  I("s_cmp_eq_u64 s[52:53], 0", SALU), I("s_cselect_b32 s54, 0, 0x7fffffff", SALU),
+                  I("s_mov_b32 s55, 0x20000", SALU),
+                  I("s_and_b32 s53, s53, 0xffff", SALU),
+                  I(f"v_lshlrev_b32_e32 v{V_STAMP + 8}, 5, v{V_STAMP + 4}", VALU), nop(4),
+                  I(f"buffer_store_dwordx4 v[{V_STAMP}:{V_STAMP + 3}], v{V_STAMP + 8}, s[52:55], 0 offen", VSTORE),
+                  I(f"buffer_store_dwordx4 v[{V_STAMP + 4}:{V_STAMP + 7}], v{V_STAMP + 8}, s[52:55], 0 offen offset:16", VSTORE),
+                  I("s_waitcnt vmcnt(0)", WAIT)]
+            code.extend(st)
         code.append(Inst("s_endpgm", SOPP))
         code.extend(self.ool)
         return code

@@ -48,8 +48,9 @@ struct BwdAsmArgs {
   float c, scale;
   int32_t flags;    // bit 0: varlen_padded_input, bit 1: dK / dV reduced over the GQA group
   int32_t pad;
+  void* stamps;     // dev timeline buffer (a generator build with FA_GBW_STAMP=1 writes it), else unused
 };
-static_assert(sizeof(BwdAsmArgs) == 216, "BwdAsmArgs layout");
+static_assert(sizeof(BwdAsmArgs) == 224, "BwdAsmArgs layout");
 
 // must match the kernarg loads of gen_dq.py (K.prologue) and KARG_SIZE
 struct DqAsmArgs {
@@ -154,6 +155,8 @@ std::vector<uint32_t> build_table(int b, int nh_grid, int h, int hk, int nblk, b
 
 bool fits32(int64_t x) { return x >= 0 && x < (1ll << 31); }
 
+void* g_stamps = nullptr;   // flash_attn_debug_bwd_stamps
+
 }  // namespace
 
 bool bwd_asm_applicable(const BwdParams& p) {
@@ -217,6 +220,7 @@ void launch_bwd_dkdv_asm(const BwdParams& p, bool is_bf16, hipStream_t stream) {
   a.nh = p.gqa_reduce ? a.group : 1;
   a.c = s.scale_log2; a.scale = s.scale;
   a.flags = (s.varlen_padded_input ? 1 : 0) | (p.gqa_reduce ? 2 : 0);
+  a.stamps = g_stamps;
   size_t sz = sizeof(a);
   void* cfg[] = {HIP_LAUNCH_PARAM_BUFFER_POINTER, &a, HIP_LAUNCH_PARAM_BUFFER_SIZE, &sz, HIP_LAUNCH_PARAM_END};
   check(hipModuleLaunchKernel(fn, (unsigned)nwg, 1, 1, 256, 1, 1, 0, stream, nullptr, cfg), "hipModuleLaunchKernel");
@@ -282,3 +286,6 @@ void launch_bwd_dq_asm(const BwdParams& p, bool is_bf16, hipStream_t stream) {
 }
 
 }  // namespace fa
+
+// Dev hook: the timeline buffer of a stamp build of the dK/dV kernel (tools/bwd_stamps.py); NULL off.
+extern "C" void flash_attn_debug_bwd_stamps(void* buf) { fa::g_stamps = buf; }
