@@ -1,4 +1,4 @@
-"""GPU parity at the BASELINE.json configs' full sizes (C4, C5), through the public API.
+"""GPU parity at the BASELINE.json configs' full sizes (C2, C3, C4, C5), through the public API.
 
 The reference's acceptance rule (tests/test_flash_attn.py:420-427, 630-639): max|x - ref| <= 2 x
 max|x_pt - ref|, ref = attention_ref in fp32, pt = attention_ref in the input dtype with
@@ -8,6 +8,11 @@ reference restricted to that slice:
   * C4 (configs[3]): flash_attn_varlen_qkvpacked_func, bf16, total 65536 tokens, cu_seqlens from
     the SURVEY 8(d) recipe (bench.c4_seqlens), h = 32, d = 128, causal; EVERY sequence and head:
     out, dqkv, and the per-batch-padded LSE (B, 32, max_seqlen) against the fp64 logsumexp.
+  * C3 (configs[2], the headline): flash_attn_func, bf16, 4 x 8192 x 16 x 128, causal; three whole
+    (batch, head) slices at full length (first, last, one in the middle): out, dq, dk, dv under the
+    2x rule, LSE against the fp64 logsumexp; every output finite everywhere.
+  * C2 (configs[1]): the same at 4 x 2048 x 16 x 64 (forward-only in the bench; the backward is
+    checked too since it is the same API call).
   * C5 (configs[4]): flash_attn_func, fp16, b = 8 per GPU, s = 32768, h = 32, hk = 8, causal; two
     (batch, kv-head) groups: out / dq per query head, dk / dv summed over the group, LSE; every
     output finite everywhere.
@@ -106,3 +111,35 @@ def test_c5_gqa_long_context_full_size():
             del ref, gr, pt, gp
         _check(f"(b {bi}, kv {kvh}) dk", dk[bi:bi + 1, :, kvh:kvh + 1], dk_ref, dk_pt)
         _check(f"(b {bi}, kv {kvh}) dv", dv[bi:bi + 1, :, kvh:kvh + 1], dv_ref, dv_pt)
+
+
+@pytest.mark.parametrize("cfg", [
+    dict(name="c3", b=4, s=8192, h=16, d=128, slices=((0, 0), (1, 7), (3, 15))),
+    dict(name="c2", b=4, s=2048, h=16, d=64, slices=((0, 0), (2, 9), (3, 15))),
+], ids=lambda c: c["name"])
+def test_headline_full_size_2x_rule(cfg):
+    """C3 / C2 at full size: whole (batch, head) slices under the reference's 2x rule
+    (tests/test_flash_attn.py:517-639 applies it to whole tensors; attention is independent per
+    (batch, head), so a slice's reference is the full-call reference restricted to it)."""
+    from flash_attn import flash_attn_func
+
+    torch.manual_seed(0)
+    b, s, h, d = cfg["b"], cfg["s"], cfg["h"], cfg["d"]
+    dt = torch.bfloat16
+    q, k, v = (torch.randn(b, s, h, d, device=DEV, dtype=dt, requires_grad=True) for _ in range(3))
+    out, lse, _ = flash_attn_func(q, k, v, causal=True, return_attn_probs=True)
+    dout = torch.randn_like(out)
+    dq, dk, dv = torch.autograd.grad(out, (q, k, v), dout)
+    for t in (out, lse, dq, dk, dv):
+        assert torch.isfinite(t).all()
+    for bi, hi in cfg["slices"]:
+        qq, kk, vv = (x.detach()[bi:bi + 1, :, hi:hi + 1] for x in (q, k, v))
+        g = dout[bi:bi + 1, :, hi:hi + 1]
+        ref, gr = _ref_grads(qq, kk, vv, g, True, True, False)
+        pt, gp = _ref_grads(qq, kk, vv, g, True, False, True)
+        _check(f"(b {bi}, h {hi}) out", out[bi:bi + 1, :, hi:hi + 1], ref, pt)
+        for j, (name, x) in enumerate((("dq", dq), ("dk", dk), ("dv", dv))):
+            _check(f"(b {bi}, h {hi}) {name}", x[bi:bi + 1, :, hi:hi + 1], gr[j], gp[j])
+        lse_ref = attention_lse_ref(qq, kk, causal=True)[0, 0]
+        torch.testing.assert_close(lse[bi, hi], lse_ref, atol=2e-3, rtol=1e-4)
+        del ref, gr, pt, gp
