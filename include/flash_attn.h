@@ -420,7 +420,10 @@ void flash_attn_timing_read(int kernel_id, double * total_ms, long * count);
 /* Test / A-B switches (no reference counterpart).  Knob ids: 0 never split K/V in the forward
  * (FLASH_ATTN_MI355X_NO_SPLITKV), 1 head-fastest work order (FLASH_ATTN_MI355X_NO_XCD_GROUP),
  * 2 XCD head-grouping threshold in MiB of streamed K/V (FLASH_ATTN_MI355X_XCD_GROUP_MIN_MIB,
- * default 256).  Each is read from its environment variable once, at first use. */
+ * default 256), 3 / 4 assembly dK/dV / dQ kernels (FLASH_ATTN_MI355X_BWD_ASM / _DQ_ASM, default 1),
+ * 5 persistent assembly forward, one workgroup per CU walking the item list
+ * (FLASH_ATTN_MI355X_FWD_PERSIST, default 1; 0 = one workgroup per item).  Each is read from its
+ * environment variable once, at first use. */
 void flash_attn_set_knob(int id, int value);
 int flash_attn_get_knob(int id);
 /* 0 routes every forward to the HIP kernel, 1 (default) lets head dim 128 take the assembly

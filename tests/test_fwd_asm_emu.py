@@ -43,6 +43,22 @@ def test_asm_forward_in_emulator(asm_text, b, sq, sk, h, hk, causal, bf16, big):
 
 
 @pytest.mark.timeout(600)
+@pytest.mark.parametrize("b,sq,sk,h,hk,causal,bf16,grid", [
+    (1, 600, 600, 2, 1, True, True, 1),      # one workgroup walks all 6 items: warm starts (>= 4 tiles)
+    (1, 600, 600, 2, 1, True, True, 4),      # snake rounds: items 0-3, then 7, 6 / 5, 4 reversed
+    (2, 130, 77, 3, 1, False, True, 2),      # 2-tile items: every successor starts cold
+    (1, 300, 700, 2, 1, True, False, 1),     # fp16, sq < sk, mixed warm / cold
+])
+def test_asm_forward_persistent_loop(asm_text, b, sq, sk, h, hk, causal, bf16, grid):
+    """the persistent item loop (fa_fwd_asm.cpp, knob 5): fewer workgroups than items; each item's
+    K/V tiles run on from its predecessor's DMA stream (switch block) when it has >= 4 tiles"""
+    eo, el, o, o_ref, lse, lse_ref = emu_fwd.run(b, sq, sk, h, hk, causal, bf16, seed=1, text=asm_text,
+                                                  verbose=False, grid=grid)
+    assert eo <= (1.6e-2 if bf16 else 2e-3), eo
+    assert el <= 1e-5, el
+
+
+@pytest.mark.timeout(600)
 def test_asm_forward_refit_at_the_diagonal(asm_text):
     """one key per row far above the rest, right at the causal diagonal: refits fire in masked
     steps, for q-block a at the end of a step (after every PV MFMA) and q-block b before its PV"""
@@ -66,7 +82,8 @@ def test_asm_forward_refit_at_the_diagonal(asm_text):
     kw = dict(q=aq, k=ak, v=av, o=ao, lse=alse, sched=asch, cuq=0, cuk=0, rng=0, seed=0, off=0,
               q_batch=s * d * 2, k_batch=s * d * 2, v_batch=s * d * 2, o_batch=s * d * 2, q_row=d * 2, kv_row=d * 2,
               o_row=d * 2, q_head=d * 2, k_head=d * 2, v_head=d * 2, o_head=d * 2, sq=s, sk=s, lse_pitch=s, h=1,
-              c=float(np.float32(d ** -0.5 * 1.4426950408889634)), flags=0)
+              c=float(np.float32(d ** -0.5 * 1.4426950408889634)), flags=0,
+              n_items=len(tab), grid=len(tab))
     akarg = heap.put(np.frombuffer(emu_fwd.pack_args(**kw), dtype=np.uint8))
     emu = Emu(asm_text, "fa_fwd_asm_d128_f16_causal", heap)
     emu.trace_labels = ["refit"]

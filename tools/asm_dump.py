@@ -73,7 +73,8 @@ def cpu(point):
     kw = dict(q=aq, k=ak, v=av, o=ao, lse=alse, sched=asch, cuq=0, cuk=0, rng=arng, seed=adump, off=0,
               q_batch=SQ * H * D * 2, k_batch=SK * HK * D * 2, v_batch=SK * HK * D * 2, o_batch=SQ * H * D * 2,
               q_row=H * D * 2, kv_row=HK * D * 2, o_row=H * D * 2, q_head=D * 2, k_head=D * 2, v_head=D * 2,
-              o_head=D * 2, sq=SQ, sk=SK, lse_pitch=SQ, h=H, c=float(np.float32(D ** -0.5 * 1.4426950408889634)), flags=0)
+              o_head=D * 2, sq=SQ, sk=SK, lse_pitch=SQ, h=H, c=float(np.float32(D ** -0.5 * 1.4426950408889634)), flags=0,
+              n_items=1, grid=1)
     akarg = heap.put(np.frombuffer(pack_args(**kw), dtype=np.uint8))
     emu = Emu(text, f"fa_fwd_asm_d128_bf16_{'causal' if CAUSAL else 'full'}", heap)
     emu.run_wg(0, akarg)

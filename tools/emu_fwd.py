@@ -43,9 +43,9 @@ def pack_args(**kw):
     assert len(head) == 120
     tail = struct.pack("<11i", kw["q_row"], kw["kv_row"], kw["o_row"], kw["q_head"], kw["k_head"], kw["v_head"],
                        kw["o_head"], kw["sq"], kw["sk"], kw["lse_pitch"], kw["h"])
-    tail += struct.pack("<fii", kw["c"], kw["flags"], 0)
+    tail += struct.pack("<fiiii", kw["c"], kw["flags"], kw["n_items"], kw["grid"], 0)
     out = head + tail
-    assert len(out) == 176, len(out)
+    assert len(out) == 184, len(out)
     return out
 
 
@@ -71,7 +71,9 @@ def reference(q, k, v, causal, scale, seqs_q=None, seqs_k=None):
     return o, lse
 
 
-def run(b=1, sq=300, sk=300, h=2, hk=1, causal=True, bf16=True, seed=0, big=None, text=None, verbose=True):
+def run(b=1, sq=300, sk=300, h=2, hk=1, causal=True, bf16=True, seed=0, big=None, text=None, verbose=True,
+        grid=None):
+    """grid: workgroups of the persistent item loop (default: one per item)"""
     rng = np.random.default_rng(seed)
     q = rng.standard_normal((b, sq, h, D)).astype(np.float32)
     k = rng.standard_normal((b, sk, hk, D)).astype(np.float32)
@@ -94,12 +96,13 @@ def run(b=1, sq=300, sk=300, h=2, hk=1, causal=True, bf16=True, seed=0, big=None
     kw = dict(q=aq, k=ak, v=av, o=ao, lse=alse, sched=asch, cuq=0, cuk=0, rng=0, seed=0, off=0,
               q_batch=sq * h * D * 2, k_batch=sk * hk * D * 2, v_batch=sk * hk * D * 2, o_batch=sq * h * D * 2,
               q_row=h * D * 2, kv_row=hk * D * 2, o_row=h * D * 2, q_head=D * 2, k_head=D * 2, v_head=D * 2,
-              o_head=D * 2, sq=sq, sk=sk, lse_pitch=sq, h=h, c=float(np.float32(scale * 1.4426950408889634)), flags=0)
+              o_head=D * 2, sq=sq, sk=sk, lse_pitch=sq, h=h, c=float(np.float32(scale * 1.4426950408889634)), flags=0,
+              n_items=len(tab), grid=grid or len(tab))
     akarg = heap.put(np.frombuffer(pack_args(**kw), dtype=np.uint8))
     text = text or asm_text()
     name = f"fa_fwd_asm_d128_{'bf16' if bf16 else 'f16'}_{'causal' if causal else 'full'}"
     emu = Emu(text, name, heap)
-    for L in range(len(tab)):
+    for L in range(grid or len(tab)):
         emu.run_wg(L, akarg)
     o = dec(heap.get(ao, b * sq * h * D * 2).view(np.uint16)).reshape(b, sq, h, D).astype(np.float64)
     lse = heap.get(alse, b * h * sq * 4).view(np.float32).reshape(b, h, sq).astype(np.float64)
@@ -123,5 +126,6 @@ if __name__ == "__main__":
     ap.add_argument("--fp16", action="store_true")
     ap.add_argument("--big", type=int, default=None)
     ap.add_argument("--seed", type=int, default=0)
+    ap.add_argument("--grid", type=int, default=None)
     a = ap.parse_args()
-    run(a.b, a.sq, a.sk, a.h, a.hk, not a.full, not a.fp16, a.seed, a.big)
+    run(a.b, a.sq, a.sk, a.h, a.hk, not a.full, not a.fp16, a.seed, a.big, grid=a.grid)

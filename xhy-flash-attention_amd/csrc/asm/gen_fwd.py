@@ -93,11 +93,14 @@ V_QOFF = (184, 185)                                      # Q / O row offsets per
 V_LSEOFF = (186, 187)
 V_LANE = 188
 V_OOFF = (189, 190)
-NVGPR = 192
+V_ROW = (192, 193)                                       # row of the lane in the block, per q-block
+V_HH4 = 194                                              # 4 * (lane >> 5)
+NVGPR = 195
 
 # ---- SGPRs ----
 S_KD, S_VD, S_QD, S_OD, S_LD = 4, 8, 12, 16, 20          # buffer descriptors
-S_C = 24
+S_WARM = 3        # 1: the next item's K/V tiles 0..2 and its Q are in flight (set by the switch block)
+S_ROUND = 24      # round r of the persistent item loop (item position: r G + (r odd ? G-1-w : w))
 S_N = 25          # step n
 S_N0 = 26         # 64 n
 S_NF2 = 27        # nfast - 2
@@ -110,11 +113,22 @@ S_DT = 33         # index of the next DMA tile
 S_NBLK = 34
 S_WAVE = 35
 S_TMP = 36        # 36..39 temps
-S_KA = 40         # kernarg block 40..83
-S_RNGD = 92       # rng_state store descriptor (92..95), written once
-NSGPR = 100
+S_KA = 40         # kernarg block 40..84 (84: grid)
+S_C = S_KA + 41   # scale * log2(e) (kernarg)
+S_NITEMS = S_KA + 43
+S_GRID = S_KA + 44
+S_RNGD = 92       # rng_state store descriptor (92..95), written once, before S_KD2 is
+# persistent item loop: the NEXT item's descriptors (its K/V tiles are DMA'd into the ring while the
+# current item finishes, its Q is loaded in the current item's last step)
+S_QD2 = 56        # over the rng / seed / offset kernargs (dead after the rng store)
+S_DLIM = 60       # tiles of the item the DMA stream currently reads (S_DT counts the issued ones)
+S_NXN = 61        # tiles of the next item (0: none / empty)
+S_KD2, S_VD2 = 92, 96
+S_SWT = 100       # switch-block temp
+S_M0R = 101       # 256 m_block of the item being set up (prologue temp)
+NSGPR = 102
 
-KARG_SIZE = 176
+KARG_SIZE = 184
 
 # dev A/B switches, read when the .s is generated (tools/asm_variant.sh)
 OPT_NOZERO = os.environ.get("FA_GEN_NOZERO") == "1"          # never zero K/V record counts
@@ -309,13 +323,9 @@ class K:
                 Inst(f"s_sub_u32 s{t}, s{S_DOFF}, {NSLOT * TILE}", SALU, rd=sr(S_DOFF), wr=sr(t) + [("scc", 0)], key=-30),
                 Inst(f"s_cmp_ge_u32 s{S_DOFF}, {NSLOT * TILE}", SALU, rd=sr(S_DOFF), wr=[("scc", 0)], key=-30),
                 Inst(f"s_cselect_b32 s{S_DOFF}, s{t}, s{S_DOFF}", SALU, rd=sr(t) + sr(S_DOFF) + [("scc", 0)], wr=sr(S_DOFF), key=-30),
-                Inst(f"s_add_u32 s{S_DT}, s{S_DT}, 1", SALU, rd=sr(S_DT), wr=sr(S_DT) + [("scc", 0)], key=-30),
             ]
-            if not OPT_NOZERO:
-                fy += [nop(15) for _ in range(OPT_ZERO_NOP)] + [
-                    Inst(f"s_cmp_lt_u32 s{S_DT}, s{S_NBLK}", SALU, rd=sr(S_DT) + sr(S_NBLK), wr=[("scc", 0)], key=-30),
-                    Inst(f"s_cselect_b32 s{S_KD + 2}, s{S_KD + 2}, 0", SALU, rd=sr(S_KD + 2) + [("scc", 0)], wr=sr(S_KD + 2), key=-30),
-                    Inst(f"s_cselect_b32 s{S_VD + 2}, s{S_VD + 2}, 0", SALU, rd=sr(S_VD + 2) + [("scc", 0)], wr=sr(S_VD + 2), key=-30)]
+            # the DMA stream passed the end of its item: switch to the next item (out of line, once)
+            fy += self.dma_count_ops(self.lab(f"{tag}_sw"), key=-30)
             # K read base of tile n+2 and prefetch of its first three fragments (next phase X)
             fy += [
                 Inst(f"s_add_u32 s{S_KOFF}, s{S_KOFF}, {TILE}", SALU, rd=sr(S_KOFF), wr=sr(S_KOFF) + [("scc", 0)], key=-20, earliest=18),
@@ -335,6 +345,13 @@ class K:
             for op in ga:
                 op.eg = 31
             fy += ga
+        if last:
+            # Q of the next item (persistent loop): the Q registers are idle from here on (no QK MFMA
+            # in the last step; the refit of q-block b, which reads them, returns before MFMA 4)
+            for j in range(2):
+                for ks in range(KS):
+                    fy.append(Inst(f"buffer_load_dwordx4 {rtxt('a', Q_(j, ks), 4)}, v{V_QOFF[j]}, s[{S_QD2}:{S_QD2 + 3}], 0 offen offset:{32 * ks}",
+                                   VLOAD, rd=vr(V_QOFF[j]) + sr(S_QD2, 4), wr=ar(Q_(j, ks), 4), key=900 + 8 * j + ks, earliest=8))
         # V read slot of the next tile
         fy += [Inst(f"s_add_u32 s{S_VOFF}, s{S_VOFF}, {TILE}", SALU, rd=sr(S_VOFF), wr=sr(S_VOFF) + [("scc", 0)], key=800, earliest=28),
                Inst(f"s_sub_u32 s{t + 2}, s{S_VOFF}, {NSLOT * TILE}", SALU, rd=sr(S_VOFF), wr=sr(t + 2) + [("scc", 0)], key=801),
@@ -349,6 +366,61 @@ class K:
                      Inst("s_waitcnt vmcnt(8) lgkmcnt(0)", WAIT),
                      Inst("s_barrier", BARRIER)]
         return body, refits
+
+    # ------------------------------------------------------------------ DMA stream across items
+    def dma_count_ops(self, lab, key=0):
+        """after one tile's K and V pieces are issued: count it; when the stream reaches the end of
+        its item, branch to the (out-of-line) switch block.  The branch is one instruction with its
+        return label, and it carries the registers the block touches so that the scheduler keeps
+        every V_VOFF update / DMA of this tile before it."""
+        self.switches.append(self.switch_block(lab))
+        touched = vr(V_VOFF, 4) + sr(S_KD, 4) + sr(S_VD, 4) + sr(S_DT) + sr(S_DLIM) + sr(S_WARM)
+        return [Inst(f"s_add_u32 s{S_DT}, s{S_DT}, 1", SALU, rd=sr(S_DT), wr=sr(S_DT) + [("scc", 0)], key=key),
+                Inst(f"s_cmp_eq_u32 s{S_DT}, s{S_DLIM}", SALU, rd=sr(S_DT) + sr(S_DLIM), wr=[("scc", 0)], key=key),
+                Inst(f"s_cbranch_scc1 {lab}\n{lab}_back:", BRANCH, rd=[("scc", 0)] + touched, wr=touched, key=key)]
+
+    def switch_block(self, lab):
+        """The DMA stream issued the last tile of its item.  If the next item has >= 4 tiles, the
+        following DMAs read it: K/V descriptors <- the next item's, per-lane offsets back to tile 0,
+        S_DT = 0, S_DLIM = its tile count, S_WARM = 1 (its tiles 0..2 get issued before the current
+        item ends, so it starts warm).  Otherwise the records are zeroed (the DMAs past the end
+        zero-fill their slots) and the next item starts cold."""
+        I = Inst
+        lz = lab + "_z"
+        ins = [label(lab),
+               I(f"s_cmp_lt_u32 s{S_NXN}, 4", SALU), I(f"s_cbranch_scc1 {lz}", BRANCH)]
+        ins += [I(f"s_mov_b32 s{S_KD + i}, s{S_KD2 + i}", SALU) for i in range(4)]
+        ins += [I(f"s_mov_b32 s{S_VD + i}, s{S_VD2 + i}", SALU) for i in range(4)]
+        ins += [I(f"s_mul_i32 s{S_SWT}, s{S_DT}, s{S_TB}", SALU)]
+        ins += [I(f"v_subrev_u32_e32 v{V_VOFF + jj}, s{S_SWT}, v{V_VOFF + jj}", VALU) for jj in range(4)]
+        ins += [I(f"s_mov_b32 s{S_DT}, 0", SALU), I(f"s_mov_b32 s{S_DLIM}, s{S_NXN}", SALU),
+                I(f"s_mov_b32 s{S_WARM}, 1", SALU), nop(4), I(f"s_branch {lab}_back", BRANCH),
+                label(lz),
+                I(f"s_mov_b32 s{S_KD + 2}, 0", SALU), I(f"s_mov_b32 s{S_VD + 2}, 0", SALU), nop(4),
+                I(f"s_branch {lab}_back", BRANCH)]
+        return ins
+
+    def dma_tile_ops(self, tag):
+        """one whole tile (K then V pieces) into the slot at S_DOFF, then the stream bookkeeping
+        (prologue use: not scheduled)"""
+        I = Inst
+        ins = []
+        for jj in range(4):
+            ins += [I(f"s_add_u32 m0, s{S_DOFF}, {jj * 4096}", SALU, rd=sr(S_DOFF), wr=[("m0", 0)]),
+                    I(f"buffer_load_dwordx4 v{V_VOFF + jj}, s[{S_KD}:{S_KD + 3}], 0 offen lds", DMA,
+                      rd=vr(V_VOFF + jj) + sr(S_KD, 4) + [("m0", 0)])]
+        for jj in range(4):
+            ins += [I(f"s_add_u32 m0, s{S_DOFF}, {VBASE + jj * 4096}", SALU, rd=sr(S_DOFF), wr=[("m0", 0)]),
+                    I(f"buffer_load_dwordx4 v{V_VOFF + jj}, s[{S_VD}:{S_VD + 3}], 0 offen lds", DMA,
+                      rd=vr(V_VOFF + jj) + sr(S_VD, 4) + [("m0", 0)])]
+        for jj in range(4):
+            ins.append(I(f"v_add_u32_e32 v{V_VOFF + jj}, s{S_TB}, v{V_VOFF + jj}", VALU, rd=sr(S_TB) + vr(V_VOFF + jj), wr=vr(V_VOFF + jj)))
+        ins += [I(f"s_add_u32 s{S_DOFF}, s{S_DOFF}, {TILE}", SALU, rd=sr(S_DOFF), wr=sr(S_DOFF)),
+                I(f"s_sub_u32 s{S_SWT}, s{S_DOFF}, {NSLOT * TILE}", SALU, rd=sr(S_DOFF), wr=sr(S_SWT)),
+                I(f"s_cmp_ge_u32 s{S_DOFF}, {NSLOT * TILE}", SALU, rd=sr(S_DOFF), wr=[("scc", 0)]),
+                I(f"s_cselect_b32 s{S_DOFF}, s{S_SWT}, s{S_DOFF}", SALU, rd=sr(S_SWT) + sr(S_DOFF), wr=sr(S_DOFF))]
+        ins += self.dma_count_ops(self.lab(f"{tag}_sw"))
+        return ins
 
     # ------------------------------------------------------------------ refit (rare, out of line)
     def refit(self, j, sreg, preg, lab, tile_add, phase):
@@ -467,37 +539,51 @@ class K:
                 Inst(f"v_permlane32_swap_b32_e32 v{x}, v{tmp}", PERM, rd=vr(x) + vr(tmp), wr=vr(x) + vr(tmp)),
                 Inst(f"v_add_f32_e32 v{x}, v{x}, v{tmp}", VALU, rd=vr(x) + vr(tmp), wr=vr(x))]
 
-    # ------------------------------------------------------------------ prologue / epilogue
-    def prologue(self, l_epi, l_entry_last, l_entry_fast, l_entry_masked):
+    # ------------------------------------------------------------------ prologue (persistent item loop)
+    # kernargs: 40..55 pointers (q k v o lse sched cuq cuk); 56..63 rng seed offset q_batch;
+    # 64..79 k_batch v_batch o_batch q_row kv_row o_row q_head k_head v_head o_head sq sk lse_pitch;
+    # 80..84 h c flags n_items grid
+    def kargs(self):
+        ka = S_KA
+        return dict(Pq=ka, Pk=ka + 2, Pv=ka + 4, Po=ka + 6, Pl=ka + 8, Psch=ka + 10, Pcq=ka + 12, Pck=ka + 14,
+                    Prng=ka + 16, Pseed=ka + 18, Poff=ka + 20, Bq=ka + 22, Bk=ka + 24, Bv=ka + 26, Bo=ka + 28,
+                    Rq=ka + 30, Rkv=ka + 31, Ro=ka + 32, Hq=ka + 33, Hk=ka + 34, Hv=ka + 35, Ho=ka + 36,
+                    SQ=ka + 37, SK=ka + 38, LP=ka + 39, NH=ka + 40, CC=ka + 41, FL=ka + 42)
+
+    def entry(self):
+        """once per workgroup: kernargs, lane constants, rng_state; falls into the cold item start"""
         I = Inst
         ins = []
         ka = S_KA
-        # kernargs: 40..55 pointers (q k v o lse sched cuq cuk); 56..63 rng seed offset q_batch;
-        # 64..79 k_batch v_batch o_batch q_row kv_row o_row q_head k_head v_head o_head sq sk lse_pitch;
-        # 80..83 h c flags pad
+        A = self.kargs()
         ins += [I(f"s_load_dwordx16 s[{ka}:{ka + 15}], s[0:1], 0x0", SMEM, rd=sr(0, 2), wr=sr(ka, 16)),
                 I(f"s_load_dwordx8 s[{ka + 16}:{ka + 23}], s[0:1], 0x40", SMEM, rd=sr(0, 2), wr=sr(ka + 16, 8)),
                 I(f"s_load_dwordx16 s[{ka + 24}:{ka + 39}], s[0:1], 0x60", SMEM, rd=sr(0, 2), wr=sr(ka + 24, 16)),
                 I(f"s_load_dwordx4 s[{ka + 40}:{ka + 43}], s[0:1], 0xa0", SMEM, rd=sr(0, 2), wr=sr(ka + 40, 4)),
+                I(f"s_load_dword s{S_GRID}, s[0:1], 0xb0", SMEM, rd=sr(0, 2), wr=sr(S_GRID)),
                 I("s_waitcnt lgkmcnt(0)", WAIT)]
-        Pq, Pk, Pv, Po, Pl, Psch, Pcq, Pck = (ka + 2 * i for i in range(8))
-        Prng, Pseed, Poff, Bq = ka + 16, ka + 18, ka + 20, ka + 22
-        Bk, Bv, Bo = ka + 24, ka + 26, ka + 28
-        Rq, Rkv, Ro, Hq, Hk, Hv, Ho, SQ, SK, LP = (ka + 30 + i for i in range(10))
-        NH, CC, FL = ka + 40, ka + 41, ka + 42
-        T0, T1, T2, T3 = S_TMP, S_TMP + 1, S_TMP + 2, S_TMP + 3
+        T0 = S_TMP
+        # varlen work list built on the device (flags bit 1): the item count is its first dword and
+        # the entries start 8 bytes in
+        l_cnt, l_cnt_done = self.lab("cnt"), self.lab("cntdone")
+        Psch = A["Psch"]
+        ins += [I(f"s_bitcmp1_b32 s{A['FL']}, 1", SALU), I(f"s_cbranch_scc1 {l_cnt}", BRANCH),
+                I(f"s_branch {l_cnt_done}", BRANCH), label(l_cnt),
+                I(f"s_load_dword s{S_NITEMS}, s[{Psch}:{Psch + 1}], 0x0", SMEM),
+                I(f"s_add_u32 s{Psch}, s{Psch}, 8", SALU), I(f"s_addc_u32 s{Psch + 1}, s{Psch + 1}, 0", SALU),
+                I("s_waitcnt lgkmcnt(0)", WAIT), label(l_cnt_done)]
         # wave index, lane values
         ins += [I("v_lshrrev_b32_e32 v1, 6, v0", VALU, rd=vr(0), wr=vr(1)),
                 I(f"v_readfirstlane_b32 s{S_WAVE}, v1", RFL, rd=vr(1), wr=sr(S_WAVE)),
                 I(f"v_and_b32_e32 v{V_LANE}, 63, v0", VALU, rd=vr(0), wr=vr(V_LANE))]
         # rng_state (block 0, wave 0): {seed, offset}; lanes >= 1 fall outside the 16-byte record
         l_norng = self.lab("norng")
+        Prng, Pseed, Poff = A["Prng"], A["Pseed"], A["Poff"]
         ins += [I(f"s_or_b32 s{T0}, s2, s{S_WAVE}", SALU, rd=sr(2) + sr(S_WAVE), wr=sr(T0)),
                 I(f"s_cmp_lg_u32 s{T0}, 0", SALU, rd=sr(T0), wr=[("scc", 0)]),
                 I(f"s_cbranch_scc1 {l_norng}", BRANCH),
                 I(f"s_cmp_eq_u64 s[{Prng}:{Prng + 1}], 0", SALU, rd=sr(Prng, 2), wr=[("scc", 0)]),
                 I(f"s_cbranch_scc1 {l_norng}", BRANCH),
-                # descriptor in SGPRs that nothing rewrites while the store may still read them
                 I(f"s_mov_b32 s{S_RNGD}, s{Prng}", SALU, rd=sr(Prng), wr=sr(S_RNGD)),
                 I(f"s_and_b32 s{S_RNGD + 1}, s{Prng + 1}, 0xffff", SALU, rd=sr(Prng + 1), wr=sr(S_RNGD + 1)),
                 I(f"s_mov_b32 s{S_RNGD + 2}, 16", SALU, wr=sr(S_RNGD + 2)),
@@ -509,153 +595,19 @@ class K:
                 I(f"v_mov_b32_e32 v7, s{Poff + 1}", VALU, rd=sr(Poff + 1), wr=vr(7)),
                 I(f"buffer_store_dwordx4 v[4:7], v2, s[{S_RNGD}:{S_RNGD + 3}], 0 offen", VSTORE, rd=vr(4, 4) + vr(2) + sr(S_RNGD, 4)),
                 label(l_norng)]
-        # schedule entry: (bidb | head << 16, kvh | m_block << 16)
-        ins += [I(f"s_lshl_b32 s{T0}, s2, 3", SALU, rd=sr(2), wr=sr(T0)),
-                I(f"s_load_dwordx2 s[{T0}:{T1}], s[{Psch}:{Psch + 1}], s{T0}", SMEM, rd=sr(Psch, 2) + sr(T0), wr=sr(T0, 2)),
-                I("s_waitcnt lgkmcnt(0)", WAIT)]
-        # scalars kept: bidb (T2), head (T3), kvh (S_N), m_block (S_N0) -- temporarily
-        BIDB, HEAD, KVH, MB = T2, T3, S_N, S_N0
-        ins += [I(f"s_and_b32 s{BIDB}, s{T0}, 0xffff", SALU, rd=sr(T0), wr=sr(BIDB)),
-                I(f"s_lshr_b32 s{HEAD}, s{T0}, 16", SALU, rd=sr(T0), wr=sr(HEAD)),
-                I(f"s_and_b32 s{KVH}, s{T1}, 0xffff", SALU, rd=sr(T1), wr=sr(KVH)),
-                I(f"s_lshr_b32 s{MB}, s{T1}, 16", SALU, rd=sr(T1), wr=sr(MB))]
-        # varlen geometry (BlockInfo, block_info.h:14-31): 64-bit byte offsets (lo, hi) of row 0 of
-        # this sequence in Q, O and K/V; seqlens in SQ / SK (overwritten in place)
-        QOFF, OOFF, KOFF = (84, 85), (86, 87), (88, 89)
-        l_q_fixed, l_q_done = self.lab("qfixed"), self.lab("qdone")
-        l_o_fixed, l_o_done = self.lab("ofixed"), self.lab("odone")
-        l_k_fixed, l_k_done = self.lab("kfixed"), self.lab("kdone")
-
-        def mul64(dst, a32, b32):
-            return [I(f"s_mul_i32 s{dst[0]}, s{a32}, s{b32}", SALU, rd=sr(a32) + sr(b32), wr=sr(dst[0])),
-                    I(f"s_mul_hi_u32 s{dst[1]}, s{a32}, s{b32}", SALU, rd=sr(a32) + sr(b32), wr=sr(dst[1]))]
-
-        def mul64_i64(dst, a32, b64):   # a32 * (b64 lo, hi) -> dst (lo, hi)
-            return [I(f"s_mul_i32 s{dst[0]}, s{a32}, s{b64}", SALU, rd=sr(a32) + sr(b64), wr=sr(dst[0])),
-                    I(f"s_mul_hi_u32 s{dst[1]}, s{a32}, s{b64}", SALU, rd=sr(a32) + sr(b64), wr=sr(dst[1])),
-                    I(f"s_mul_i32 s{T0}, s{a32}, s{b64 + 1}", SALU, rd=sr(a32) + sr(b64 + 1), wr=sr(T0)),
-                    I(f"s_add_u32 s{dst[1]}, s{dst[1]}, s{T0}", SALU, rd=sr(dst[1]) + sr(T0), wr=sr(dst[1]))]
-
-        for cu, bstride, rstride, off, seq, lf, ld in ((Pcq, Bq, Rq, QOFF, SQ, l_q_fixed, l_q_done),
-                                                       (Pcq, Bo, Ro, OOFF, None, l_o_fixed, l_o_done),
-                                                       (Pck, Bk, Rkv, KOFF, SK, l_k_fixed, l_k_done)):
-            ins += [I(f"s_cmp_eq_u64 s[{cu}:{cu + 1}], 0", SALU, rd=sr(cu, 2), wr=[("scc", 0)]),
-                    I(f"s_cbranch_scc1 {lf}", BRANCH),
-                    I(f"s_lshl_b32 s{T1}, s{BIDB}, 2", SALU, rd=sr(BIDB), wr=sr(T1)),
-                    I(f"s_load_dwordx2 s[{off[0]}:{off[1]}], s[{cu}:{cu + 1}], s{T1}", SMEM, rd=sr(cu, 2) + sr(T1), wr=sr(off[0], 2)),
-                    I("s_waitcnt lgkmcnt(0)", WAIT)]
-            if seq is not None:
-                ins += [I(f"s_sub_u32 s{seq}, s{off[1]}, s{off[0]}", SALU, rd=sr(off[0], 2), wr=sr(seq))]
-            ins += [I(f"s_bitcmp1_b32 s{FL}, 0", SALU, rd=sr(FL), wr=[("scc", 0)]),
-                    I(f"s_cbranch_scc1 {lf}", BRANCH),
-                    I(f"s_mov_b32 s{T1}, s{off[0]}", SALU, rd=sr(off[0]), wr=sr(T1))]
-            ins += mul64(off, T1, rstride)
-            ins += [I(f"s_branch {ld}", BRANCH), label(lf)]
-            ins += mul64_i64(off, BIDB, bstride)
-            ins += [label(ld)]
-        # m0 = 256 m_block; exit when m0 >= sq
-        M0R = S_DT
-        ins += [I(f"s_lshl_b32 s{M0R}, s{MB}, 8", SALU, rd=sr(MB), wr=sr(M0R)),
-                I(f"s_cmp_ge_i32 s{M0R}, s{SQ}", SALU, rd=sr(M0R) + sr(SQ), wr=[("scc", 0)]),
-                I(f"s_cbranch_scc1 {self.lab_end}", BRANCH)]
-        # rows of this workgroup: nrow = min(sq - m0, 256)
-        NROW = S_NBLK
-        ins += [I(f"s_sub_u32 s{NROW}, s{SQ}, s{M0R}", SALU, rd=sr(SQ) + sr(M0R), wr=sr(NROW)),
-                I(f"s_min_u32 s{NROW}, s{NROW}, {BM}", SALU, rd=sr(NROW), wr=sr(NROW))]
-
-        def addr(dst4, ptr, off64, head, hstride, rows=None, rstride=None, nrec=None):
-            """descriptor at ptr + off64 + head * hstride (+ rows * rstride)"""
-            o = []
-            o += [I(f"s_mul_i32 s{T0}, s{head}, s{hstride}", SALU, rd=sr(head) + sr(hstride), wr=sr(T0)),
-                  I(f"s_mul_hi_u32 s{T1}, s{head}, s{hstride}", SALU, rd=sr(head) + sr(hstride), wr=sr(T1)),
-                  I(f"s_add_u32 s{dst4}, s{ptr}, s{T0}", SALU, rd=sr(ptr) + sr(T0), wr=sr(dst4) + [("scc", 0)]),
-                  I(f"s_addc_u32 s{dst4 + 1}, s{ptr + 1}, s{T1}", SALU, rd=sr(ptr + 1) + sr(T1) + [("scc", 0)], wr=sr(dst4 + 1) + [("scc", 0)]),
-                  I(f"s_add_u32 s{dst4}, s{dst4}, s{off64[0]}", SALU, rd=sr(dst4) + sr(off64[0]), wr=sr(dst4) + [("scc", 0)]),
-                  I(f"s_addc_u32 s{dst4 + 1}, s{dst4 + 1}, s{off64[1]}", SALU, rd=sr(dst4 + 1) + sr(off64[1]) + [("scc", 0)], wr=sr(dst4 + 1))]
-            if rows is not None:
-                o += [I(f"s_mul_i32 s{T0}, s{rows}, s{rstride}", SALU, rd=sr(rows) + sr(rstride), wr=sr(T0)),
-                      I(f"s_mul_hi_u32 s{T1}, s{rows}, s{rstride}", SALU, rd=sr(rows) + sr(rstride), wr=sr(T1)),
-                      I(f"s_add_u32 s{dst4}, s{dst4}, s{T0}", SALU, rd=sr(dst4) + sr(T0), wr=sr(dst4) + [("scc", 0)]),
-                      I(f"s_addc_u32 s{dst4 + 1}, s{dst4 + 1}, s{T1}", SALU, rd=sr(dst4 + 1) + sr(T1), wr=sr(dst4 + 1))]
-            o += [I(f"s_and_b32 s{dst4 + 1}, s{dst4 + 1}, 0xffff", SALU, rd=sr(dst4 + 1), wr=sr(dst4 + 1))]
-            o += nrec
-            o += [I(f"s_mov_b32 s{dst4 + 3}, 0x20000", SALU, wr=sr(dst4 + 3))]
-            return o
-
-        # Q / O descriptors: rows [m0, m0 + nrow) of this sequence and head
-        ins += addr(S_QD, Pq, QOFF, HEAD, Hq, rows=M0R, rstride=Rq,
-                    nrec=[I(f"s_mul_i32 s{S_QD + 2}, s{NROW}, s{Rq}", SALU, rd=sr(NROW) + sr(Rq), wr=sr(S_QD + 2))])
-        ins += addr(S_OD, Po, OOFF, HEAD, Ho, rows=M0R, rstride=Ro,
-                    nrec=[I(f"s_mul_i32 s{S_OD + 2}, s{NROW}, s{Ro}", SALU, rd=sr(NROW) + sr(Ro), wr=sr(S_OD + 2))])
-        # K / V descriptors: every key of this sequence and kv head (host checks sk * kv_row < 2^31)
-        ins += addr(S_KD, Pk, KOFF, KVH, Hk,
-                    nrec=[I(f"s_mul_i32 s{S_KD + 2}, s{SK}, s{Rkv}", SALU, rd=sr(SK) + sr(Rkv), wr=sr(S_KD + 2))])
-        ins += addr(S_VD, Pv, KOFF, KVH, Hv,
-                    nrec=[I(f"s_mul_i32 s{S_VD + 2}, s{SK}, s{Rkv}", SALU, rd=sr(SK) + sr(Rkv), wr=sr(S_VD + 2))])
-        # LSE descriptor: lse + ((bidb * h + head) * lse_pitch + m0) * 4
-        # idx (64-bit, in S_LD+2 lo / S_LD+3 hi) = (bidb * h + head) * lse_pitch + m0; bytes = 4 idx
-        ins += [I(f"s_mul_i32 s{T0}, s{BIDB}, s{NH}", SALU, rd=sr(BIDB) + sr(NH), wr=sr(T0)),
-                I(f"s_add_u32 s{T0}, s{T0}, s{HEAD}", SALU, rd=sr(T0) + sr(HEAD), wr=sr(T0)),
-                I(f"s_mul_i32 s{S_LD + 2}, s{T0}, s{LP}", SALU, rd=sr(T0) + sr(LP), wr=sr(S_LD + 2)),
-                I(f"s_mul_hi_u32 s{S_LD + 3}, s{T0}, s{LP}", SALU, rd=sr(T0) + sr(LP), wr=sr(S_LD + 3)),
-                I(f"s_add_u32 s{S_LD + 2}, s{S_LD + 2}, s{M0R}", SALU, rd=sr(S_LD + 2) + sr(M0R), wr=sr(S_LD + 2) + [("scc", 0)]),
-                I(f"s_addc_u32 s{S_LD + 3}, s{S_LD + 3}, 0", SALU, rd=sr(S_LD + 3), wr=sr(S_LD + 3)),
-                I(f"s_lshl_b64 s[{S_LD + 2}:{S_LD + 3}], s[{S_LD + 2}:{S_LD + 3}], 2", SALU, rd=sr(S_LD + 2, 2), wr=sr(S_LD + 2, 2)),
-                I(f"s_add_u32 s{S_LD}, s{Pl}, s{S_LD + 2}", SALU, rd=sr(Pl) + sr(S_LD + 2), wr=sr(S_LD) + [("scc", 0)]),
-                I(f"s_addc_u32 s{S_LD + 1}, s{Pl + 1}, s{S_LD + 3}", SALU, rd=sr(Pl + 1) + sr(S_LD + 3), wr=sr(S_LD + 1)),
-                I(f"s_and_b32 s{S_LD + 1}, s{S_LD + 1}, 0xffff", SALU, rd=sr(S_LD + 1), wr=sr(S_LD + 1)),
-                I(f"s_lshl_b32 s{S_LD + 2}, s{NROW}, 2", SALU, rd=sr(NROW), wr=sr(S_LD + 2)),
-                I(f"s_mov_b32 s{S_LD + 3}, 0x20000", SALU, wr=sr(S_LD + 3))]
-        # tile counts: n_end = causal ? min(sk, m0 + 256) : sk; nblk = ceil(n_end / 64);
-        # nfast = min(nblk, (causal ? min(sk, m0 + 1) : sk) / 64)
-        if self.causal:
-            ins += [I(f"s_add_u32 s{T0}, s{M0R}, {BM}", SALU, rd=sr(M0R), wr=sr(T0)),
-                    I(f"s_min_i32 s{T0}, s{T0}, s{SK}", SALU, rd=sr(T0) + sr(SK), wr=sr(T0)),
-                    I(f"s_add_u32 s{T1}, s{M0R}, 1", SALU, rd=sr(M0R), wr=sr(T1)),
-                    I(f"s_min_i32 s{T1}, s{T1}, s{SK}", SALU, rd=sr(T1) + sr(SK), wr=sr(T1))]
-        else:
-            ins += [I(f"s_mov_b32 s{T0}, s{SK}", SALU, rd=sr(SK), wr=sr(T0)),
-                    I(f"s_mov_b32 s{T1}, s{SK}", SALU, rd=sr(SK), wr=sr(T1))]
-        ins += [I(f"s_max_i32 s{T0}, s{T0}, 0", SALU, rd=sr(T0), wr=sr(T0)),
-                I(f"s_add_u32 s{T0}, s{T0}, {BN - 1}", SALU, rd=sr(T0), wr=sr(T0)),
-                I(f"s_lshr_b32 s{S_NBLK}, s{T0}, 6", SALU, rd=sr(T0), wr=sr(S_NBLK)),
-                I(f"s_max_i32 s{T1}, s{T1}, 0", SALU, rd=sr(T1), wr=sr(T1)),
-                I(f"s_lshr_b32 s{T1}, s{T1}, 6", SALU, rd=sr(T1), wr=sr(T1)),
-                I(f"s_min_u32 s{T1}, s{T1}, s{S_NBLK}", SALU, rd=sr(T1) + sr(S_NBLK), wr=sr(T1)),
-                I(f"s_sub_i32 s{S_NF2}, s{T1}, 2", SALU, rd=sr(T1), wr=sr(S_NF2)),
-                I(f"s_sub_i32 s{S_NL1}, s{S_NBLK}, 1", SALU, rd=sr(S_NBLK), wr=sr(S_NL1)),
-                I(f"s_mov_b32 s{S_C}, s{CC}", SALU, rd=sr(CC), wr=sr(S_C)),
-                I(f"s_lshl_b32 s{S_TB}, s{Rkv}, 6", SALU, rd=sr(Rkv), wr=sr(S_TB))]
+        Rq, Rkv, Ro = A["Rq"], A["Rkv"], A["Ro"]
         # ---- per-lane values (v1 = wave, V_LANE = lane) ----
-        r, hh = "v2", "v3"
         ins += [I(f"v_and_b32_e32 v2, 31, v{V_LANE}", VALU, rd=vr(V_LANE), wr=vr(2)),
-                I(f"v_lshrrev_b32_e32 v3, 5, v{V_LANE}", VALU, rd=vr(V_LANE), wr=vr(3))]
+                I(f"v_lshrrev_b32_e32 v3, 5, v{V_LANE}", VALU, rd=vr(V_LANE), wr=vr(3)),
+                I(f"v_lshlrev_b32_e32 v{V_HH4}, 2, v3", VALU, rd=vr(3), wr=vr(V_HH4))]
         # Q / O row offsets: row (in the block) = 64 wave + 32 j + r
         for j in range(2):
-            ins += [I(f"v_lshl_add_u32 v4, v1, 6, v2", VALU, rd=vr(1) + vr(2), wr=vr(4)),
-                    I(f"v_add_u32_e32 v4, {32 * j}, v4", VALU, rd=vr(4), wr=vr(4)),
-                    I(f"v_mul_lo_u32 v{V_QOFF[j]}, v4, s{Rq}", VALU, rd=vr(4) + sr(Rq), wr=vr(V_QOFF[j])),
+            ins += [I(f"v_lshl_add_u32 v{V_ROW[j]}, v1, 6, v2", VALU, rd=vr(1) + vr(2), wr=vr(V_ROW[j])),
+                    I(f"v_add_u32_e32 v{V_ROW[j]}, {32 * j}, v{V_ROW[j]}", VALU, rd=vr(V_ROW[j]), wr=vr(V_ROW[j])),
+                    I(f"v_mul_lo_u32 v{V_QOFF[j]}, v{V_ROW[j]}, s{Rq}", VALU, rd=vr(V_ROW[j]) + sr(Rq), wr=vr(V_QOFF[j])),
                     I(f"v_lshl_add_u32 v{V_QOFF[j]}, v3, 4, v{V_QOFF[j]}", VALU, rd=vr(3) + vr(V_QOFF[j]), wr=vr(V_QOFF[j])),
-                    I(f"v_lshlrev_b32_e32 v{V_LSEOFF[j]}, 2, v4", VALU, rd=vr(4), wr=vr(V_LSEOFF[j])),
-                    # mask limit base: (causal ? min(m0 + row, sk - 1) : sk - 1) - 4 hh
-                    I(f"v_add_u32_e32 v5, s{M0R}, v4", VALU, rd=sr(M0R) + vr(4), wr=vr(5)),
-                    I(f"s_sub_i32 s{T0}, s{SK}, 1", SALU, rd=sr(SK), wr=sr(T0))]
-            if self.causal:
-                ins += [I(f"v_min_i32_e32 v5, s{T0}, v5", VALU, rd=sr(T0) + vr(5), wr=vr(5))]
-            else:
-                ins += [I(f"v_mov_b32_e32 v5, s{T0}", VALU, rd=sr(T0), wr=vr(5))]
-            ins += [I(f"v_lshlrev_b32_e32 v6, 2, v3", VALU, rd=vr(3), wr=vr(6)),
-                    I(f"v_sub_u32_e32 v{V_LB[j]}, v5, v6", VALU, rd=vr(5) + vr(6), wr=vr(V_LB[j]))]
-        # Q fragments into the accumulator file: lane holds Q[row][16 ks + 8 hh .. +7]
-        for j in range(2):
-            for ks in range(KS):
-                ins.append(I(f"buffer_load_dwordx4 {rtxt('a', Q_(j, ks), 4)}, v{V_QOFF[j]}, s[{S_QD}:{S_QD + 3}], 0 offen offset:{32 * ks}",
-                             VLOAD, rd=vr(V_QOFF[j]) + sr(S_QD, 4), wr=ar(Q_(j, ks), 4)))
-        # O row offsets for the stores: row * o_row + 16 hh
-        for j in range(2):
-            ins += [I(f"v_lshl_add_u32 v4, v1, 6, v2", VALU, rd=vr(1) + vr(2), wr=vr(4)),
-                    I(f"v_add_u32_e32 v4, {32 * j}, v4", VALU, rd=vr(4), wr=vr(4)),
-                    I(f"v_mul_lo_u32 v{V_OOFF[j]}, v4, s{Ro}", VALU, rd=vr(4) + sr(Ro), wr=vr(V_OOFF[j])),
+                    I(f"v_lshlrev_b32_e32 v{V_LSEOFF[j]}, 2, v{V_ROW[j]}", VALU, rd=vr(V_ROW[j]), wr=vr(V_LSEOFF[j])),
+                    I(f"v_mul_lo_u32 v{V_OOFF[j]}, v{V_ROW[j]}, s{Ro}", VALU, rd=vr(V_ROW[j]) + sr(Ro), wr=vr(V_OOFF[j])),
                     I(f"v_lshl_add_u32 v{V_OOFF[j]}, v3, 4, v{V_OOFF[j]}", VALU, rd=vr(3) + vr(V_OOFF[j]), wr=vr(V_OOFF[j]))]
         # LDS lane bases (fa_common.h LdsBases): rb = r*64 + ((c ^ xr) << 4), c = hh / 2+hh, xr = (r>>2)&3
         ins += [I("v_bfe_u32 v4, v2, 2, 2", VALU, rd=vr(2), wr=vr(4)),                      # xr
@@ -682,7 +634,7 @@ class K:
                 I("v_add_u32_e32 v9, 2, v3", VALU, rd=vr(3), wr=vr(9)),
                 I("v_xor_b32_e32 v9, v7, v9", VALU, rd=vr(7) + vr(9), wr=vr(9)),
                 I(f"v_lshl_add_u32 v{V_TB1}, v9, 4, v8", VALU, rd=vr(9) + vr(8), wr=vr(V_TB1))]
-        # DMA voffsets: row = 16 wave + lane / 4, chunk = (lane & 3) ^ ((row >> 2) & 3);
+        # DMA voffsets (tile 0): row = 16 wave + lane / 4, chunk = (lane & 3) ^ ((row >> 2) & 3);
         # voff_j = row * kv_row + 64 j + 16 chunk
         ins += [I(f"v_lshrrev_b32_e32 v4, 2, v{V_LANE}", VALU, rd=vr(V_LANE), wr=vr(4)),
                 I("v_lshl_add_u32 v4, v1, 4, v4", VALU, rd=vr(1) + vr(4), wr=vr(4)),              # row
@@ -694,48 +646,244 @@ class K:
         for jj in range(1, 4):
             ins.append(I(f"v_add_u32_e32 v{V_VOFF + jj}, {64 * jj}, v{V_VOFF}", VALU, rd=vr(V_VOFF), wr=vr(V_VOFF + jj)))
         ins += [I(f"v_mov_b32_e32 v{V_NINF}, 0xff800000", VALU, wr=vr(V_NINF)),
-                I(f"s_lshl_b32 s{S_DOFF}, s{S_WAVE}, 10", SALU, rd=sr(S_WAVE), wr=sr(S_DOFF)),
-                I(f"s_mov_b32 s{S_KOFF}, 0", SALU, wr=sr(S_KOFF)),
-                I(f"s_mov_b32 s{S_VOFF}, {VBASE}", SALU, wr=sr(S_VOFF)),
+                I(f"s_lshl_b32 s{S_TB}, s{Rkv}, 6", SALU, rd=sr(Rkv), wr=sr(S_TB)),
+                I(f"s_mov_b32 s{S_ROUND}, 0", SALU, wr=sr(S_ROUND)),
+                I(f"s_mov_b32 s{S_WARM}, 0", SALU, wr=sr(S_WARM)),
                 I(f"s_mov_b32 s{S_DT}, 0", SALU, wr=sr(S_DT)),
-                I(f"s_mov_b32 s{S_N}, 0", SALU, wr=sr(S_N)),
-                I(f"s_mov_b32 s{S_N0}, 0", SALU, wr=sr(S_N0))]
-        # zero O, running sums
-        for i in range(128):
-            ins.append(I(f"v_accvgpr_write_b32 a{i}, 0", ACCW, wr=ar(i)))
-        ins += [I(f"v_mov_b32_e32 v{V_L[0]}, 0", VALU, wr=vr(V_L[0])),
-                I(f"v_mov_b32_e32 v{V_L[1]}, 0", VALU, wr=vr(V_L[1])),
-                I(f"v_mov_b32_e32 v{V_NEGMC[0]}, 0", VALU, wr=vr(V_NEGMC[0])),
-                I(f"v_mov_b32_e32 v{V_NEGMC[1]}, 0", VALU, wr=vr(V_NEGMC[1]))]
+                # the rng_state store has read its descriptor before anything rewrites s92..95
+                I("s_waitcnt vmcnt(0)", WAIT)]
+        return ins
+
+    def item_pos(self, dst, plus):
+        """dst = r G + (r odd ? G - 1 - w : w), r = S_ROUND + plus (snake order over the sorted items)"""
+        I = Inst
+        T, R = S_TMP, S_TMP + 1
+        return [I(f"s_add_u32 s{R}, s{S_ROUND}, {plus}", SALU),
+                I(f"s_mul_i32 s{dst}, s{R}, s{S_GRID}", SALU),
+                I(f"s_sub_u32 s{T}, s{S_GRID}, 1", SALU),
+                I(f"s_sub_u32 s{T}, s{T}, s2", SALU),
+                I(f"s_bitcmp1_b32 s{R}, 0", SALU),
+                I(f"s_cselect_b32 s{T}, s{T}, s2", SALU),
+                I(f"s_add_u32 s{dst}, s{dst}, s{T}", SALU)]
+
+    def item_geom(self, kind, l_skip):
+        """Geometry of the item at list position S_SWT.  kind 'cold' / 'warm': the current item --
+        Q (cold) / O / LSE (and K / V when cold) descriptors, m0 in S_M0R, tile counts; 'next': the
+        next item's Q / K / V descriptors (S_QD2 / S_KD2 / S_VD2) and tile count S_NXN (0 when it
+        does not exist or is empty).  The table entry is (bidb | head << 16, kvh | m_block << 16)."""
+        I = Inst
+        A = self.kargs()
+        T0, T1, T2, T3 = S_TMP, S_TMP + 1, S_TMP + 2, S_TMP + 3
+        nxt = kind == "next"
+        ins = []
+        l_none = self.lab("none") if nxt else None
+        l_done = self.lab("gdone") if nxt else None
+        if nxt:
+            ins += self.item_pos(S_SWT, 1)
+            ins += [I(f"s_cmp_ge_u32 s{S_SWT}, s{S_NITEMS}", SALU), I(f"s_cbranch_scc1 {l_none}", BRANCH)]
+        Psch = A["Psch"]
+        ins += [I(f"s_lshl_b32 s{T0}, s{S_SWT}, 3", SALU, rd=sr(S_SWT), wr=sr(T0)),
+                I(f"s_load_dwordx2 s[{T0}:{T1}], s[{Psch}:{Psch + 1}], s{T0}", SMEM, rd=sr(Psch, 2) + sr(T0), wr=sr(T0, 2)),
+                I("s_waitcnt lgkmcnt(0)", WAIT)]
+        # scalars: bidb (T2), head (T3), kvh (S_N), m_block (S_N0) -- temporarily
+        BIDB, HEAD, KVH, MB = T2, T3, S_N, S_N0
+        ins += [I(f"s_and_b32 s{BIDB}, s{T0}, 0xffff", SALU, rd=sr(T0), wr=sr(BIDB)),
+                I(f"s_lshr_b32 s{HEAD}, s{T0}, 16", SALU, rd=sr(T0), wr=sr(HEAD)),
+                I(f"s_and_b32 s{KVH}, s{T1}, 0xffff", SALU, rd=sr(T1), wr=sr(KVH)),
+                I(f"s_lshr_b32 s{MB}, s{T1}, 16", SALU, rd=sr(T1), wr=sr(MB))]
+        # varlen geometry (BlockInfo, block_info.h:14-31): 64-bit byte offsets (lo, hi) of row 0 of
+        # this sequence in Q, O and K/V; seqlens in SQ / SK (overwritten in place)
+        QOFF, OOFF, KOFF = (86, 87), (88, 89), (90, 91)
+        SQ, SK = A["SQ"], A["SK"]
+
+        def mul64(dst, a32, b32):
+            return [I(f"s_mul_i32 s{dst[0]}, s{a32}, s{b32}", SALU, rd=sr(a32) + sr(b32), wr=sr(dst[0])),
+                    I(f"s_mul_hi_u32 s{dst[1]}, s{a32}, s{b32}", SALU, rd=sr(a32) + sr(b32), wr=sr(dst[1]))]
+
+        def mul64_i64(dst, a32, b64):   # a32 * (b64 lo, hi) -> dst (lo, hi)
+            return [I(f"s_mul_i32 s{dst[0]}, s{a32}, s{b64}", SALU, rd=sr(a32) + sr(b64), wr=sr(dst[0])),
+                    I(f"s_mul_hi_u32 s{dst[1]}, s{a32}, s{b64}", SALU, rd=sr(a32) + sr(b64), wr=sr(dst[1])),
+                    I(f"s_mul_i32 s{T0}, s{a32}, s{b64 + 1}", SALU, rd=sr(a32) + sr(b64 + 1), wr=sr(T0)),
+                    I(f"s_add_u32 s{dst[1]}, s{dst[1]}, s{T0}", SALU, rd=sr(dst[1]) + sr(T0), wr=sr(dst[1]))]
+
+        parts = [(A["Pcq"], A["Bq"], A["Rq"], QOFF, SQ)]
+        if not nxt:
+            parts.append((A["Pcq"], A["Bo"], A["Ro"], OOFF, None))
+        parts.append((A["Pck"], A["Bk"], A["Rkv"], KOFF, SK))
+        for cu, bstride, rstride, off, seq in parts:
+            lf, ld = self.lab("fixed"), self.lab("vdone")
+            ins += [I(f"s_cmp_eq_u64 s[{cu}:{cu + 1}], 0", SALU, rd=sr(cu, 2), wr=[("scc", 0)]),
+                    I(f"s_cbranch_scc1 {lf}", BRANCH),
+                    I(f"s_lshl_b32 s{T1}, s{BIDB}, 2", SALU, rd=sr(BIDB), wr=sr(T1)),
+                    I(f"s_load_dwordx2 s[{off[0]}:{off[1]}], s[{cu}:{cu + 1}], s{T1}", SMEM, rd=sr(cu, 2) + sr(T1), wr=sr(off[0], 2)),
+                    I("s_waitcnt lgkmcnt(0)", WAIT)]
+            if seq is not None:
+                ins += [I(f"s_sub_u32 s{seq}, s{off[1]}, s{off[0]}", SALU, rd=sr(off[0], 2), wr=sr(seq))]
+            ins += [I(f"s_bitcmp1_b32 s{A['FL']}, 0", SALU, rd=sr(A["FL"]), wr=[("scc", 0)]),
+                    I(f"s_cbranch_scc1 {lf}", BRANCH),
+                    I(f"s_mov_b32 s{T1}, s{off[0]}", SALU, rd=sr(off[0]), wr=sr(T1))]
+            ins += mul64(off, T1, rstride)
+            ins += [I(f"s_branch {ld}", BRANCH), label(lf)]
+            ins += mul64_i64(off, BIDB, bstride)
+            ins += [label(ld)]
+        # m0 = 256 m_block; an item past its sequence is skipped (cur) / counts as absent (next)
+        M0R = S_M0R
+        ins += [I(f"s_lshl_b32 s{M0R}, s{MB}, 8", SALU, rd=sr(MB), wr=sr(M0R)),
+                I(f"s_cmp_ge_i32 s{M0R}, s{SQ}", SALU, rd=sr(M0R) + sr(SQ), wr=[("scc", 0)]),
+                I(f"s_cbranch_scc1 {l_none if nxt else l_skip}", BRANCH)]
+        # rows of this item: nrow = min(sq - m0, 256)
+        NROW = S_SWT if nxt else S_NBLK
+        ins += [I(f"s_sub_u32 s{NROW}, s{SQ}, s{M0R}", SALU, rd=sr(SQ) + sr(M0R), wr=sr(NROW)),
+                I(f"s_min_u32 s{NROW}, s{NROW}, {BM}", SALU, rd=sr(NROW), wr=sr(NROW))]
+
+        def addr(dst4, ptr, off64, head, hstride, rows=None, rstride=None, nrec=None):
+            """descriptor at ptr + off64 + head * hstride (+ rows * rstride)"""
+            o = []
+            o += [I(f"s_mul_i32 s{T0}, s{head}, s{hstride}", SALU, rd=sr(head) + sr(hstride), wr=sr(T0)),
+                  I(f"s_mul_hi_u32 s{T1}, s{head}, s{hstride}", SALU, rd=sr(head) + sr(hstride), wr=sr(T1)),
+                  I(f"s_add_u32 s{dst4}, s{ptr}, s{T0}", SALU, rd=sr(ptr) + sr(T0), wr=sr(dst4) + [("scc", 0)]),
+                  I(f"s_addc_u32 s{dst4 + 1}, s{ptr + 1}, s{T1}", SALU, rd=sr(ptr + 1) + sr(T1) + [("scc", 0)], wr=sr(dst4 + 1) + [("scc", 0)]),
+                  I(f"s_add_u32 s{dst4}, s{dst4}, s{off64[0]}", SALU, rd=sr(dst4) + sr(off64[0]), wr=sr(dst4) + [("scc", 0)]),
+                  I(f"s_addc_u32 s{dst4 + 1}, s{dst4 + 1}, s{off64[1]}", SALU, rd=sr(dst4 + 1) + sr(off64[1]) + [("scc", 0)], wr=sr(dst4 + 1))]
+            if rows is not None:
+                o += [I(f"s_mul_i32 s{T0}, s{rows}, s{rstride}", SALU, rd=sr(rows) + sr(rstride), wr=sr(T0)),
+                      I(f"s_mul_hi_u32 s{T1}, s{rows}, s{rstride}", SALU, rd=sr(rows) + sr(rstride), wr=sr(T1)),
+                      I(f"s_add_u32 s{dst4}, s{dst4}, s{T0}", SALU, rd=sr(dst4) + sr(T0), wr=sr(dst4) + [("scc", 0)]),
+                      I(f"s_addc_u32 s{dst4 + 1}, s{dst4 + 1}, s{T1}", SALU, rd=sr(dst4 + 1) + sr(T1), wr=sr(dst4 + 1))]
+            o += [I(f"s_and_b32 s{dst4 + 1}, s{dst4 + 1}, 0xffff", SALU, rd=sr(dst4 + 1), wr=sr(dst4 + 1))]
+            o += nrec
+            o += [I(f"s_mov_b32 s{dst4 + 3}, 0x20000", SALU, wr=sr(dst4 + 3))]
+            return o
+
+        Rq, Rkv, Ro = A["Rq"], A["Rkv"], A["Ro"]
+        qd = S_QD2 if nxt else S_QD
+        kd, vd = (S_KD2, S_VD2) if nxt else (S_KD, S_VD)
+        if kind != "warm":
+            ins += addr(qd, A["Pq"], QOFF, HEAD, A["Hq"], rows=M0R, rstride=Rq,
+                        nrec=[I(f"s_mul_i32 s{qd + 2}, s{NROW}, s{Rq}", SALU, rd=sr(NROW) + sr(Rq), wr=sr(qd + 2))])
+        if not nxt:
+            ins += addr(S_OD, A["Po"], OOFF, HEAD, A["Ho"], rows=M0R, rstride=Ro,
+                        nrec=[I(f"s_mul_i32 s{S_OD + 2}, s{NROW}, s{Ro}", SALU, rd=sr(NROW) + sr(Ro), wr=sr(S_OD + 2))])
+        # K / V descriptors: every key of this sequence and kv head (host checks sk * kv_row < 2^31)
+        if kind != "warm":
+            ins += addr(kd, A["Pk"], KOFF, KVH, A["Hk"],
+                        nrec=[I(f"s_mul_i32 s{kd + 2}, s{SK}, s{Rkv}", SALU, rd=sr(SK) + sr(Rkv), wr=sr(kd + 2))])
+            ins += addr(vd, A["Pv"], KOFF, KVH, A["Hv"],
+                        nrec=[I(f"s_mul_i32 s{vd + 2}, s{SK}, s{Rkv}", SALU, rd=sr(SK) + sr(Rkv), wr=sr(vd + 2))])
+        if not nxt:
+            # LSE descriptor: lse + ((bidb * h + head) * lse_pitch + m0) * 4
+            ins += [I(f"s_mul_i32 s{T0}, s{BIDB}, s{A['NH']}", SALU, rd=sr(BIDB) + sr(A["NH"]), wr=sr(T0)),
+                    I(f"s_add_u32 s{T0}, s{T0}, s{HEAD}", SALU, rd=sr(T0) + sr(HEAD), wr=sr(T0)),
+                    I(f"s_mul_i32 s{S_LD + 2}, s{T0}, s{A['LP']}", SALU, rd=sr(T0) + sr(A["LP"]), wr=sr(S_LD + 2)),
+                    I(f"s_mul_hi_u32 s{S_LD + 3}, s{T0}, s{A['LP']}", SALU, rd=sr(T0) + sr(A["LP"]), wr=sr(S_LD + 3)),
+                    I(f"s_add_u32 s{S_LD + 2}, s{S_LD + 2}, s{M0R}", SALU, rd=sr(S_LD + 2) + sr(M0R), wr=sr(S_LD + 2) + [("scc", 0)]),
+                    I(f"s_addc_u32 s{S_LD + 3}, s{S_LD + 3}, 0", SALU, rd=sr(S_LD + 3), wr=sr(S_LD + 3)),
+                    I(f"s_lshl_b64 s[{S_LD + 2}:{S_LD + 3}], s[{S_LD + 2}:{S_LD + 3}], 2", SALU, rd=sr(S_LD + 2, 2), wr=sr(S_LD + 2, 2)),
+                    I(f"s_add_u32 s{S_LD}, s{A['Pl']}, s{S_LD + 2}", SALU, rd=sr(A["Pl"]) + sr(S_LD + 2), wr=sr(S_LD) + [("scc", 0)]),
+                    I(f"s_addc_u32 s{S_LD + 1}, s{A['Pl'] + 1}, s{S_LD + 3}", SALU, rd=sr(A["Pl"] + 1) + sr(S_LD + 3), wr=sr(S_LD + 1)),
+                    I(f"s_and_b32 s{S_LD + 1}, s{S_LD + 1}, 0xffff", SALU, rd=sr(S_LD + 1), wr=sr(S_LD + 1)),
+                    I(f"s_lshl_b32 s{S_LD + 2}, s{NROW}, 2", SALU, rd=sr(NROW), wr=sr(S_LD + 2)),
+                    I(f"s_mov_b32 s{S_LD + 3}, 0x20000", SALU, wr=sr(S_LD + 3))]
+        # tile counts: n_end = causal ? min(sk, m0 + 256) : sk; nblk = ceil(n_end / 64);
+        # nfast = min(nblk, (causal ? min(sk, m0 + 1) : sk) / 64)
+        if self.causal:
+            ins += [I(f"s_add_u32 s{T0}, s{M0R}, {BM}", SALU, rd=sr(M0R), wr=sr(T0)),
+                    I(f"s_min_i32 s{T0}, s{T0}, s{SK}", SALU, rd=sr(T0) + sr(SK), wr=sr(T0)),
+                    I(f"s_add_u32 s{T1}, s{M0R}, 1", SALU, rd=sr(M0R), wr=sr(T1)),
+                    I(f"s_min_i32 s{T1}, s{T1}, s{SK}", SALU, rd=sr(T1) + sr(SK), wr=sr(T1))]
+        else:
+            ins += [I(f"s_mov_b32 s{T0}, s{SK}", SALU, rd=sr(SK), wr=sr(T0)),
+                    I(f"s_mov_b32 s{T1}, s{SK}", SALU, rd=sr(SK), wr=sr(T1))]
+        nb = S_NXN if nxt else S_NBLK
+        ins += [I(f"s_max_i32 s{T0}, s{T0}, 0", SALU, rd=sr(T0), wr=sr(T0)),
+                I(f"s_add_u32 s{T0}, s{T0}, {BN - 1}", SALU, rd=sr(T0), wr=sr(T0)),
+                I(f"s_lshr_b32 s{nb}, s{T0}, 6", SALU, rd=sr(T0), wr=sr(nb))]
+        if not nxt:
+            ins += [I(f"s_max_i32 s{T1}, s{T1}, 0", SALU, rd=sr(T1), wr=sr(T1)),
+                    I(f"s_lshr_b32 s{T1}, s{T1}, 6", SALU, rd=sr(T1), wr=sr(T1)),
+                    I(f"s_min_u32 s{T1}, s{T1}, s{S_NBLK}", SALU, rd=sr(T1) + sr(S_NBLK), wr=sr(T1)),
+                    I(f"s_sub_i32 s{S_NF2}, s{T1}, 2", SALU, rd=sr(T1), wr=sr(S_NF2)),
+                    I(f"s_sub_i32 s{S_NL1}, s{S_NBLK}, 1", SALU, rd=sr(S_NBLK), wr=sr(S_NL1))]
+            # per-lane mask limit base: (causal ? min(m0 + row, sk - 1) : sk - 1) - 4 hh
+            ins += [I(f"s_sub_i32 s{T0}, s{SK}, 1", SALU, rd=sr(SK), wr=sr(T0))]
+            for j in range(2):
+                if self.causal:
+                    ins += [I(f"v_add_u32_e32 v{V_LB[j]}, s{M0R}, v{V_ROW[j]}", VALU, rd=sr(M0R) + vr(V_ROW[j]), wr=vr(V_LB[j])),
+                            I(f"v_min_i32_e32 v{V_LB[j]}, s{T0}, v{V_LB[j]}", VALU, rd=sr(T0) + vr(V_LB[j]), wr=vr(V_LB[j]))]
+                else:
+                    ins += [I(f"v_mov_b32_e32 v{V_LB[j]}, s{T0}", VALU, rd=sr(T0), wr=vr(V_LB[j]))]
+                ins += [I(f"v_sub_u32_e32 v{V_LB[j]}, v{V_LB[j]}, v{V_HH4}", VALU, rd=vr(V_LB[j]) + vr(V_HH4), wr=vr(V_LB[j]))]
+        else:
+            ins += [I(f"s_branch {l_done}", BRANCH), label(l_none),
+                    I(f"s_mov_b32 s{S_NXN}, 0", SALU)]
+            ins += [I(f"s_mov_b32 s{S_QD2 + i}, s{S_QD + i}", SALU) for i in range(4)]
+            ins += [I(f"s_mov_b32 s{S_QD2 + 2}, 0", SALU), label(l_done)]
+        return ins
+
+    def item_start(self, l_cold, l_cold_wait, l_warm, l_skip, l_tile0, l_epi, l_end):
+        """cold start (first item; after an item whose successor could not be prefetched) and warm
+        start (the next item's K/V tiles 0..2 and Q already issued by the previous item)"""
+        I = Inst
+        ins = []
+        # ---- cold
+        ins += [label(l_cold_wait), Inst("s_waitcnt vmcnt(0) lgkmcnt(0)", WAIT), Inst("s_barrier", BARRIER),
+                label(l_cold)]
+        ins += self.item_pos(S_SWT, 0)
+        ins += [I(f"s_cmp_ge_u32 s{S_SWT}, s{S_NITEMS}", SALU), I(f"s_cbranch_scc1 {l_end}", BRANCH)]
+        ins += self.item_geom("cold", l_skip)
+        # DMA offsets back to tile 0 of the fresh descriptors
+        ins += [I(f"s_mul_i32 s{S_SWT}, s{S_DT}, s{S_TB}", SALU)]
+        ins += [I(f"v_subrev_u32_e32 v{V_VOFF + jj}, s{S_SWT}, v{V_VOFF + jj}", VALU) for jj in range(4)]
+        ins += [I(f"s_mov_b32 s{S_DT}, 0", SALU), I(f"s_mov_b32 s{S_DLIM}, s{S_NBLK}", SALU)]
+        # Q fragments into the accumulator file: lane holds Q[row][16 ks + 8 hh .. +7]
+        for j in range(2):
+            for ks in range(KS):
+                ins.append(I(f"buffer_load_dwordx4 {rtxt('a', Q_(j, ks), 4)}, v{V_QOFF[j]}, s[{S_QD}:{S_QD + 3}], 0 offen offset:{32 * ks}",
+                             VLOAD, rd=vr(V_QOFF[j]) + sr(S_QD, 4), wr=ar(Q_(j, ks), 4)))
+        ins += self.item_geom("next", None)
+        ins += [I(f"s_mov_b32 s{S_WARM}, 0", SALU),
+                I(f"s_mov_b32 s{S_KOFF}, 0", SALU),
+                I(f"s_lshl_b32 s{S_DOFF}, s{S_WAVE}, 10", SALU)]
+        ins += self.item_zero()
         # no tiles at all: epilogue (O = 0, LSE = +inf)
         ins += [I(f"s_cmp_eq_u32 s{S_NBLK}, 0", SALU, rd=sr(S_NBLK), wr=[("scc", 0)]),
                 I("s_waitcnt vmcnt(0)", WAIT),
                 I(f"s_cbranch_scc1 {l_epi}", BRANCH)]
-        # DMA of tiles 0..3 (tiles past nblk: zero records)
         for tile in range(4):
-            if not OPT_NOZERO:
-                ins += [nop(15) for _ in range(OPT_ZERO_NOP)] + [
-                    I(f"s_cmp_lt_u32 s{S_DT}, s{S_NBLK}", SALU, rd=sr(S_DT) + sr(S_NBLK), wr=[("scc", 0)]),
-                    I(f"s_cselect_b32 s{S_KD + 2}, s{S_KD + 2}, 0", SALU, rd=sr(S_KD + 2), wr=sr(S_KD + 2)),
-                    I(f"s_cselect_b32 s{S_VD + 2}, s{S_VD + 2}, 0", SALU, rd=sr(S_VD + 2), wr=sr(S_VD + 2))]
-            for jj in range(4):
-                ins += [I(f"s_add_u32 m0, s{S_DOFF}, {jj * 4096}", SALU, rd=sr(S_DOFF), wr=[("m0", 0)]),
-                        I(f"buffer_load_dwordx4 v{V_VOFF + jj}, s[{S_KD}:{S_KD + 3}], 0 offen lds", DMA,
-                          rd=vr(V_VOFF + jj) + sr(S_KD, 4) + [("m0", 0)])]
-            for jj in range(4):
-                ins += [I(f"s_add_u32 m0, s{S_DOFF}, {VBASE + jj * 4096}", SALU, rd=sr(S_DOFF), wr=[("m0", 0)]),
-                        I(f"buffer_load_dwordx4 v{V_VOFF + jj}, s[{S_VD}:{S_VD + 3}], 0 offen lds", DMA,
-                          rd=vr(V_VOFF + jj) + sr(S_VD, 4) + [("m0", 0)])]
-            for jj in range(4):
-                ins.append(I(f"v_add_u32_e32 v{V_VOFF + jj}, s{S_TB}, v{V_VOFF + jj}", VALU, rd=sr(S_TB) + vr(V_VOFF + jj), wr=vr(V_VOFF + jj)))
-            ins += [I(f"s_add_u32 s{S_DOFF}, s{S_DOFF}, {TILE}", SALU, rd=sr(S_DOFF), wr=sr(S_DOFF)),
-                    I(f"s_add_u32 s{S_DT}, s{S_DT}, 1", SALU, rd=sr(S_DT), wr=sr(S_DT))]
-        # Q + tiles 0, 1, 2 landed (tile 3 in flight; K(2) is prefetched during step 0)
-        ins += [I("s_waitcnt vmcnt(8)", WAIT), I("s_barrier", BARRIER)]
+            ins += self.dma_tile_ops(f"c{tile}")
+        ins += [I(f"s_branch {l_tile0}", BRANCH)]
+        ins += [label(l_skip), I(f"s_add_u32 s{S_ROUND}, s{S_ROUND}, 1", SALU), I(f"s_branch {l_cold}", BRANCH)]
+        # ---- warm
+        ins += [label(l_warm)]
+        ins += self.item_pos(S_SWT, 0)
+        ins += [I(f"s_mov_b32 s{S_QD + i}, s{S_QD2 + i}", SALU) for i in range(4)]
+        ins += self.item_geom("warm", l_skip)
+        ins += self.item_geom("next", None)
+        ins += [I(f"s_mov_b32 s{S_WARM}, 0", SALU),
+                I(f"s_sub_u32 s{S_KOFF}, s{S_VOFF}, {VBASE}", SALU)]
+        ins += self.item_zero()
+        ins += self.dma_tile_ops("w3")
+        return ins
+
+    def item_zero(self):
+        I = Inst
+        ins = [I(f"s_mov_b32 s{S_N}, 0", SALU, wr=sr(S_N)),
+               I(f"s_mov_b32 s{S_N0}, 0", SALU, wr=sr(S_N0))]
+        ins += [I(f"v_accvgpr_write_b32 a{i}, 0", ACCW, wr=ar(i)) for i in range(128)]
+        ins += [I(f"v_mov_b32_e32 v{V_L[0]}, 0", VALU, wr=vr(V_L[0])),
+                I(f"v_mov_b32_e32 v{V_L[1]}, 0", VALU, wr=vr(V_L[1])),
+                I(f"v_mov_b32_e32 v{V_NEGMC[0]}, 0", VALU, wr=vr(V_NEGMC[0])),
+                I(f"v_mov_b32_e32 v{V_NEGMC[1]}, 0", VALU, wr=vr(V_NEGMC[1]))]
+        return ins
+
+    def tile0(self, l_entry_last, l_entry_fast, l_entry_masked):
+        """Q + tiles 0, 1, 2 landed (tile 3 in flight); tile 0: S(0, a), S(0, b) -> masked, explicit
+        row max, P(0, a); then into the step loop"""
+        I = Inst
+        ins = [I("s_waitcnt vmcnt(8)", WAIT), I("s_barrier", BARRIER)]
         ins += self.dump("pro_lds")
-        # ---- tile 0: S(0, a), S(0, b) -> masked, explicit row max, P(0, a)
-        ins += [I(f"v_add_u32_e32 v{V_KB0}, 0, v{V_RB0}", VALU, rd=vr(V_RB0), wr=vr(V_KB0)),
-                I(f"v_add_u32_e32 v{V_KB1}, 0, v{V_RB1}", VALU, rd=vr(V_RB1), wr=vr(V_KB1))]
+        ins += [I(f"v_add_u32_e32 v{V_KB0}, s{S_KOFF}, v{V_RB0}", VALU, rd=sr(S_KOFF) + vr(V_RB0), wr=vr(V_KB0)),
+                I(f"v_add_u32_e32 v{V_KB1}, s{S_KOFF}, v{V_RB1}", VALU, rd=sr(S_KOFF) + vr(V_RB1), wr=vr(V_KB1))]
         mfm = []
         for i in range(32):
             st, ks, j = i // 16, (i % 16) // 2, i % 2
@@ -770,8 +918,12 @@ class K:
         ins += sm
         ins += [Inst(f"v_mov_b32_e32 v{V_L[0]}, v{V_PS[0]}", VALU, rd=vr(V_PS[0]), wr=vr(V_L[0]))]
         ins += self.dump("pro_end")
-        # entry (S_KOFF addresses tile n+1 = 1 at step 0; the LAST step's refit takes S_KOFF - TILE)
-        ins += [I(f"s_mov_b32 s{S_KOFF}, {TILE}", SALU, wr=sr(S_KOFF)),
+        # V reads tile 0 (slot S_KOFF); S_KOFF -> tile 1 (the LAST step's refit takes S_KOFF - TILE)
+        ins += [I(f"s_add_u32 s{S_VOFF}, s{S_KOFF}, {VBASE}", SALU),
+                I(f"s_add_u32 s{S_KOFF}, s{S_KOFF}, {TILE}", SALU),
+                I(f"s_sub_u32 s{S_SWT}, s{S_KOFF}, {NSLOT * TILE}", SALU),
+                I(f"s_cmp_ge_u32 s{S_KOFF}, {NSLOT * TILE}", SALU),
+                I(f"s_cselect_b32 s{S_KOFF}, s{S_SWT}, s{S_KOFF}", SALU),
                 I(f"s_cmp_eq_u32 s{S_NBLK}, 1", SALU, rd=sr(S_NBLK), wr=[("scc", 0)]),
                 I(f"s_cbranch_scc1 {l_entry_last}", BRANCH)]
         # K(1) base + prefetch of its first three fragments
@@ -785,6 +937,7 @@ class K:
                 I(f"s_branch {l_entry_masked}", BRANCH)]
         return ins
 
+    # ------------------------------------------------------------------ epilogue
     def epilogue(self):
         ins = []
         t = 0   # the score registers are free after the last step
@@ -821,12 +974,12 @@ class K:
 
     # ------------------------------------------------------------------ whole kernel
     def build(self):
-        self.lab_end = self.lab("end")
+        self.switches = []
+        l_end = self.lab("end")
+        self.lab_end = l_end
         l_epi = self.lab("epi")
-        L = {k: self.lab(k) for k in ("fast0", "fast1", "sel0", "sel1", "masked0", "masked1", "last0", "last1")}
-        pro = self.prologue(l_epi, L["last0"], L["fast0"], L["sel0"])
-        blocks = []     # (instructions, predecessors' tail for hazard checks)
-        refits = []
+        L = {k: self.lab(k) for k in ("fast0", "fast1", "sel0", "sel1", "masked0", "masked1", "last0", "last1",
+                                      "cold", "coldw", "warm", "skip", "tile0")}
         code = []
 
         def emit_block(insts, pre=()):
@@ -835,7 +988,12 @@ class K:
             code.extend(out)
             return out
 
-        pro_out = emit_block(pro)
+        tailpad = [nop(15)]   # block entries: every predecessor ends with a barrier / branch; pad anyway
+        emit_block(self.entry())
+        emit_block(self.item_start(L["cold"], L["coldw"], L["warm"], L["skip"], L["tile0"], l_epi, l_end), pre=tailpad)
+        code.append(label(L["tile0"]))
+        emit_block(self.tile0(L["last0"], L["fast0"], L["sel0"]), pre=tailpad)
+        refits = []
         f0, r = self.step(0, "fast", "f0"); refits += r
         f1, r = self.step(1, "fast", "f1"); refits += r
         m0, r = self.step(0, "masked", "m0"); refits += r
@@ -843,7 +1001,6 @@ class K:
         la0, r = self.step(0, "last", "l0"); refits += r
         la1, r = self.step(1, "last", "l1"); refits += r
         I = Inst
-        tailpad = [nop(15)]   # block entries: every predecessor ends with a barrier / branch; pad anyway
         code.append(label(L["fast0"]))
         emit_block(f0 + self.dump("f0_end"), pre=tailpad)
         code += [I(f"s_cmp_gt_i32 s{S_N}, s{S_NF2}", SALU), I(f"s_cbranch_scc1 {L['sel1']}", BRANCH)]
@@ -866,10 +1023,16 @@ class K:
         emit_block(la1, pre=tailpad)
         code.append(label(l_epi))
         emit_block([nop(15)] + self.epilogue(), pre=tailpad)
-        code.append(label(self.lab_end))
+        # next item of this workgroup: warm when the DMA stream already runs into it
+        code += [I(f"s_add_u32 s{S_ROUND}, s{S_ROUND}, 1", SALU),
+                 I(f"s_cmp_eq_u32 s{S_WARM}, 1", SALU), I(f"s_cbranch_scc1 {L['warm']}", BRANCH),
+                 I(f"s_branch {L['coldw']}", BRANCH)]
+        code.append(label(l_end))
         code.append(I("s_endpgm", SOPP))
         for rb in refits:
             code.extend(rb)
+        for sb in self.switches:
+            emit_block(sb, pre=tailpad)
         return code
 
     def render(self):

@@ -42,14 +42,17 @@ struct FwdAsmArgs {
   int32_t sq, sk, lse_pitch, h;
   float c;
   int32_t flags;    // bit 0: varlen_padded_input
+  int32_t n_items;  // entries of the work table
+  int32_t grid;     // workgroups: workgroup w runs items r G + (r odd ? G - 1 - w : w), r = 0, 1, ...
   int32_t pad;
 };
-static_assert(sizeof(FwdAsmArgs) == 176, "FwdAsmArgs layout");
+static_assert(sizeof(FwdAsmArgs) == 184, "FwdAsmArgs layout");
 
 constexpr int kMaxDev = 64;
 struct DevModule {
   hipModule_t mod = nullptr;
   hipFunction_t fn[4] = {};   // [bf16 causal, bf16 full, f16 causal, f16 full]
+  int cus = 0;
   std::map<std::tuple<int, int, int, int, int>, uint32_t*> tables;
 };
 std::mutex g_mu;
@@ -69,6 +72,7 @@ DevModule& module_for(int dev) {
   if (m.mod == nullptr) {
     check(hipModuleLoadData(&m.mod, fa_fwd_asm_co), "hipModuleLoadData");
     for (int i = 0; i < 4; ++i) check(hipModuleGetFunction(&m.fn[i], m.mod, kNames[i]), kNames[i]);
+    check(hipDeviceGetAttribute(&m.cus, hipDeviceAttributeMultiprocessorCount, dev), "hipDeviceGetAttribute");
   }
   return m;
 }
@@ -102,6 +106,59 @@ std::vector<uint32_t> build_table(int b, int h, int hk, int nmb, int hp) {
 }
 
 bool fits32(int64_t x) { return x >= 0 && x < (1ll << 31); }
+
+// Varlen work list, built on the device (the host cannot list the items without reading
+// cu_seqlens back): the (sequence, query block, head) items that hold rows, heaviest first --
+// query block index descending; within a level, sequences by block count descending, heads
+// fastest (as build_table's order without the empty items).  out[0] = item count, entry i at
+// out[2 + 2 i] (the kernel reads the count from the first dword, the entries 8 bytes in).
+// Shared memory: nb[b] | order[b] | start[nmb + 1] | cur[nmb + 1] | level offset[nmb].
+constexpr int kVarlenMaxSeqs = 8192, kVarlenMaxBlocks = 2048;
+__global__ void __launch_bounds__(1024) varlen_items_kernel(const int* cu_q, int b, int h, int g, int nmb,
+                                                            uint32_t* out) {
+  extern __shared__ int sm[];
+  int* nb = sm;
+  int* order = nb + b;
+  int* start = order + b;
+  int* cur = start + nmb + 1;
+  int* off = cur + nmb + 1;
+  const int t = threadIdx.x, T = blockDim.x;
+  for (int i = t; i <= nmb; i += T) start[i] = 0;
+  __syncthreads();
+  for (int s = t; s < b; s += T) {
+    const int len = cu_q[s + 1] - cu_q[s];
+    int n = len > 0 ? (len + 255) / 256 : 0;
+    n = n > nmb ? nmb : n;
+    nb[s] = n;
+    atomicAdd(&start[n], 1);
+  }
+  __syncthreads();
+  if (t == 0) {
+    // start[n] = first sorted position of the sequences with nb == n (larger nb first), which is
+    // also #{s : nb[s] > n}: the number of sequences present at level n
+    int acc = 0;
+    for (int n = nmb; n >= 0; --n) { const int c = start[n]; start[n] = acc; cur[n] = acc; acc += c; }
+    int total = 0;
+    for (int mb = nmb - 1; mb >= 0; --mb) { off[mb] = total; total += h * start[mb]; }
+    out[0] = (uint32_t)total;
+    out[1] = 0;
+  }
+  __syncthreads();
+  for (int s = t; s < b; s += T) order[atomicAdd(&cur[nb[s]], 1)] = s;
+  __syncthreads();
+  const int total = (int)out[0];
+  for (int p = t; p < total; p += T) {
+    int lo = 0, hi = nmb - 1;      // smallest mb with off[mb] <= p (off falls as mb grows)
+    while (lo < hi) {
+      const int mid = (lo + hi) >> 1;
+      if (off[mid] <= p) hi = mid; else lo = mid + 1;
+    }
+    const int mb = lo, r = p - off[mb], rank = r / h, head = r - rank * h;
+    const int s = order[rank];
+    out[2 + 2 * p] = (uint32_t)s | ((uint32_t)head << 16);
+    out[3 + 2 * p] = (uint32_t)(head / g) | ((uint32_t)mb << 16);
+  }
+}
 
 }  // namespace
 
@@ -140,6 +197,7 @@ bool launch_fwd_asm(const FwdParams& p, bool is_bf16, hipStream_t stream) {
   if (nwg > 0x7fffffff) return false;
   hipFunction_t fn;
   uint32_t* table;
+  int cus = 0;
   {
     std::lock_guard<std::mutex> lk(g_mu);
     DevModule& m = module_for(dev);
@@ -154,6 +212,29 @@ bool launch_fwd_asm(const FwdParams& p, bool is_bf16, hipStream_t stream) {
       it = m.tables.emplace(key, d).first;
     }
     table = it->second;
+    cus = m.cus;
+  }
+  // Persistent grid (knob 5, default on): one workgroup per CU (the kernel's 160 KiB of LDS allows
+  // one), each walking the heaviest-first item list in snake order, so the rounds pair heavy and
+  // light causal blocks and every item after the first starts with its K/V tiles and Q already
+  // issued by its predecessor.  Varlen tables hold empty items (blocks past a sequence) and the
+  // XCD-grouped order is built for one item per workgroup: those keep G = items.
+  long long grid = nwg;
+  const bool persist = knob(kKnobFwdPersist) != 0 && p.head_group == 0 && cus > 0;
+  uint32_t* vtab = nullptr;   // device-built varlen work list (stream-ordered allocation)
+  if (persist && s.cu_seqlens_q != nullptr) {
+    if (s.b <= kVarlenMaxSeqs && p.num_m_blocks <= kVarlenMaxBlocks) {
+      check(hipMallocAsync(reinterpret_cast<void**>(&vtab), (size_t)(2 * nwg + 2) * sizeof(uint32_t), stream),
+            "hipMallocAsync (varlen work list)");
+      const size_t shm = (size_t)(2 * s.b + 3 * (p.num_m_blocks + 1)) * sizeof(int);
+      hipLaunchKernelGGL(varlen_items_kernel, dim3(1), dim3(1024), shm, stream, s.cu_seqlens_q, s.b, s.h,
+                         s.h / s.hk, p.num_m_blocks, vtab);
+      check(hipGetLastError(), "varlen_items_kernel");
+      table = vtab;
+      if (nwg > cus) grid = cus;
+    }
+  } else if (persist && nwg > cus) {
+    grid = cus;
   }
   FwdAsmArgs a;
   std::memset(&a, 0, sizeof(a));
@@ -166,10 +247,13 @@ bool launch_fwd_asm(const FwdParams& p, bool is_bf16, hipStream_t stream) {
   a.q_head = (int32_t)q_head; a.k_head = (int32_t)k_head; a.v_head = (int32_t)v_head; a.o_head = (int32_t)o_head;
   a.sq = s.seqlen_q; a.sk = s.seqlen_k; a.lse_pitch = s.lse_pitch; a.h = s.h;
   a.c = s.scale_log2;
-  a.flags = s.varlen_padded_input ? 1 : 0;
+  a.flags = (s.varlen_padded_input ? 1 : 0) | (vtab != nullptr ? 2 : 0);
+  a.n_items = (int32_t)nwg;
+  a.grid = (int32_t)grid;
   size_t sz = sizeof(a);
   void* cfg[] = {HIP_LAUNCH_PARAM_BUFFER_POINTER, &a, HIP_LAUNCH_PARAM_BUFFER_SIZE, &sz, HIP_LAUNCH_PARAM_END};
-  check(hipModuleLaunchKernel(fn, (unsigned)nwg, 1, 1, 256, 1, 1, 0, stream, nullptr, cfg), "hipModuleLaunchKernel");
+  check(hipModuleLaunchKernel(fn, (unsigned)grid, 1, 1, 256, 1, 1, 0, stream, nullptr, cfg), "hipModuleLaunchKernel");
+  if (vtab != nullptr) check(hipFreeAsync(vtab, stream), "hipFreeAsync (varlen work list)");
   return true;
 }
 

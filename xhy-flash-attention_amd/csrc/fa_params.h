@@ -168,7 +168,9 @@ enum Knob { kKnobNoSplitKv = 0 /* FLASH_ATTN_MI355X_NO_SPLITKV: 1 = never split 
             kKnobXcdGroupMinMiB = 2 /* FLASH_ATTN_MI355X_XCD_GROUP_MIN_MIB: grouping threshold */,
             kKnobBwdAsm = 3 /* FLASH_ATTN_MI355X_BWD_ASM: 0 = HIP dK/dV kernel for every call */,
             kKnobDqAsm = 4 /* FLASH_ATTN_MI355X_DQ_ASM: 0 = HIP dQ kernel for every call */,
-            kNumKnobs = 5 };
+            kKnobFwdPersist = 5 /* FLASH_ATTN_MI355X_FWD_PERSIST: 0 = assembly forward with one
+                                   workgroup per item, 1 = one persistent workgroup per CU */,
+            kNumKnobs = 6 };
 int knob(int id);
 void set_knob(int id, int value);
 
