@@ -34,9 +34,10 @@ def asm_text():
     (2, 130, 77, 1, 1, False, True, None),      # ragged non-causal, nblk = 2
     (1, 520, 520, 1, 1, True, True, 400),       # forced refits (late score jump)
 ])
-def test_asm_forward_in_emulator(asm_text, b, sq, sk, h, hk, causal, bf16, big):
+@pytest.mark.parametrize("d", [128, 64])
+def test_asm_forward_in_emulator(asm_text, b, sq, sk, h, hk, causal, bf16, big, d):
     eo, el, o, o_ref, lse, lse_ref = emu_fwd.run(b, sq, sk, h, hk, causal, bf16, seed=0, big=big,
-                                                  text=asm_text, verbose=False)
+                                                  text=asm_text, verbose=False, d=d)
     # output rounding of bf16 / fp16 (|O| <= ~4) and fp32 LSE arithmetic
     assert eo <= (1.6e-2 if bf16 else 2e-3), eo
     assert el <= 1e-5, el
@@ -49,11 +50,12 @@ def test_asm_forward_in_emulator(asm_text, b, sq, sk, h, hk, causal, bf16, big):
     (2, 130, 77, 3, 1, False, True, 2),      # 2-tile items: every successor starts cold
     (1, 300, 700, 2, 1, True, False, 1),     # fp16, sq < sk, mixed warm / cold
 ])
-def test_asm_forward_persistent_loop(asm_text, b, sq, sk, h, hk, causal, bf16, grid):
+@pytest.mark.parametrize("d", [128, 64])
+def test_asm_forward_persistent_loop(asm_text, b, sq, sk, h, hk, causal, bf16, grid, d):
     """the persistent item loop (fa_fwd_asm.cpp, knob 5): fewer workgroups than items; each item's
     K/V tiles run on from its predecessor's DMA stream (switch block) when it has >= 4 tiles"""
     eo, el, o, o_ref, lse, lse_ref = emu_fwd.run(b, sq, sk, h, hk, causal, bf16, seed=1, text=asm_text,
-                                                  verbose=False, grid=grid)
+                                                  verbose=False, grid=grid, d=d)
     assert eo <= (1.6e-2 if bf16 else 2e-3), eo
     assert el <= 1e-5, el
 
@@ -107,8 +109,9 @@ def test_generated_kernels_are_hazard_free():
 
     text = subprocess.run([sys.executable, os.path.join(ROOT, "xhy-flash-attention_amd", "csrc", "asm", "gen_fwd.py")],
                           check=True, capture_output=True, text=True).stdout
-    assert text.count(".amdhsa_kernel ") == 4
-    assert ".amdhsa_group_segment_fixed_size 163840" in text
+    assert text.count(".amdhsa_kernel ") == 8
+    assert text.count(".amdhsa_group_segment_fixed_size 163840") == 4     # d = 128: 5-deep K/V rings
+    assert text.count(".amdhsa_group_segment_fixed_size 81920") == 4      # d = 64
     # no instruction reads M0 as an LDS-DMA destination within 0 wait states of its write
     lines = [x.strip() for x in text.splitlines()]
     for i, x in enumerate(lines):

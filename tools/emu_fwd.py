@@ -72,8 +72,9 @@ def reference(q, k, v, causal, scale, seqs_q=None, seqs_k=None):
 
 
 def run(b=1, sq=300, sk=300, h=2, hk=1, causal=True, bf16=True, seed=0, big=None, text=None, verbose=True,
-        grid=None):
-    """grid: workgroups of the persistent item loop (default: one per item)"""
+        grid=None, d=128):
+    """grid: workgroups of the persistent item loop (default: one per item); d: head dim (128, 64)"""
+    D = d
     rng = np.random.default_rng(seed)
     q = rng.standard_normal((b, sq, h, D)).astype(np.float32)
     k = rng.standard_normal((b, sk, hk, D)).astype(np.float32)
@@ -100,7 +101,7 @@ def run(b=1, sq=300, sk=300, h=2, hk=1, causal=True, bf16=True, seed=0, big=None
               n_items=len(tab), grid=grid or len(tab))
     akarg = heap.put(np.frombuffer(pack_args(**kw), dtype=np.uint8))
     text = text or asm_text()
-    name = f"fa_fwd_asm_d128_{'bf16' if bf16 else 'f16'}_{'causal' if causal else 'full'}"
+    name = f"fa_fwd_asm_d{D}_{'bf16' if bf16 else 'f16'}_{'causal' if causal else 'full'}"
     emu = Emu(text, name, heap)
     for L in range(grid or len(tab)):
         emu.run_wg(L, akarg)
@@ -127,5 +128,6 @@ if __name__ == "__main__":
     ap.add_argument("--big", type=int, default=None)
     ap.add_argument("--seed", type=int, default=0)
     ap.add_argument("--grid", type=int, default=None)
+    ap.add_argument("--d", type=int, default=128)
     a = ap.parse_args()
-    run(a.b, a.sq, a.sk, a.h, a.hk, not a.full, not a.fp16, a.seed, a.big, grid=a.grid)
+    run(a.b, a.sq, a.sk, a.h, a.hk, not a.full, not a.fp16, a.seed, a.big, grid=a.grid, d=a.d)

@@ -43,28 +43,39 @@ from isa import (ACCR, ACCW, BARRIER, BRANCH, DMA, LABEL, LDS, MFMA, NOP, PERM, 
                  TRANS, VALU, VLOAD, VSTORE, WAIT, Counters, Inst, add_waits, ar, fix_hazards, label, nop,
                  rtxt, schedule, sr, vr)
 
-D = 128
-KS = D // 16          # QK^T k-steps
-NP = D // 32          # d tiles of O
 BN = 64               # keys per K/V tile
 BM = 256              # query rows per workgroup
-TILE = BN * D * 2     # bytes per K (or V) tile
 NSLOT = 5
-VBASE = NSLOT * TILE
-LDS_BYTES = 2 * NSLOT * TILE
-assert LDS_BYTES <= 163840
+
+
+def configure(d):
+    """head dim of the kernels generated next (128 or 64): K/V tiles of 64 keys x d, D / 32 column
+    blocks of 64 bytes per key row (one DMA piece each), AGPR layout O | Q | K ring | V ring"""
+    global D, KS, NP, TILE, VBASE, LDS_BYTES, QB, KF, VF, NX, NY
+    D = d
+    KS = D // 16          # QK^T k-steps
+    NP = D // 32          # d tiles of O = column blocks of a K/V tile
+    TILE = BN * D * 2     # bytes per K (or V) tile
+    VBASE = NSLOT * TILE
+    LDS_BYTES = 2 * NSLOT * TILE
+    assert LDS_BYTES <= 163840
+    QB = 2 * NP * 16
+    KF = QB + 2 * KS * 4
+    VF = KF + 32
+    NX = 2 * KS * 2       # phase X MFMAs: S(n+1) of 2 q-blocks, 2 key subtiles
+    NY = NP * 8           # phase Y MFMAs: PV(n) of 2 q-blocks
+
+
+configure(128)
+
 
 # ---- AGPRs ----
 def O_(j, dt):
-    return 64 * j + 16 * dt
+    return 2 * NP * 8 * j + 16 * dt
 
 
 def Q_(j, ks):
-    return 128 + 32 * j + 4 * ks
-
-
-KF = 192
-VF = 224
+    return QB + KS * 4 * j + 4 * ks
 
 # ---- VGPRs ----
 SA = 0
@@ -169,7 +180,7 @@ class K:
         return Inst(t, MFMA, rd=ar(VF + 4 * vslot, 4) + vr(preg, 4) + ar(o, 16), wr=ar(o, 16), rd_c=ar(o, 16))
 
     def kread(self, f, kslot, **kw):
-        st, ks = f // 8, f % 8
+        st, ks = f // KS, f % KS
         base = V_KB0 if ks % 2 == 0 else V_KB1
         off = (ks // 2) * BN * 64 + st * 32 * 64
         return Inst(f"ds_read_b128 {rtxt('a', KF + 4 * kslot, 4)}, v{base} offset:{off}", LDS,
@@ -255,9 +266,9 @@ class K:
         # ---------------- phase X
         mx = []
         if not last:
-            for i in range(32):
-                st, ks, j = i // 16, (i % 16) // 2, i % 2
-                f = st * 8 + ks
+            for i in range(NX):
+                st, ks, j = i // (2 * KS), (i % (2 * KS)) // 2, i % 2
+                f = st * KS + ks
                 sreg = (SA if j == 0 else SB(p ^ 1)) + 16 * st
                 mx.append(self.mfma_s(sreg, f % 8, j, ks, ks == 0))
         fx = []
@@ -267,11 +278,11 @@ class K:
         vb = fx[-2:]
         if not last:
             # K fragments 3..15 (0..2 were prefetched at the end of the previous step)
-            for f in range(3, 16):
+            for f in range(3, 2 * KS):
                 eg = max(2 * (f - 3), 2 * (f - 8) + 3)
                 fx.append(self.kread(f, f % 8, key=-100 + f, earliest=eg, deadline=2 * f - 1))
             # K DMA of tile n+4 (4 pieces)
-            for jj in range(4):
+            for jj in range(NP):
                 m = Inst(f"s_add_u32 m0, s{S_DOFF}, {jj * 4096}", SALU, rd=sr(S_DOFF), wr=[("m0", 0)], key=-60 + 4 * jj,
                          earliest=3 + 7 * jj)
                 d = Inst(f"buffer_load_dwordx4 v{V_VOFF + jj}, s[{S_KD}:{S_KD + 3}], 0 offen lds", DMA,
@@ -283,11 +294,11 @@ class K:
         # V fragments of d-tiles 0 and 1 (8 frags) for phase Y
         for f in range(8):
             for h in range(2):
-                fx.append(self.vread(f, f % 8, h, key=-80 + 2 * f + h, earliest=(14 + 2 * f) if not last else None))
+                fx.append(self.vread(f, f % 8, h, key=-80 + 2 * f + h, earliest=max(0, NX - 18 + 2 * f) if not last else None))
         xs = schedule(mx, fx) if mx else schedule([], fx)
         # ---------------- phase Y
         my = []
-        for i in range(32):
+        for i in range(NY):
             dt, w = i // 8, i % 8
             j, kk = w // 4, w % 4
             f = 4 * dt + kk
@@ -298,7 +309,7 @@ class K:
         refits.append(self.refit(1, SB(p), PB, rl_b, tile_add=0, phase="Y"))
         fy += self.guard_ops(1, rl_b, key=-200, deadline=4)
         # V fragments of d-tiles 2, 3
-        for f in range(8, 16):
+        for f in range(8, 4 * NP):
             dt, kk = f // 4, f % 4
             eg = 8 * (dt - 2) + 4 + kk + 1
             dl = 8 * dt + kk - 2
@@ -310,7 +321,7 @@ class K:
             sm_a, sum_a = self.softmax_ops(0, SA, PA(p ^ 1), masked, (S_N0, 64), key0=0)
             fy += sm_a
             # V DMA of tile n+4, then advance the DMA offsets / slot / record counts
-            for jj in range(4):
+            for jj in range(NP):
                 fy.append(Inst(f"s_add_u32 m0, s{S_DOFF}, {VBASE + jj * 4096}", SALU, rd=sr(S_DOFF), wr=[("m0", 0)],
                                key=-60 + 4 * jj, earliest=2 + 6 * jj))
                 fy.append(Inst(f"buffer_load_dwordx4 v{V_VOFF + jj}, s[{S_VD}:{S_VD + 3}], 0 offen lds", DMA,
@@ -328,7 +339,7 @@ class K:
             fy += self.dma_count_ops(self.lab(f"{tag}_sw"), key=-30)
             # K read base of tile n+2 and prefetch of its first three fragments (next phase X)
             fy += [
-                Inst(f"s_add_u32 s{S_KOFF}, s{S_KOFF}, {TILE}", SALU, rd=sr(S_KOFF), wr=sr(S_KOFF) + [("scc", 0)], key=-20, earliest=18),
+                Inst(f"s_add_u32 s{S_KOFF}, s{S_KOFF}, {TILE}", SALU, rd=sr(S_KOFF), wr=sr(S_KOFF) + [("scc", 0)], key=-20, earliest=NY - 14),
                 Inst(f"s_sub_u32 s{t + 1}, s{S_KOFF}, {NSLOT * TILE}", SALU, rd=sr(S_KOFF), wr=sr(t + 1) + [("scc", 0)], key=-20),
                 Inst(f"s_cmp_ge_u32 s{S_KOFF}, {NSLOT * TILE}", SALU, rd=sr(S_KOFF), wr=[("scc", 0)], key=-20),
                 Inst(f"s_cselect_b32 s{S_KOFF}, s{t + 1}, s{S_KOFF}", SALU, rd=sr(t + 1) + sr(S_KOFF) + [("scc", 0)], wr=sr(S_KOFF), key=-20),
@@ -336,14 +347,14 @@ class K:
                 Inst(f"v_add_u32_e32 v{V_KB1}, s{S_KOFF}, v{V_RB1}", VALU, rd=sr(S_KOFF) + vr(V_RB1), wr=vr(V_KB1), key=-20),
             ]
             for f in range(3):
-                fy.append(self.kread(f, f % 8, key=-19 + f, earliest=22 + 2 * f))
+                fy.append(self.kread(f, f % 8, key=-19 + f, earliest=NY - 10 + 2 * f))
             rl_a = self.lab(f"{tag}_refit_a")
             refits.append(self.refit(0, SA, PA(p ^ 1), rl_a, tile_add=64, phase="end"))
             # after the phase's LAST MFMA: refit_a borrows the V fragment ring as scratch and rescales
             # O_a, so no PV MFMA may still be pending (placed earlier, it corrupted the d-tile 3 MFMAs)
             ga = self.guard_ops(0, rl_a, key=700)
             for op in ga:
-                op.eg = 31
+                op.eg = NY - 1
             fy += ga
         if last:
             # Q of the next item (persistent loop): the Q registers are idle from here on (no QK MFMA
@@ -353,7 +364,7 @@ class K:
                     fy.append(Inst(f"buffer_load_dwordx4 {rtxt('a', Q_(j, ks), 4)}, v{V_QOFF[j]}, s[{S_QD2}:{S_QD2 + 3}], 0 offen offset:{32 * ks}",
                                    VLOAD, rd=vr(V_QOFF[j]) + sr(S_QD2, 4), wr=ar(Q_(j, ks), 4), key=900 + 8 * j + ks, earliest=8))
         # V read slot of the next tile
-        fy += [Inst(f"s_add_u32 s{S_VOFF}, s{S_VOFF}, {TILE}", SALU, rd=sr(S_VOFF), wr=sr(S_VOFF) + [("scc", 0)], key=800, earliest=28),
+        fy += [Inst(f"s_add_u32 s{S_VOFF}, s{S_VOFF}, {TILE}", SALU, rd=sr(S_VOFF), wr=sr(S_VOFF) + [("scc", 0)], key=800, earliest=NY - 4),
                Inst(f"s_sub_u32 s{t + 2}, s{S_VOFF}, {NSLOT * TILE}", SALU, rd=sr(S_VOFF), wr=sr(t + 2) + [("scc", 0)], key=801),
                Inst(f"s_cmp_ge_u32 s{S_VOFF}, {VBASE + NSLOT * TILE}", SALU, rd=sr(S_VOFF), wr=[("scc", 0)], key=802),
                Inst(f"s_cselect_b32 s{S_VOFF}, s{t + 2}, s{S_VOFF}", SALU, rd=sr(t + 2) + sr(S_VOFF) + [("scc", 0)], wr=sr(S_VOFF), key=803)]
@@ -363,7 +374,7 @@ class K:
             # tiles <= n+3 landed in every wave (K(n+3) is prefetched in the next step's phase Y)
             body += [Inst(f"s_add_u32 s{S_N}, s{S_N}, 1", SALU, rd=sr(S_N), wr=sr(S_N) + [("scc", 0)]),
                      Inst(f"s_add_u32 s{S_N0}, s{S_N0}, {BN}", SALU, rd=sr(S_N0), wr=sr(S_N0) + [("scc", 0)]),
-                     Inst("s_waitcnt vmcnt(8) lgkmcnt(0)", WAIT),
+                     Inst(f"s_waitcnt vmcnt({2 * NP}) lgkmcnt(0)", WAIT),
                      Inst("s_barrier", BARRIER)]
         return body, refits
 
@@ -374,7 +385,7 @@ class K:
         return label, and it carries the registers the block touches so that the scheduler keeps
         every V_VOFF update / DMA of this tile before it."""
         self.switches.append(self.switch_block(lab))
-        touched = vr(V_VOFF, 4) + sr(S_KD, 4) + sr(S_VD, 4) + sr(S_DT) + sr(S_DLIM) + sr(S_WARM)
+        touched = vr(V_VOFF, NP) + sr(S_KD, 4) + sr(S_VD, 4) + sr(S_DT) + sr(S_DLIM) + sr(S_WARM)
         return [Inst(f"s_add_u32 s{S_DT}, s{S_DT}, 1", SALU, rd=sr(S_DT), wr=sr(S_DT) + [("scc", 0)], key=key),
                 Inst(f"s_cmp_eq_u32 s{S_DT}, s{S_DLIM}", SALU, rd=sr(S_DT) + sr(S_DLIM), wr=[("scc", 0)], key=key),
                 Inst(f"s_cbranch_scc1 {lab}\n{lab}_back:", BRANCH, rd=[("scc", 0)] + touched, wr=touched, key=key)]
@@ -392,7 +403,7 @@ class K:
         ins += [I(f"s_mov_b32 s{S_KD + i}, s{S_KD2 + i}", SALU) for i in range(4)]
         ins += [I(f"s_mov_b32 s{S_VD + i}, s{S_VD2 + i}", SALU) for i in range(4)]
         ins += [I(f"s_mul_i32 s{S_SWT}, s{S_DT}, s{S_TB}", SALU)]
-        ins += [I(f"v_subrev_u32_e32 v{V_VOFF + jj}, s{S_SWT}, v{V_VOFF + jj}", VALU) for jj in range(4)]
+        ins += [I(f"v_subrev_u32_e32 v{V_VOFF + jj}, s{S_SWT}, v{V_VOFF + jj}", VALU) for jj in range(NP)]
         ins += [I(f"s_mov_b32 s{S_DT}, 0", SALU), I(f"s_mov_b32 s{S_DLIM}, s{S_NXN}", SALU),
                 I(f"s_mov_b32 s{S_WARM}, 1", SALU), nop(4), I(f"s_branch {lab}_back", BRANCH),
                 label(lz),
@@ -405,15 +416,15 @@ class K:
         (prologue use: not scheduled)"""
         I = Inst
         ins = []
-        for jj in range(4):
+        for jj in range(NP):
             ins += [I(f"s_add_u32 m0, s{S_DOFF}, {jj * 4096}", SALU, rd=sr(S_DOFF), wr=[("m0", 0)]),
                     I(f"buffer_load_dwordx4 v{V_VOFF + jj}, s[{S_KD}:{S_KD + 3}], 0 offen lds", DMA,
                       rd=vr(V_VOFF + jj) + sr(S_KD, 4) + [("m0", 0)])]
-        for jj in range(4):
+        for jj in range(NP):
             ins += [I(f"s_add_u32 m0, s{S_DOFF}, {VBASE + jj * 4096}", SALU, rd=sr(S_DOFF), wr=[("m0", 0)]),
                     I(f"buffer_load_dwordx4 v{V_VOFF + jj}, s[{S_VD}:{S_VD + 3}], 0 offen lds", DMA,
                       rd=vr(V_VOFF + jj) + sr(S_VD, 4) + [("m0", 0)])]
-        for jj in range(4):
+        for jj in range(NP):
             ins.append(I(f"v_add_u32_e32 v{V_VOFF + jj}, s{S_TB}, v{V_VOFF + jj}", VALU, rd=sr(S_TB) + vr(V_VOFF + jj), wr=vr(V_VOFF + jj)))
         ins += [I(f"s_add_u32 s{S_DOFF}, s{S_DOFF}, {TILE}", SALU, rd=sr(S_DOFF), wr=sr(S_DOFF)),
                 I(f"s_sub_u32 s{S_SWT}, s{S_DOFF}, {NSLOT * TILE}", SALU, rd=sr(S_DOFF), wr=sr(S_SWT)),
@@ -643,7 +654,7 @@ class K:
                 I("v_xor_b32_e32 v5, v5, v6", VALU, rd=vr(5) + vr(6), wr=vr(5)),                   # chunk
                 I(f"v_mul_lo_u32 v4, v4, s{Rkv}", VALU, rd=vr(4) + sr(Rkv), wr=vr(4)),
                 I(f"v_lshl_add_u32 v{V_VOFF}, v5, 4, v4", VALU, rd=vr(5) + vr(4), wr=vr(V_VOFF))]
-        for jj in range(1, 4):
+        for jj in range(1, NP):
             ins.append(I(f"v_add_u32_e32 v{V_VOFF + jj}, {64 * jj}, v{V_VOFF}", VALU, rd=vr(V_VOFF), wr=vr(V_VOFF + jj)))
         ins += [I(f"v_mov_b32_e32 v{V_NINF}, 0xff800000", VALU, wr=vr(V_NINF)),
                 I(f"s_lshl_b32 s{S_TB}, s{Rkv}, 6", SALU, rd=sr(Rkv), wr=sr(S_TB)),
@@ -833,7 +844,7 @@ class K:
         ins += self.item_geom("cold", l_skip)
         # DMA offsets back to tile 0 of the fresh descriptors
         ins += [I(f"s_mul_i32 s{S_SWT}, s{S_DT}, s{S_TB}", SALU)]
-        ins += [I(f"v_subrev_u32_e32 v{V_VOFF + jj}, s{S_SWT}, v{V_VOFF + jj}", VALU) for jj in range(4)]
+        ins += [I(f"v_subrev_u32_e32 v{V_VOFF + jj}, s{S_SWT}, v{V_VOFF + jj}", VALU) for jj in range(NP)]
         ins += [I(f"s_mov_b32 s{S_DT}, 0", SALU), I(f"s_mov_b32 s{S_DLIM}, s{S_NBLK}", SALU)]
         # Q fragments into the accumulator file: lane holds Q[row][16 ks + 8 hh .. +7]
         for j in range(2):
@@ -869,7 +880,7 @@ class K:
         I = Inst
         ins = [I(f"s_mov_b32 s{S_N}, 0", SALU, wr=sr(S_N)),
                I(f"s_mov_b32 s{S_N0}, 0", SALU, wr=sr(S_N0))]
-        ins += [I(f"v_accvgpr_write_b32 a{i}, 0", ACCW, wr=ar(i)) for i in range(128)]
+        ins += [I(f"v_accvgpr_write_b32 a{i}, 0", ACCW, wr=ar(i)) for i in range(2 * NP * 16)]
         ins += [I(f"v_mov_b32_e32 v{V_L[0]}, 0", VALU, wr=vr(V_L[0])),
                 I(f"v_mov_b32_e32 v{V_L[1]}, 0", VALU, wr=vr(V_L[1])),
                 I(f"v_mov_b32_e32 v{V_NEGMC[0]}, 0", VALU, wr=vr(V_NEGMC[0])),
@@ -880,18 +891,18 @@ class K:
         """Q + tiles 0, 1, 2 landed (tile 3 in flight); tile 0: S(0, a), S(0, b) -> masked, explicit
         row max, P(0, a); then into the step loop"""
         I = Inst
-        ins = [I("s_waitcnt vmcnt(8)", WAIT), I("s_barrier", BARRIER)]
+        ins = [I(f"s_waitcnt vmcnt({2 * NP})", WAIT), I("s_barrier", BARRIER)]
         ins += self.dump("pro_lds")
         ins += [I(f"v_add_u32_e32 v{V_KB0}, s{S_KOFF}, v{V_RB0}", VALU, rd=sr(S_KOFF) + vr(V_RB0), wr=vr(V_KB0)),
                 I(f"v_add_u32_e32 v{V_KB1}, s{S_KOFF}, v{V_RB1}", VALU, rd=sr(S_KOFF) + vr(V_RB1), wr=vr(V_KB1))]
         mfm = []
-        for i in range(32):
-            st, ks, j = i // 16, (i % 16) // 2, i % 2
-            f = st * 8 + ks
+        for i in range(NX):
+            st, ks, j = i // (2 * KS), (i % (2 * KS)) // 2, i % 2
+            f = st * KS + ks
             sreg = (SA if j == 0 else SB(0)) + 16 * st
             mfm.append(self.mfma_s(sreg, f % 8, j, ks, ks == 0))
         reads = []
-        for f in range(16):
+        for f in range(2 * KS):
             reads.append(self.kread(f, f % 8, key=f, earliest=max(2 * (f - 3), 2 * (f - 8) + 3) if f >= 3 else None,
                                     deadline=2 * f - 1 if f >= 3 else 0))
         body = schedule(mfm, reads)
@@ -1100,14 +1111,16 @@ class K:
 
 
 def main():
-    kernels = [K(bf, ca) for bf in (True, False) for ca in (True, False)]
     out = ['\t.amdgcn_target "amdgcn-amd-amdhsa--gfx950"', "\t.amdhsa_code_object_version 5", "\t.text"]
-    for k in kernels:
-        out.append(k.render())
-        out.append(k.descriptor())
+    meta = []
+    for d in (128, 64):
+        configure(d)
+        for k in [K(bf, ca) for bf in (True, False) for ca in (True, False)]:
+            out.append(k.render())
+            out.append(k.descriptor())
+            meta.append(k.metadata().rstrip("\n"))
     out.append("\t.amdgpu_metadata\n---\namdhsa.kernels:")
-    for k in kernels:
-        out.append(k.metadata().rstrip("\n"))
+    out += meta
     out.append("amdhsa.target: amdgcn-amd-amdhsa--gfx950\namdhsa.version:\n  - 1\n  - 2\n...\n\t.end_amdgpu_metadata")
     sys.stdout.write("\n".join(out) + "\n")
 

@@ -638,7 +638,7 @@ template <bool BF16, int D, bool CAUSAL, bool DROPOUT>
 static void run_fwd(const FwdParams& p, hipStream_t stream) {
   dim3 grid(p.s.b * p.s.h * p.num_m_blocks);   // 1-D: heads fastest, heaviest query block first
   prof_begin(kTimeFwd, stream);
-  if constexpr (!DROPOUT && D == 128) {   // hand-scheduled assembly kernel (fa_fwd_asm.cpp)
+  if constexpr (!DROPOUT && (D == 128 || D == 64)) {   // hand-scheduled assembly kernels (fa_fwd_asm.cpp)
     if (launch_fwd_asm(p, BF16, stream)) {
       prof_end(kTimeFwd, stream);
       return;

@@ -1,8 +1,9 @@
 // Host side of the hand-scheduled assembly forward (csrc/asm/gen_fwd.py -> fa_fwd_asm.s, assembled
 // for gfx950 and embedded in this library as a code object).
 //
-// The kernel covers the headline path: head dim 128, bf16 / fp16, causal or not, fixed length or
-// varlen (cu_seqlens, varlen_padded_input), GQA, no dropout / mask / return_softmax / split-KV.
+// The kernels cover the headline path: head dim 128 (and 64: C2), bf16 / fp16, causal or not, fixed
+// length or varlen (cu_seqlens, varlen_padded_input), GQA, no dropout / mask / return_softmax /
+// split-KV.
 // Everything else -- and this path when it is switched off -- goes to fwd_kernel (fa_fwd.hip).
 //
 // Loading: the embedded code object is loaded with hipModuleLoadData once per device (first call),
@@ -51,7 +52,7 @@ static_assert(sizeof(FwdAsmArgs) == 184, "FwdAsmArgs layout");
 constexpr int kMaxDev = 64;
 struct DevModule {
   hipModule_t mod = nullptr;
-  hipFunction_t fn[4] = {};   // [bf16 causal, bf16 full, f16 causal, f16 full]
+  hipFunction_t fn[8] = {};   // d 128 then d 64: [bf16 causal, bf16 full, f16 causal, f16 full]
   int cus = 0;
   std::map<std::tuple<int, int, int, int, int>, uint32_t*> tables;
 };
@@ -59,8 +60,10 @@ std::mutex g_mu;
 DevModule g_dev[kMaxDev];
 int g_enabled = -1;   // -1: not read yet
 
-const char* kNames[4] = {"fa_fwd_asm_d128_bf16_causal", "fa_fwd_asm_d128_bf16_full",
-                         "fa_fwd_asm_d128_f16_causal", "fa_fwd_asm_d128_f16_full"};
+const char* kNames[8] = {"fa_fwd_asm_d128_bf16_causal", "fa_fwd_asm_d128_bf16_full",
+                         "fa_fwd_asm_d128_f16_causal", "fa_fwd_asm_d128_f16_full",
+                         "fa_fwd_asm_d64_bf16_causal", "fa_fwd_asm_d64_bf16_full",
+                         "fa_fwd_asm_d64_f16_causal", "fa_fwd_asm_d64_f16_full"};
 
 void check(hipError_t e, const char* what) {
   if (e != hipSuccess) throw std::runtime_error(std::string("flash_attn_fwd (asm path): ") + what + ": " + hipGetErrorString(e));
@@ -71,7 +74,7 @@ DevModule& module_for(int dev) {
   DevModule& m = g_dev[dev];
   if (m.mod == nullptr) {
     check(hipModuleLoadData(&m.mod, fa_fwd_asm_co), "hipModuleLoadData");
-    for (int i = 0; i < 4; ++i) check(hipModuleGetFunction(&m.fn[i], m.mod, kNames[i]), kNames[i]);
+    for (int i = 0; i < 8; ++i) check(hipModuleGetFunction(&m.fn[i], m.mod, kNames[i]), kNames[i]);
     check(hipDeviceGetAttribute(&m.cus, hipDeviceAttributeMultiprocessorCount, dev), "hipDeviceGetAttribute");
   }
   return m;
@@ -177,7 +180,7 @@ bool launch_fwd_asm(const FwdParams& p, bool is_bf16, hipStream_t stream) {
     }
     if (!g_enabled) return false;
   }
-  if (s.d != 128 || s.dropout || s.mask != nullptr || s.fm_lts != nullptr || p.p_out != nullptr ||
+  if ((s.d != 128 && s.d != 64) || s.dropout || s.mask != nullptr || s.fm_lts != nullptr || p.p_out != nullptr ||
       p.n_split != 0 || p.pack_g != 1)
     return false;
   if (p.k_row != p.v_row) return false;   // the K and V DMA share per-lane offsets
@@ -201,7 +204,7 @@ bool launch_fwd_asm(const FwdParams& p, bool is_bf16, hipStream_t stream) {
   {
     std::lock_guard<std::mutex> lk(g_mu);
     DevModule& m = module_for(dev);
-    fn = m.fn[(is_bf16 ? 0 : 2) + (s.causal ? 0 : 1)];
+    fn = m.fn[(s.d == 64 ? 4 : 0) + (is_bf16 ? 0 : 2) + (s.causal ? 0 : 1)];
     auto key = std::make_tuple(s.b, s.h, s.hk, p.num_m_blocks, p.head_group);
     auto it = m.tables.find(key);
     if (it == m.tables.end()) {
