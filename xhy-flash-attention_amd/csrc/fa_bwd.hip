@@ -119,38 +119,55 @@ __device__ inline int dma_voff(int pc, int lane, int64_t row_stride, int dlim) {
 // ------------------------------------------------------------------------------------------------
 template <bool BF16>
 __global__ void __launch_bounds__(256) bwd_pre_kernel(const BwdParams p) {
+  // HBM-bound (reads O and dO once): each 16-lane group handles kPreRows rows 16 apart, all their
+  // loads issued before any arithmetic, so a lane keeps 2 kPreRows 16-byte loads in flight
+  constexpr int kPreRows = 4;
   using E = Elt<BF16>;
   const AttnShape s = p.s;
   const int bh = blockIdx.x;
   const int bidb = bh / s.h, head = bh - bidb * s.h;
   const SeqGeom g = seq_geom(p, bidb);
-  const int row = blockIdx.y * 16 + (threadIdx.x >> 4);
   const int l16 = threadIdx.x & 15;
-  if (row >= g.sq) {
-    // assembly dK / dV path: the rows of the last 32-row group past seqlen_q read zero chain starts
-    if (p.lsed != nullptr && l16 == 0 && row < ((g.sq + 31) & ~31)) {
-      float* grp = p.lsed + (((int64_t)bidb * s.h + head) * p.lsed_ng + (row >> 5)) * 64 + (row & 31);
-      grp[0] = 0.f;
-      grp[32] = 0.f;
-    }
-    return;
-  }
-  const u16* O = (const u16*)p.o + g.o_off + (int64_t)head * p.o_head + (int64_t)row * p.o_row;
-  const u16* dO = (const u16*)p.dout + g.do_off + (int64_t)head * p.do_head + (int64_t)row * p.do_row;
-  float acc = 0.f;
-  for (int c = l16; c < s.d / 8; c += 16) {
-    const u32x4_t a = *(const u32x4_t*)(O + 8 * c);
-    const u32x4_t b = *(const u32x4_t*)(dO + 8 * c);
+  const int nch = s.d / 8;   // 16-byte chunks per row (<= 32)
+  u32x4_t a[kPreRows][2], b[kPreRows][2];
 #pragma unroll
-    for (int w = 0; w < 4; ++w) {
-      acc += E::to_f32(a[w] & 0xffff) * E::to_f32(b[w] & 0xffff);
-      acc += E::to_f32(a[w] >> 16) * E::to_f32(b[w] >> 16);
+  for (int r = 0; r < kPreRows; ++r) {
+    const int row = blockIdx.y * (16 * kPreRows) + r * 16 + (threadIdx.x >> 4);
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      const int c = l16 + 16 * u;
+      a[r][u] = b[r][u] = u32x4_t{0, 0, 0, 0};
+      if (row < g.sq && c < nch) {
+        a[r][u] = *(const u32x4_t*)((const u16*)p.o + g.o_off + (int64_t)head * p.o_head + (int64_t)row * p.o_row + 8 * c);
+        b[r][u] = *(const u32x4_t*)((const u16*)p.dout + g.do_off + (int64_t)head * p.do_head + (int64_t)row * p.do_row + 8 * c);
+      }
     }
   }
+  const int64_t bhi = (int64_t)bidb * s.h + head;
 #pragma unroll
-  for (int m = 8; m >= 1; m >>= 1) acc += __shfl_xor(acc, m, 16);
-  if (l16 == 0) {
-    const int64_t bhi = (int64_t)bidb * s.h + head;
+  for (int r = 0; r < kPreRows; ++r) {
+    const int row = blockIdx.y * (16 * kPreRows) + r * 16 + (threadIdx.x >> 4);
+    float acc = 0.f;
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+#pragma unroll
+      for (int w = 0; w < 4; ++w) {
+        acc += E::to_f32(a[r][u][w] & 0xffff) * E::to_f32(b[r][u][w] & 0xffff);
+        acc += E::to_f32(a[r][u][w] >> 16) * E::to_f32(b[r][u][w] >> 16);
+      }
+    }
+#pragma unroll
+    for (int m = 8; m >= 1; m >>= 1) acc += __shfl_xor(acc, m, 16);
+    if (l16 != 0) continue;
+    if (row >= g.sq) {
+      // assembly dK / dV path: the rows of the last 32-row group past seqlen_q read zero chain starts
+      if (p.lsed != nullptr && row < ((g.sq + 31) & ~31)) {
+        float* grp = p.lsed + (bhi * p.lsed_ng + (row >> 5)) * 64 + (row & 31);
+        grp[0] = 0.f;
+        grp[32] = 0.f;
+      }
+      continue;
+    }
     // with dropout the reference keeps D scaled down by the keep probability (flash_bwd_kernel.h:178-182)
     const float dv = s.dropout ? acc * s.p_keep : acc;
     p.dsum[bhi * p.seqlen_q_rounded + row] = dv;
@@ -1145,7 +1162,7 @@ static void launch_bwd_t(const BwdParams& p, hipStream_t stream) {
   {
     // (assembly dK / dV: also the zero rows up to the last 32-row group)
     const int rows = p.lsed != nullptr ? 32 * p.lsed_ng : p.s.seqlen_q;
-    dim3 grid(p.s.b * p.s.h, (rows + 15) / 16);
+    dim3 grid(p.s.b * p.s.h, (rows + 63) / 64);   // 64 rows per block (bwd_pre_kernel kPreRows)
     prof_begin(kTimeBwdPre, stream);
     hipLaunchKernelGGL((bwd_pre_kernel<BF16>), grid, dim3(256), 0, stream, p);
     prof_end(kTimeBwdPre, stream);
