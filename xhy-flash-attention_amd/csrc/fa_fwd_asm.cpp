@@ -110,28 +110,32 @@ std::vector<uint32_t> build_table(int b, int h, int hk, int nmb, int hp) {
 
 bool fits32(int64_t x) { return x >= 0 && x < (1ll << 31); }
 
-// Varlen work list, built on the device (the host cannot list the items without reading
-// cu_seqlens back): the (sequence, query block, head) items that hold rows, heaviest first --
-// query block index descending; within a level, sequences by block count descending, heads
-// fastest (as build_table's order without the empty items).  out[0] = item count, entry i at
-// out[2 + 2 i] (the kernel reads the count from the first dword, the entries 8 bytes in).
-// Shared memory: nb[b] | order[b] | start[nmb + 1] | cur[nmb + 1] | level offset[nmb].
 constexpr int kVarlenMaxSeqs = 8192, kVarlenMaxBlocks = 2048;
-__global__ void __launch_bounds__(1024) varlen_items_kernel(const int* cu_q, int b, int h, int g, int nmb,
-                                                            uint32_t* out) {
+
+// Varlen work lists, built on the device (the host cannot list the items without reading
+// cu_seqlens back): the (sequence, block, head) items that hold rows or keys, heaviest first.
+// A sequence of len rows has n = ceil(len / rows_per_block) blocks; item levels lev = n-1 .. 0 go
+// in descending order across all sequences (the forward / dQ: block = lev, whose causal work grows
+// with it; dK / dV (reverse): block = n - 1 - lev, whose causal sweep shrinks with the block index);
+// within a level, sequences by block count descending, heads fastest.  out[0] = item count,
+// entry i at out[2 + 2 i] = (seq | head << 16, head / gdiv | block << 16) -- the host tables'
+// format (the kernels read the count from the first dword, the entries 8 bytes in).
+// Shared memory: nb[b] | order[b] | start[nlev + 1] | cur[nlev + 1] | level offset[nlev].
+__global__ void __launch_bounds__(1024) varlen_items_kernel(const int* cu, int b, int nh, int gdiv, int rows,
+                                                            int nlev, int reverse, uint32_t* out) {
   extern __shared__ int sm[];
   int* nb = sm;
   int* order = nb + b;
   int* start = order + b;
-  int* cur = start + nmb + 1;
-  int* off = cur + nmb + 1;
+  int* cur = start + nlev + 1;
+  int* off = cur + nlev + 1;
   const int t = threadIdx.x, T = blockDim.x;
-  for (int i = t; i <= nmb; i += T) start[i] = 0;
+  for (int i = t; i <= nlev; i += T) start[i] = 0;
   __syncthreads();
   for (int s = t; s < b; s += T) {
-    const int len = cu_q[s + 1] - cu_q[s];
-    int n = len > 0 ? (len + 255) / 256 : 0;
-    n = n > nmb ? nmb : n;
+    const int len = cu[s + 1] - cu[s];
+    int n = len > 0 ? (len + rows - 1) / rows : 0;
+    n = n > nlev ? nlev : n;
     nb[s] = n;
     atomicAdd(&start[n], 1);
   }
@@ -140,9 +144,9 @@ __global__ void __launch_bounds__(1024) varlen_items_kernel(const int* cu_q, int
     // start[n] = first sorted position of the sequences with nb == n (larger nb first), which is
     // also #{s : nb[s] > n}: the number of sequences present at level n
     int acc = 0;
-    for (int n = nmb; n >= 0; --n) { const int c = start[n]; start[n] = acc; cur[n] = acc; acc += c; }
+    for (int n = nlev; n >= 0; --n) { const int c = start[n]; start[n] = acc; cur[n] = acc; acc += c; }
     int total = 0;
-    for (int mb = nmb - 1; mb >= 0; --mb) { off[mb] = total; total += h * start[mb]; }
+    for (int lv = nlev - 1; lv >= 0; --lv) { off[lv] = total; total += nh * start[lv]; }
     out[0] = (uint32_t)total;
     out[1] = 0;
   }
@@ -151,18 +155,36 @@ __global__ void __launch_bounds__(1024) varlen_items_kernel(const int* cu_q, int
   __syncthreads();
   const int total = (int)out[0];
   for (int p = t; p < total; p += T) {
-    int lo = 0, hi = nmb - 1;      // smallest mb with off[mb] <= p (off falls as mb grows)
+    int lo = 0, hi = nlev - 1;      // smallest level with off[level] <= p (off falls as the level grows)
     while (lo < hi) {
       const int mid = (lo + hi) >> 1;
       if (off[mid] <= p) hi = mid; else lo = mid + 1;
     }
-    const int mb = lo, r = p - off[mb], rank = r / h, head = r - rank * h;
+    const int lv = lo, r = p - off[lv], rank = r / nh, head = r - rank * nh;
     const int s = order[rank];
+    const int blk = reverse ? nb[s] - 1 - lv : lv;
     out[2 + 2 * p] = (uint32_t)s | ((uint32_t)head << 16);
-    out[3 + 2 * p] = (uint32_t)(head / g) | ((uint32_t)mb << 16);
+    out[3 + 2 * p] = (uint32_t)(head / gdiv) | ((uint32_t)blk << 16);
   }
 }
 
+}  // namespace
+
+bool varlen_items_fit(int b, int nlev) { return b <= kVarlenMaxSeqs && nlev <= kVarlenMaxBlocks; }
+
+uint32_t* build_varlen_items(const int* cu, int b, int nh, int gdiv, int rows, int nlev, bool reverse,
+                             long long max_items, hipStream_t stream) {
+  uint32_t* tab = nullptr;
+  check(hipMallocAsync(reinterpret_cast<void**>(&tab), (size_t)(2 * max_items + 2) * sizeof(uint32_t), stream),
+        "hipMallocAsync (varlen work list)");
+  const size_t shm = (size_t)(2 * b + 3 * (nlev + 1)) * sizeof(int);
+  hipLaunchKernelGGL(varlen_items_kernel, dim3(1), dim3(1024), shm, stream, cu, b, nh, gdiv, rows, nlev,
+                     reverse ? 1 : 0, tab);
+  check(hipGetLastError(), "varlen_items_kernel");
+  return tab;
+}
+
+namespace {
 }  // namespace
 
 void fwd_asm_enable(int on) {
@@ -226,13 +248,8 @@ bool launch_fwd_asm(const FwdParams& p, bool is_bf16, hipStream_t stream) {
   const bool persist = knob(kKnobFwdPersist) != 0 && p.head_group == 0 && cus > 0;
   uint32_t* vtab = nullptr;   // device-built varlen work list (stream-ordered allocation)
   if (persist && s.cu_seqlens_q != nullptr) {
-    if (s.b <= kVarlenMaxSeqs && p.num_m_blocks <= kVarlenMaxBlocks) {
-      check(hipMallocAsync(reinterpret_cast<void**>(&vtab), (size_t)(2 * nwg + 2) * sizeof(uint32_t), stream),
-            "hipMallocAsync (varlen work list)");
-      const size_t shm = (size_t)(2 * s.b + 3 * (p.num_m_blocks + 1)) * sizeof(int);
-      hipLaunchKernelGGL(varlen_items_kernel, dim3(1), dim3(1024), shm, stream, s.cu_seqlens_q, s.b, s.h,
-                         s.h / s.hk, p.num_m_blocks, vtab);
-      check(hipGetLastError(), "varlen_items_kernel");
+    if (varlen_items_fit(s.b, p.num_m_blocks)) {
+      vtab = build_varlen_items(s.cu_seqlens_q, s.b, s.h, s.h / s.hk, 256, p.num_m_blocks, false, nwg, stream);
       table = vtab;
       if (nwg > cus) grid = cus;
     }

@@ -174,4 +174,10 @@ enum Knob { kKnobNoSplitKv = 0 /* FLASH_ATTN_MI355X_NO_SPLITKV: 1 = never split 
 int knob(int id);
 void set_knob(int id, int value);
 
+// Varlen work lists built on the device (fa_fwd_asm.cpp varlen_items_kernel): stream-ordered
+// allocation of 2 max_items + 2 dwords, [count, 0, entries...]; the caller frees it with hipFreeAsync.
+bool varlen_items_fit(int b, int nlev);
+uint32_t* build_varlen_items(const int* cu, int b, int nh, int gdiv, int rows, int nlev, bool reverse,
+                             long long max_items, hipStream_t stream);
+
 }  // namespace fa
