@@ -438,16 +438,6 @@ class K:
         ins += [I("v_lshrrev_b32_e32 v1, 6, v0", VALU, rd=vr(0), wr=vr(1)),
                 I(f"v_readfirstlane_b32 s{S_WAVE}, v1", RFL, rd=vr(1), wr=sr(S_WAVE)),
                 I(f"v_and_b32_e32 v{V_LANE}, 63, v0", VALU, rd=vr(0), wr=vr(V_LANE))]
-        # device-built varlen work list (flags bit 2): the item count is its first dword, the entries
-        # start 8 bytes in; workgroups past the count have no item
-        l_cnt, l_cnt_done = self.lab("cnt"), self.lab("cntdone")
-        ins += [I(f"s_bitcmp1_b32 s{FLG}, 2", SALU), I(f"s_cbranch_scc1 {l_cnt}", BRANCH),
-                I(f"s_branch {l_cnt_done}", BRANCH), label(l_cnt),
-                I(f"s_load_dword s{T0}, s[{Psch}:{Psch + 1}], 0x0", SMEM),
-                I(f"s_add_u32 s{Psch}, s{Psch}, 8", SALU), I(f"s_addc_u32 s{Psch + 1}, s{Psch + 1}, 0", SALU),
-                I("s_waitcnt lgkmcnt(0)", WAIT),
-                I(f"s_cmp_ge_u32 s2, s{T0}", SALU), I(f"s_cbranch_scc1 {self.lab_end}", BRANCH),
-                label(l_cnt_done)]
         # schedule entry: (bidb | hx << 16, kvh | kblock << 16)
         ins += [I(f"s_lshl_b32 s{T0}, s2, 3", SALU, rd=sr(2), wr=sr(T0)),
                 I(f"s_load_dwordx2 s[{T1}:{T2}], s[{Psch}:{Psch + 1}], s{T0}", SMEM, rd=sr(Psch, 2) + sr(T0), wr=sr(T1, 2)),

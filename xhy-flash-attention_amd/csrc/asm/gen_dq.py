@@ -313,16 +313,6 @@ class K:
         Rq, Rkv, Rdo, Rdq, Hq, Hk, Hv, Hdo, Hdq = (P(28 + i) for i in range(9))
         SQ, SK, LP, DPt, NH, NHK, FLG = (P(37 + i) for i in range(7))
         T = [S_TMP + i for i in range(9)]
-        # device-built varlen work list (flags bit 1): the item count is its first dword, the entries
-        # start 8 bytes in; workgroups past the count have no item
-        l_cnt, l_cnt_done = self.lab("cnt"), self.lab("cntdone")
-        ins += [I(f"s_bitcmp1_b32 s{FLG}, 1", SALU), I(f"s_cbranch_scc1 {l_cnt}", BRANCH),
-                I(f"s_branch {l_cnt_done}", BRANCH), label(l_cnt),
-                I(f"s_load_dword s{T[0]}, s[{Psch}:{Psch + 1}], 0x0", SMEM),
-                I(f"s_add_u32 s{Psch}, s{Psch}, 8", SALU), I(f"s_addc_u32 s{Psch + 1}, s{Psch + 1}, 0", SALU),
-                I("s_waitcnt lgkmcnt(0)", WAIT),
-                I(f"s_cmp_ge_u32 s2, s{T[0]}", SALU), I(f"s_cbranch_scc1 {self.lab_end}", BRANCH),
-                label(l_cnt_done)]
         ins += [I(f"s_load_dwordx2 s[{S_C}:{S_SCALE}], s[0:1], 0xb0", SMEM, rd=sr(0, 2), wr=sr(S_C, 2)),
                 I("v_lshrrev_b32_e32 v1, 6, v0", VALU, rd=vr(0), wr=vr(1)),
                 I(f"v_readfirstlane_b32 s{S_WAVE}, v1", RFL, rd=vr(1), wr=sr(S_WAVE)),

@@ -106,7 +106,9 @@ V_LANE = 188
 V_OOFF = (189, 190)
 V_ROW = (192, 193)                                       # row of the lane in the block, per q-block
 V_HH4 = 194                                              # 4 * (lane >> 5)
-NVGPR = 195
+V_TRI = 196   # 196..211: causal diagonal chain start (-inf where key > query in a 32 x 32 S^T subtile)
+V_NT = 212    # 212..227: all -inf chain start (a subtile wholly above the diagonal)
+NVGPR = 228
 
 # ---- SGPRs ----
 S_KD, S_VD, S_QD, S_OD, S_LD = 4, 8, 12, 16, 20          # buffer descriptors
@@ -136,6 +138,8 @@ S_DLIM = 60       # tiles of the item the DMA stream currently reads (S_DT count
 S_NXN = 61        # tiles of the next item (0: none / empty)
 S_KD2, S_VD2 = 92, 96
 S_SWT = 100       # switch-block temp
+S_WD = 85         # wave + m0 / 64: a diagonal tile t is visible to this wave (u = S_WD - t >= 1),
+                  # on its diagonal (u = 0) or above it (u < 0)
 S_M0R = 101       # 256 m_block of the item being set up (prologue temp)
 NSGPR = 102
 
@@ -143,6 +147,7 @@ KARG_SIZE = 184
 
 # dev A/B switches, read when the .s is generated (tools/asm_variant.sh)
 OPT_NOZERO = os.environ.get("FA_GEN_NOZERO") == "1"          # never zero K/V record counts
+OPT_NODIAG = os.environ.get("FA_GEN_NODIAG") == "1"          # causal diagonal: generic masked steps only
 OPT_ZERO_NOP = int(os.environ.get("FA_GEN_ZERO_NOP", "0"))    # s_nop 15 x N before zeroing them
 # debug: at the named point, workgroup 0 stores every register of each wave (and wave 0 the LDS) to
 # the buffer whose address is passed as the `seed` kernarg, then ends (tools/asm_dump.py)
@@ -166,12 +171,19 @@ class K:
         return f".L{self.name}_{s}_{self.uid}"
 
     # ------------------------------------------------------------------ instruction builders
-    def mfma_s(self, st_reg, kslot, j, ks, first):
-        c = "0" if first else rtxt("v", st_reg, 16)
+    def mfma_s(self, st_reg, kslot, j, ks, first, bias=None):
+        """S^T chain step; the first step starts from 0 or from a bias tile (bias: VGPR base of a
+        16-register -inf / 0 mask tile: the causal mask folded into the chain start)"""
+        if first:
+            c = "0" if bias is None else rtxt("v", bias, 16)
+            rc = [] if bias is None else vr(bias, 16)
+        else:
+            c = rtxt("v", st_reg, 16)
+            rc = vr(st_reg, 16)
         t = (f"v_mfma_f32_32x32x16_{self.ty} {rtxt('v', st_reg, 16)}, {rtxt('a', KF + 4 * kslot, 4)}, "
              f"{rtxt('a', Q_(j, ks), 4)}, {c}")
-        rd = ar(KF + 4 * kslot, 4) + ar(Q_(j, ks), 4) + ([] if first else vr(st_reg, 16))
-        return Inst(t, MFMA, rd=rd, wr=vr(st_reg, 16), rd_c=[] if first else vr(st_reg, 16))
+        rd = ar(KF + 4 * kslot, 4) + ar(Q_(j, ks), 4) + rc
+        return Inst(t, MFMA, rd=rd, wr=vr(st_reg, 16), rd_c=rc)
 
     def mfma_o(self, j, dt, vslot, preg):
         o = O_(j, dt)
@@ -259,9 +271,20 @@ class K:
     # ------------------------------------------------------------------ one pipelined step
     def step(self, p, variant, tag):
         """step n: phase X (QK(n+1) || softmax(n, b)), phase Y (PV(n) || softmax(n+1, a)).
-        variant: 'fast', 'masked' or 'last'.  Returns (instruction list, refit blocks)."""
+        variant: 'fast', 'masked' or 'last', or (causal, a full diagonal tile n+1 that is not the
+        item's last) 'diag' / 'dead': the fast step with the causal mask of S(n+1) folded into the
+        chain starts -- on this wave's diagonal the 32 x 32 subtiles (q-block j, key subtile st) are
+        the triangle (j == st), wholly visible (j > st) or wholly hidden (j < st); above it, all
+        hidden.  Returns (instruction list, refit blocks)."""
         last = variant == "last"
-        masked = variant != "fast"
+        masked = variant in ("masked", "last")
+
+        def bias(j, st):
+            if variant == "dead":
+                return V_NT
+            if variant == "diag":
+                return V_TRI if j == st else (None if j > st else V_NT)
+            return None
         refits = []
         # ---------------- phase X
         mx = []
@@ -270,7 +293,7 @@ class K:
                 st, ks, j = i // (2 * KS), (i % (2 * KS)) // 2, i % 2
                 f = st * KS + ks
                 sreg = (SA if j == 0 else SB(p ^ 1)) + 16 * st
-                mx.append(self.mfma_s(sreg, f % 8, j, ks, ks == 0))
+                mx.append(self.mfma_s(sreg, f % 8, j, ks, ks == 0, bias=bias(j, st)))
         fx = []
         # V base of tile n (slot offset S_VOFF, already advanced at the end of the previous step)
         fx.append(Inst(f"v_add_u32_e32 v{V_VB0}, s{S_VOFF}, v{V_TB0}", VALU, rd=sr(S_VOFF) + vr(V_TB0), wr=vr(V_VB0), key=0))
@@ -656,8 +679,18 @@ class K:
                 I(f"v_lshl_add_u32 v{V_VOFF}, v5, 4, v4", VALU, rd=vr(5) + vr(4), wr=vr(V_VOFF))]
         for jj in range(1, NP):
             ins.append(I(f"v_add_u32_e32 v{V_VOFF + jj}, {64 * jj}, v{V_VOFF}", VALU, rd=vr(V_VOFF), wr=vr(V_VOFF + jj)))
-        ins += [I(f"v_mov_b32_e32 v{V_NINF}, 0xff800000", VALU, wr=vr(V_NINF)),
-                I(f"s_lshl_b32 s{S_TB}, s{Rkv}, 6", SALU, rd=sr(Rkv), wr=sr(S_TB)),
+        ins += [I(f"v_mov_b32_e32 v{V_NINF}, 0xff800000", VALU, wr=vr(V_NINF))]
+        if self.causal:
+            # diagonal mask tiles: element g of a lane holds key (g & 3) + 8 (g >> 2) + 4 hh of the
+            # subtile, query r = lane & 31 (v2)
+            for g in range(16):
+                kr = (g & 3) + 8 * (g >> 2)
+                ins += [I(f"v_add_u32_e32 v4, {kr}, v{V_HH4}", VALU, rd=vr(V_HH4), wr=vr(4)),
+                        I("v_cmp_gt_u32_e32 vcc, v4, v2", VALU, rd=vr(4) + vr(2), wr=[("vcc", 0)]),
+                        I(f"v_cndmask_b32_e64 v{V_TRI + g}, 0, v{V_NINF}, vcc", VALU,
+                          rd=vr(V_NINF) + [("vcc", 0)], wr=vr(V_TRI + g)),
+                        I(f"v_mov_b32_e32 v{V_NT + g}, v{V_NINF}", VALU, rd=vr(V_NINF), wr=vr(V_NT + g))]
+        ins += [I(f"s_lshl_b32 s{S_TB}, s{Rkv}, 6", SALU, rd=sr(Rkv), wr=sr(S_TB)),
                 I(f"s_mov_b32 s{S_ROUND}, 0", SALU, wr=sr(S_ROUND)),
                 I(f"s_mov_b32 s{S_WARM}, 0", SALU, wr=sr(S_WARM)),
                 I(f"s_mov_b32 s{S_DT}, 0", SALU, wr=sr(S_DT)),
@@ -810,7 +843,9 @@ class K:
                 I(f"s_add_u32 s{T0}, s{T0}, {BN - 1}", SALU, rd=sr(T0), wr=sr(T0)),
                 I(f"s_lshr_b32 s{nb}, s{T0}, 6", SALU, rd=sr(T0), wr=sr(nb))]
         if not nxt:
-            ins += [I(f"s_max_i32 s{T1}, s{T1}, 0", SALU, rd=sr(T1), wr=sr(T1)),
+            ins += [I(f"s_lshr_b32 s{S_WD}, s{M0R}, 6", SALU, rd=sr(M0R), wr=sr(S_WD)),
+                    I(f"s_add_u32 s{S_WD}, s{S_WD}, s{S_WAVE}", SALU, rd=sr(S_WD) + sr(S_WAVE), wr=sr(S_WD)),
+                    I(f"s_max_i32 s{T1}, s{T1}, 0", SALU, rd=sr(T1), wr=sr(T1)),
                     I(f"s_lshr_b32 s{T1}, s{T1}, 6", SALU, rd=sr(T1), wr=sr(T1)),
                     I(f"s_min_u32 s{T1}, s{T1}, s{S_NBLK}", SALU, rd=sr(T1) + sr(S_NBLK), wr=sr(T1)),
                     I(f"s_sub_i32 s{S_NF2}, s{T1}, 2", SALU, rd=sr(T1), wr=sr(S_NF2)),
@@ -990,7 +1025,7 @@ class K:
         self.lab_end = l_end
         l_epi = self.lab("epi")
         L = {k: self.lab(k) for k in ("fast0", "fast1", "sel0", "sel1", "masked0", "masked1", "last0", "last1",
-                                      "cold", "coldw", "warm", "skip", "tile0")}
+                                      "cold", "coldw", "warm", "skip", "tile0", "diag0", "diag1", "dead0", "dead1")}
         code = []
 
         def emit_block(insts, pre=()):
@@ -1011,7 +1046,25 @@ class K:
         m1, r = self.step(1, "masked", "m1"); refits += r
         la0, r = self.step(0, "last", "l0"); refits += r
         la1, r = self.step(1, "last", "l1"); refits += r
+        if self.causal:
+            dg0, r = self.step(0, "diag", "g0"); refits += r
+            dg1, r = self.step(1, "diag", "g1"); refits += r
+            dd0, r = self.step(0, "dead", "d0"); refits += r
+            dd1, r = self.step(1, "dead", "d1"); refits += r
         I = Inst
+
+        def select(par):
+            """causal: the step's S(n+1) tile t = n + 1, not the item's last (n + 1 < NL1) ->
+            u = S_WD - t: >= 1 visible (fast body), 0 diagonal, < 0 above the diagonal"""
+            if not self.causal or OPT_NODIAG:
+                return []
+            t = S_SWT
+            return [I(f"s_add_u32 s{t}, s{S_N}, 1", SALU),
+                    I(f"s_cmp_ge_u32 s{t}, s{S_NL1}", SALU), I(f"s_cbranch_scc1 {L['masked%d' % par]}", BRANCH),
+                    I(f"s_sub_i32 s{t}, s{S_WD}, s{t}", SALU),
+                    I(f"s_cmp_gt_i32 s{t}, 0", SALU), I(f"s_cbranch_scc1 {L['fast%d' % par]}", BRANCH),
+                    I(f"s_cmp_eq_u32 s{t}, 0", SALU), I(f"s_cbranch_scc1 {L['diag%d' % par]}", BRANCH),
+                    I(f"s_branch {L['dead%d' % par]}", BRANCH)]
         code.append(label(L["fast0"]))
         emit_block(f0 + self.dump("f0_end"), pre=tailpad)
         code += [I(f"s_cmp_gt_i32 s{S_N}, s{S_NF2}", SALU), I(f"s_cbranch_scc1 {L['sel1']}", BRANCH)]
@@ -1020,16 +1073,27 @@ class K:
         code += [I(f"s_cmp_le_i32 s{S_N}, s{S_NF2}", SALU), I(f"s_cbranch_scc1 {L['fast0']}", BRANCH)]
         code.append(label(L["sel0"]))
         code += [I(f"s_cmp_eq_u32 s{S_N}, s{S_NL1}", SALU), I(f"s_cbranch_scc1 {L['last0']}", BRANCH)]
+        code += select(0)
         code.append(label(L["masked0"]))
         emit_block(m0 + self.dump("m0_end"), pre=tailpad)
         code.append(label(L["sel1"]))
         code += [I(f"s_cmp_eq_u32 s{S_N}, s{S_NL1}", SALU), I(f"s_cbranch_scc1 {L['last1']}", BRANCH)]
+        code += select(1)
         code.append(label(L["masked1"]))
         emit_block(m1, pre=tailpad)
         code += [I(f"s_branch {L['sel0']}", BRANCH)]
         code.append(label(L["last0"]))
         emit_block(la0 + self.dump("l0_end"), pre=tailpad)
         code += [I(f"s_branch {l_epi}", BRANCH)]
+        if self.causal:
+            for par, body in ((0, dg0), (1, dg1)):
+                code.append(label(L["diag%d" % par]))
+                emit_block(body, pre=tailpad)
+                code += [I(f"s_branch {L['sel%d' % (1 - par)]}", BRANCH)]
+            for par, body in ((0, dd0), (1, dd1)):
+                code.append(label(L["dead%d" % par]))
+                emit_block(body, pre=tailpad)
+                code += [I(f"s_branch {L['sel%d' % (1 - par)]}", BRANCH)]
         code.append(label(L["last1"]))
         emit_block(la1, pre=tailpad)
         code.append(label(l_epi))

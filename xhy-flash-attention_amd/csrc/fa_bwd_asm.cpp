@@ -46,8 +46,7 @@ struct BwdAsmArgs {
   int32_t q_head, k_head, v_head, do_head, dk_head, dv_head;           // bytes
   int32_t sq, sk, h, ng, nh, group;
   float c, scale;
-  int32_t flags;    // bit 0: varlen_padded_input, bit 1: dK / dV reduced over the GQA group,
-                    // bit 2: sched is a device-built varlen work list ([count, 0, entries])
+  int32_t flags;    // bit 0: varlen_padded_input, bit 1: dK / dV reduced over the GQA group
   int32_t pad;
   void* stamps;     // dev timeline buffer (a generator build with FA_GBW_STAMP=1 writes it), else unused
 };
@@ -61,7 +60,7 @@ struct DqAsmArgs {
   int32_t q_row, kv_row, do_row, dq_row;                            // bytes
   int32_t q_head, k_head, v_head, do_head, dq_head;                 // bytes
   int32_t sq, sk, lse_pitch, dsum_pitch, h, hk;
-  int32_t flags;    // bit 0: varlen_padded_input, bit 1: sched is a device-built varlen work list
+  int32_t flags;    // bit 0: varlen_padded_input
   float c, scale;
 };
 static_assert(sizeof(DqAsmArgs) == 184, "DqAsmArgs layout");
@@ -206,14 +205,6 @@ void launch_bwd_dkdv_asm(const BwdParams& p, bool is_bf16, hipStream_t stream) {
     }
     table = it->second;
   }
-  // varlen: the key blocks that exist, longest causal sweep first (device-built list); the grid
-  // keeps its upper bound and the workgroups past the list's count exit at once
-  uint32_t* vtab = nullptr;
-  if (s.cu_seqlens_k != nullptr && varlen_items_fit(s.b, nblk)) {
-    vtab = build_varlen_items(s.cu_seqlens_k, s.b, nh_grid, p.gqa_reduce ? 1 : s.h / s.hk, kBkn, nblk, true, nwg,
-                              stream);
-    table = vtab;
-  }
   BwdAsmArgs a;
   std::memset(&a, 0, sizeof(a));
   a.q = p.q; a.k = p.k; a.v = p.v; a.dout = p.dout; a.dk = p.dk; a.dv = p.dv;
@@ -228,12 +219,11 @@ void launch_bwd_dkdv_asm(const BwdParams& p, bool is_bf16, hipStream_t stream) {
   a.group = s.h / s.hk;
   a.nh = p.gqa_reduce ? a.group : 1;
   a.c = s.scale_log2; a.scale = s.scale;
-  a.flags = (s.varlen_padded_input ? 1 : 0) | (p.gqa_reduce ? 2 : 0) | (vtab != nullptr ? 4 : 0);
+  a.flags = (s.varlen_padded_input ? 1 : 0) | (p.gqa_reduce ? 2 : 0);
   a.stamps = g_stamps;
   size_t sz = sizeof(a);
   void* cfg[] = {HIP_LAUNCH_PARAM_BUFFER_POINTER, &a, HIP_LAUNCH_PARAM_BUFFER_SIZE, &sz, HIP_LAUNCH_PARAM_END};
   check(hipModuleLaunchKernel(fn, (unsigned)nwg, 1, 1, 256, 1, 1, 0, stream, nullptr, cfg), "hipModuleLaunchKernel");
-  if (vtab != nullptr) check(hipFreeAsync(vtab, stream), "hipFreeAsync (varlen work list)");
 }
 
 bool dq_asm_applicable(const BwdParams& p) {
@@ -277,12 +267,6 @@ void launch_bwd_dq_asm(const BwdParams& p, bool is_bf16, hipStream_t stream) {
     }
     table = it->second;
   }
-  // varlen: the query blocks that exist, heaviest first (device-built list, as the forward's)
-  uint32_t* vtab = nullptr;
-  if (s.cu_seqlens_q != nullptr && p.dq_head_group == 0 && varlen_items_fit(s.b, nmb)) {
-    vtab = build_varlen_items(s.cu_seqlens_q, s.b, s.h, s.h / s.hk, 256, nmb, false, nwg, stream);
-    table = vtab;
-  }
   DqAsmArgs a;
   std::memset(&a, 0, sizeof(a));
   a.q = p.q; a.k = p.k; a.v = p.v; a.dout = p.dout; a.dq = p.dq;
@@ -294,12 +278,11 @@ void launch_bwd_dq_asm(const BwdParams& p, bool is_bf16, hipStream_t stream) {
   a.do_head = (int32_t)(2 * p.do_head); a.dq_head = (int32_t)(2 * p.dq_head);
   a.sq = s.seqlen_q; a.sk = s.seqlen_k; a.lse_pitch = s.lse_pitch; a.dsum_pitch = p.seqlen_q_rounded;
   a.h = s.h; a.hk = s.hk;
-  a.flags = (s.varlen_padded_input ? 1 : 0) | (vtab != nullptr ? 2 : 0);
+  a.flags = s.varlen_padded_input ? 1 : 0;
   a.c = s.scale_log2; a.scale = s.scale;
   size_t sz = sizeof(a);
   void* cfg[] = {HIP_LAUNCH_PARAM_BUFFER_POINTER, &a, HIP_LAUNCH_PARAM_BUFFER_SIZE, &sz, HIP_LAUNCH_PARAM_END};
   check(hipModuleLaunchKernel(fn, (unsigned)nwg, 1, 1, 256, 1, 1, 0, stream, nullptr, cfg), "hipModuleLaunchKernel (dQ)");
-  if (vtab != nullptr) check(hipFreeAsync(vtab, stream), "hipFreeAsync (varlen work list)");
 }
 
 }  // namespace fa
