@@ -49,6 +49,7 @@ def test_asm_forward_in_emulator(asm_text, b, sq, sk, h, hk, causal, bf16, big, 
     (1, 600, 600, 2, 1, True, True, 4),      # snake rounds: items 0-3, then 7, 6 / 5, 4 reversed
     (2, 130, 77, 3, 1, False, True, 2),      # 2-tile items: every successor starts cold
     (1, 300, 700, 2, 1, True, False, 1),     # fp16, sq < sk, mixed warm / cold
+    (1, 600, 600, 8, 2, True, True, 8),      # G % 8 == 0: odd rounds reverse groups of 8 (XCD kept)
 ])
 @pytest.mark.parametrize("d", [128, 64])
 def test_asm_forward_persistent_loop(asm_text, b, sq, sk, h, hk, causal, bf16, grid, d):

@@ -148,6 +148,7 @@ KARG_SIZE = 184
 # dev A/B switches, read when the .s is generated (tools/asm_variant.sh)
 OPT_NOZERO = os.environ.get("FA_GEN_NOZERO") == "1"          # never zero K/V record counts
 OPT_NODIAG = os.environ.get("FA_GEN_NODIAG") == "1"          # causal diagonal: generic masked steps only
+OPT_PLAIN_SNAKE = os.environ.get("FA_GEN_PLAIN_SNAKE") == "1"  # snake reversal over single workgroups
 OPT_ZERO_NOP = int(os.environ.get("FA_GEN_ZERO_NOP", "0"))    # s_nop 15 x N before zeroing them
 # debug: at the named point, workgroup 0 stores every register of each wave (and wave 0 the LDS) to
 # the buffer whose address is passed as the `seed` kernarg, then ends (tools/asm_dump.py)
@@ -699,13 +700,29 @@ class K:
         return ins
 
     def item_pos(self, dst, plus):
-        """dst = r G + (r odd ? G - 1 - w : w), r = S_ROUND + plus (snake order over the sorted items)"""
+        """dst = r G + (r odd ? rev(w) : w), r = S_ROUND + plus: snake order over the sorted items.
+        rev(w) = G - 8 - (w & ~7) + (w & 7) when G % 8 == 0 -- the reversal runs over groups of 8
+        workgroups, so workgroup w stays on the items of the XCD it runs on (w mod 8; the heads of a
+        level are fastest in the list, so a head keeps its XCD and its K/V stay in that L2) -- else
+        G - 1 - w."""
         I = Inst
-        T, R = S_TMP, S_TMP + 1
+        T, R, U = S_TMP, S_TMP + 1, S_TMP + 2
         return [I(f"s_add_u32 s{R}, s{S_ROUND}, {plus}", SALU),
                 I(f"s_mul_i32 s{dst}, s{R}, s{S_GRID}", SALU),
-                I(f"s_sub_u32 s{T}, s{S_GRID}, 1", SALU),
+                I(f"s_and_b32 s{U}, s2, {0 if OPT_PLAIN_SNAKE else 7}", SALU),
+                I(f"s_lshl_b32 s{U}, s{U}, 1", SALU),
+                I(f"s_sub_u32 s{T}, s{S_GRID}, {1 if OPT_PLAIN_SNAKE else 8}", SALU),
                 I(f"s_sub_u32 s{T}, s{T}, s2", SALU),
+                I(f"s_add_u32 s{T}, s{T}, s{U}", SALU),
+                I(f"s_sub_u32 s{U}, s{S_GRID}, 1", SALU),
+                I(f"s_sub_u32 s{U}, s{U}, s2", SALU),
+                I(f"s_and_b32 s{R + 0}, s{R}, 1", SALU),          # keep r's parity only (dst holds r G)
+                I(f"s_bitcmp1_b32 s{S_GRID}, 0", SALU),
+                I(f"s_cselect_b32 s{T}, s{U}, s{T}", SALU),
+                I(f"s_bitcmp1_b32 s{S_GRID}, 1", SALU),
+                I(f"s_cselect_b32 s{T}, s{U}, s{T}", SALU),
+                I(f"s_bitcmp1_b32 s{S_GRID}, 2", SALU),
+                I(f"s_cselect_b32 s{T}, s{U}, s{T}", SALU),
                 I(f"s_bitcmp1_b32 s{R}, 0", SALU),
                 I(f"s_cselect_b32 s{T}, s{T}, s2", SALU),
                 I(f"s_add_u32 s{dst}, s{dst}, s{T}", SALU)]
