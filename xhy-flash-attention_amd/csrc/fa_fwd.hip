@@ -669,8 +669,9 @@ static void dispatch_d(const FwdParams& p, hipStream_t stream) {
   else if (d <= 64) run_fwd<BF16, 64, CAUSAL, DROPOUT>(p, stream);
   else if (d <= 96) run_fwd<BF16, 96, CAUSAL, DROPOUT>(p, stream);
   else if (d <= 128) run_fwd<BF16, 128, CAUSAL, DROPOUT>(p, stream);
-  // d in (128, 160] runs the D = 192 tiles: a dedicated D = 160 instantiation measured slower
-  // (2 x 4096 x 16 causal, tools/hdim_bench.py: 0.331 ms at D = 160 vs 0.312 ms at D = 192)
+  // dedicated tiles (reference hdim160); at 2 x 4096 x 16 causal a d = 160 forward takes the same
+  // time on these as on the D = 192 tiles (0.331 / 0.326 ms, tools/hdim_bench.py): not MFMA-bound
+  else if (d <= 160) run_fwd<BF16, 160, CAUSAL, DROPOUT>(p, stream);
   else if (d <= 192) run_fwd<BF16, 192, CAUSAL, DROPOUT>(p, stream);
   else if (d <= 224) run_fwd<BF16, 224, CAUSAL, DROPOUT>(p, stream);   // (reference hdim224)
   else if (d <= 256) run_fwd<BF16, 256, CAUSAL, DROPOUT>(p, stream);
