@@ -149,6 +149,7 @@ KARG_SIZE = 184
 OPT_NOZERO = os.environ.get("FA_GEN_NOZERO") == "1"          # never zero K/V record counts
 OPT_NODIAG = os.environ.get("FA_GEN_NODIAG") == "1"          # causal diagonal: generic masked steps only
 OPT_PLAIN_SNAKE = os.environ.get("FA_GEN_PLAIN_SNAKE") == "1"  # snake reversal over single workgroups
+OPT_BUDGET = int(os.environ.get("FA_GEN_BUDGET", "24"))        # filler issue cycles per MFMA gap
 OPT_ZERO_NOP = int(os.environ.get("FA_GEN_ZERO_NOP", "0"))    # s_nop 15 x N before zeroing them
 # debug: at the named point, workgroup 0 stores every register of each wave (and wave 0 the LDS) to
 # the buffer whose address is passed as the `seed` kernarg, then ends (tools/asm_dump.py)
@@ -319,7 +320,7 @@ class K:
         for f in range(8):
             for h in range(2):
                 fx.append(self.vread(f, f % 8, h, key=-80 + 2 * f + h, earliest=max(0, NX - 18 + 2 * f) if not last else None))
-        xs = schedule(mx, fx) if mx else schedule([], fx)
+        xs = schedule(mx, fx, budget=OPT_BUDGET) if mx else schedule([], fx)
         # ---------------- phase Y
         my = []
         for i in range(NY):
@@ -392,7 +393,7 @@ class K:
                Inst(f"s_sub_u32 s{t + 2}, s{S_VOFF}, {NSLOT * TILE}", SALU, rd=sr(S_VOFF), wr=sr(t + 2) + [("scc", 0)], key=801),
                Inst(f"s_cmp_ge_u32 s{S_VOFF}, {VBASE + NSLOT * TILE}", SALU, rd=sr(S_VOFF), wr=[("scc", 0)], key=802),
                Inst(f"s_cselect_b32 s{S_VOFF}, s{t + 2}, s{S_VOFF}", SALU, rd=sr(t + 2) + sr(S_VOFF) + [("scc", 0)], wr=sr(S_VOFF), key=803)]
-        ys = schedule(my, fy)
+        ys = schedule(my, fy, budget=OPT_BUDGET)
         body = xs + ys
         if not last:
             # tiles <= n+3 landed in every wave (K(n+3) is prefetched in the next step's phase Y)
@@ -529,7 +530,9 @@ class K:
         I = Inst
         D, SO, SW = 96, 90, 91
         ins = [Inst("s_waitcnt vmcnt(0) lgkmcnt(0)", WAIT), nop(15), nop(15),
-               I(f"s_mov_b32 s{D}, s{S_KA + 18}", SALU), I(f"s_and_b32 s{D + 1}, s{S_KA + 19}, 0xffff", SALU),
+               # the seed kernarg SGPRs are S_QD2 by now: reload the dump address from the kernarg segment
+               I(f"s_load_dwordx2 s[{D}:{D + 1}], s[0:1], 0x48", SMEM), Inst("s_waitcnt lgkmcnt(0)", WAIT),
+               I(f"s_and_b32 s{D + 1}, s{D + 1}, 0xffff", SALU),
                I(f"s_cmp_eq_u32 s2, 0", SALU), I(f"s_cselect_b32 s{D + 2}, 0x7fffffff, 0", SALU),
                I(f"s_mov_b32 s{D + 3}, 0x20000", SALU),
                I(f"s_mul_i32 s{SW}, s{S_WAVE}, {DUMP_SLOTS * 256}", SALU),
