@@ -220,42 +220,43 @@ bool launch_fwd_asm(const FwdParams& p, bool is_bf16, hipStream_t stream) {
   const long long nwg = (long long)s.b * s.h * p.num_m_blocks;
   if (nwg <= 0) return true;
   if (nwg > 0x7fffffff) return false;
+  // Persistent grid (knob 5, default on): one workgroup per CU (the kernel's 160 KiB of LDS allows
+  // one), each walking the heaviest-first item list in snake order, so the rounds pair heavy and
+  // light causal blocks and every item after the first starts with its K/V tiles and Q already
+  // issued by its predecessor.  Varlen launches take their list from the device
+  // (varlen_items_kernel: the host cannot see cu_seqlens, and a host table would hold the empty
+  // blocks past each sequence); the XCD-grouped order (head_group > 0) is built for one item per
+  // workgroup and keeps G = items.
   hipFunction_t fn;
-  uint32_t* table;
+  uint32_t* table = nullptr;
   int cus = 0;
+  const bool persist = knob(kKnobFwdPersist) != 0 && p.head_group == 0;
+  const bool dev_list = persist && s.cu_seqlens_q != nullptr && varlen_items_fit(s.b, p.num_m_blocks);
   {
     std::lock_guard<std::mutex> lk(g_mu);
     DevModule& m = module_for(dev);
     fn = m.fn[(s.d == 64 ? 4 : 0) + (is_bf16 ? 0 : 2) + (s.causal ? 0 : 1)];
-    auto key = std::make_tuple(s.b, s.h, s.hk, p.num_m_blocks, p.head_group);
-    auto it = m.tables.find(key);
-    if (it == m.tables.end()) {
-      std::vector<uint32_t> t = build_table(s.b, s.h, s.hk, p.num_m_blocks, p.head_group);
-      uint32_t* d = nullptr;
-      check(hipMalloc(&d, t.size() * sizeof(uint32_t)), "hipMalloc (schedule table)");
-      check(hipMemcpy(d, t.data(), t.size() * sizeof(uint32_t), hipMemcpyHostToDevice), "hipMemcpy (schedule table)");
-      it = m.tables.emplace(key, d).first;
-    }
-    table = it->second;
     cus = m.cus;
-  }
-  // Persistent grid (knob 5, default on): one workgroup per CU (the kernel's 160 KiB of LDS allows
-  // one), each walking the heaviest-first item list in snake order, so the rounds pair heavy and
-  // light causal blocks and every item after the first starts with its K/V tiles and Q already
-  // issued by its predecessor.  Varlen tables hold empty items (blocks past a sequence) and the
-  // XCD-grouped order is built for one item per workgroup: those keep G = items.
-  long long grid = nwg;
-  const bool persist = knob(kKnobFwdPersist) != 0 && p.head_group == 0 && cus > 0;
-  uint32_t* vtab = nullptr;   // device-built varlen work list (stream-ordered allocation)
-  if (persist && s.cu_seqlens_q != nullptr) {
-    if (varlen_items_fit(s.b, p.num_m_blocks)) {
-      vtab = build_varlen_items(s.cu_seqlens_q, s.b, s.h, s.h / s.hk, 256, p.num_m_blocks, false, nwg, stream);
-      table = vtab;
-      if (nwg > cus) grid = cus;
+    if (!dev_list) {   // host table, cached per shape
+      auto key = std::make_tuple(s.b, s.h, s.hk, p.num_m_blocks, p.head_group);
+      auto it = m.tables.find(key);
+      if (it == m.tables.end()) {
+        std::vector<uint32_t> t = build_table(s.b, s.h, s.hk, p.num_m_blocks, p.head_group);
+        uint32_t* d = nullptr;
+        check(hipMalloc(&d, t.size() * sizeof(uint32_t)), "hipMalloc (schedule table)");
+        check(hipMemcpy(d, t.data(), t.size() * sizeof(uint32_t), hipMemcpyHostToDevice), "hipMemcpy (schedule table)");
+        it = m.tables.emplace(key, d).first;
+      }
+      table = it->second;
     }
-  } else if (persist && nwg > cus) {
-    grid = cus;
   }
+  uint32_t* vtab = nullptr;   // device-built varlen work list (stream-ordered allocation)
+  if (dev_list) {
+    vtab = build_varlen_items(s.cu_seqlens_q, s.b, s.h, s.h / s.hk, 256, p.num_m_blocks, false, nwg, stream);
+    table = vtab;
+  }
+  long long grid = nwg;
+  if (persist && cus > 0 && nwg > cus && (dev_list || s.cu_seqlens_q == nullptr)) grid = cus;
   FwdAsmArgs a;
   std::memset(&a, 0, sizeof(a));
   a.q = p.q; a.k = p.k; a.v = p.v; a.o = p.o; a.lse = p.lse;
