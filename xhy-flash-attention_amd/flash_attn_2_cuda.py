@@ -12,6 +12,7 @@ rejects them, and a missing library raises ImportError at import time.
 """
 from __future__ import annotations
 
+import contextlib
 import ctypes
 import os
 
@@ -79,6 +80,26 @@ def _stream(t: torch.Tensor):
     return ctypes.c_void_p(torch.cuda.current_stream(t.device).cuda_stream)
 
 
+def _device_guard(dev: torch.device):
+    """the launch runs with `dev` current (the C ABI launches on the current device, as the
+    reference's CUDAGuard arranges); no guard when it already is (host overhead per call)"""
+    if dev.index is None or dev.index == torch.cuda.current_device():
+        return contextlib.nullcontext()
+    return torch.cuda.device(dev)
+
+
+_GFX950 = {}   # device index -> is gfx950 (device properties are fixed for the process)
+
+
+def _is_gfx950(dev: torch.device) -> bool:
+    idx = dev.index if dev.index is not None else torch.cuda.current_device()
+    ok = _GFX950.get(idx)
+    if ok is None:
+        ok = getattr(torch.cuda.get_device_properties(idx), "gcnArchName", "").startswith("gfx950")
+        _GFX950[idx] = ok
+    return ok
+
+
 def _ptr(t):
     return ctypes.c_void_p(t.data_ptr()) if t is not None else ctypes.c_void_p(0)
 
@@ -106,8 +127,7 @@ def _vec_ok(t: torch.Tensor) -> torch.Tensor:
 
 def _check_inputs(q, k, v, name="FlashAttention"):
     _check(q.is_cuda and k.is_cuda and v.is_cuda, "Input tensor must be on CUDA device")
-    props = torch.cuda.get_device_properties(q.device)
-    _check(getattr(props, "gcnArchName", "").startswith("gfx950"),
+    _check(_is_gfx950(q.device),
            "FlashAttention MI355X build only supports gfx950 (MI355X) GPUs")
     _check(q.dtype in (torch.float16, torch.bfloat16),
            "FlashAttention only support fp16 and bf16 data type")
@@ -189,7 +209,7 @@ def fwd(q, k, v, out_, p_dropout, softmax_scale, is_causal, return_softmax, gen_
     seqlen_q_rounded = _round_multiple(seqlen_q, 128)
     seqlen_k_rounded = _round_multiple(seqlen_k, 128)
 
-    with torch.cuda.device(q.device):
+    with _device_guard(q.device):
         softmax_lse = torch.empty((batch_size, num_heads, seqlen_q), dtype=torch.float32, device=q.device)
         p = None
         if return_softmax:   # S_dmask (b, h, sq_r, sk_r), dropped elements negated
@@ -265,7 +285,7 @@ def varlen_fwd(q, k, v, out_, cu_seqlens_q, cu_seqlens_k, max_seqlen_q, max_seql
     seqlen_q_rounded = _round_multiple(max_seqlen_q, 128)
     seqlen_k_rounded = _round_multiple(max_seqlen_k, 128)
 
-    with torch.cuda.device(q.device):
+    with _device_guard(q.device):
         softmax_lse = torch.empty((batch_size, num_heads, max_seqlen_q), dtype=torch.float32, device=q.device)
         if zero_tensors:
             out.zero_()
@@ -346,7 +366,7 @@ def bwd(dout, q, k, v, out, softmax_lse, dq_, dk_, dv_, p_dropout, softmax_scale
     dk, dk_given = _grad_buffer(dk_, k)
     dv, dv_given = _grad_buffer(dv_, v)
 
-    with torch.cuda.device(q.device):
+    with _device_guard(q.device):
         softmax_d = torch.empty((batch_size, num_heads, seqlen_q_rounded), dtype=torch.float32, device=q.device)
         # scratch for the kernels' -LSE/scale rows (the reference allocates (b, h, sq_r, d_r) here for
         # its fp32 atomic dQ accumulator; the MI355X backward needs only (b, h, sq_r))
@@ -407,7 +427,7 @@ def varlen_bwd(dout, q, k, v, out, softmax_lse, dq_, dk_, dv_, cu_seqlens_q, cu_
     dk, dk_given = _grad_buffer(dk_, k)
     dv, dv_given = _grad_buffer(dv_, v)
 
-    with torch.cuda.device(q.device):
+    with _device_guard(q.device):
         softmax_d = torch.empty((batch_size, num_heads, seqlen_q_rounded), dtype=torch.float32, device=q.device)
         # scratch for the kernels' -LSE/scale rows (the reference allocates (b, h, sq_r, d_r) here for
         # its fp32 atomic dQ accumulator; the MI355X backward needs only (b, h, sq_r))
