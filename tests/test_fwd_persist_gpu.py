@@ -57,3 +57,23 @@ def test_persistent_forward_varlen_bitwise(d):
     assert torch.equal(o1, o0)
     for i, n in enumerate(lens):     # LSE rows past a sequence's length are not written
         assert torch.equal(l1[i, :, :n], l0[i, :, :n])
+
+
+@pytest.mark.parametrize("nseq", [3000, 5000])
+def test_persistent_forward_many_sequences(nseq):
+    """thousands of short sequences: the device-built list (3000; its shared memory holds 2 ints per
+    sequence) and, past the builder's limit (5000), the host table with one workgroup per item"""
+    from flash_attn import flash_attn_varlen_func
+
+    g = torch.Generator().manual_seed(nseq)
+    lens = torch.randint(1, 300, (nseq,), generator=g).tolist()
+    cu = torch.tensor([0] + lens, dtype=torch.int64).cumsum(0).to(torch.int32).to(DEV)
+    total, h, d = sum(lens), 2, 64
+    torch.manual_seed(0)
+    q, k, v = (torch.randn(total, h, d, device=DEV, dtype=torch.bfloat16) for _ in range(3))
+    (o1, l1, _), (o0, l0, _) = _both(lambda: flash_attn_varlen_func(
+        q, k, v, cu, cu, max(lens), max(lens), causal=True, return_attn_probs=True))
+    assert torch.equal(o1, o0)
+    n = torch.tensor(lens, device=DEV)
+    valid = torch.arange(l1.shape[-1], device=DEV)[None, None, :] < n[:, None, None]
+    assert torch.equal(l1[valid.expand_as(l1)], l0[valid.expand_as(l0)])

@@ -110,7 +110,7 @@ std::vector<uint32_t> build_table(int b, int h, int hk, int nmb, int hp) {
 
 bool fits32(int64_t x) { return x >= 0 && x < (1ll << 31); }
 
-constexpr int kVarlenMaxSeqs = 8192, kVarlenMaxBlocks = 2048;
+constexpr int kVarlenMaxSeqs = 4096, kVarlenMaxBlocks = 2048;
 
 // Varlen work lists, built on the device (the host cannot list the items without reading
 // cu_seqlens back): the (sequence, block, head) items that hold rows or keys, heaviest first.
@@ -170,7 +170,12 @@ __global__ void __launch_bounds__(1024) varlen_items_kernel(const int* cu, int b
 
 }  // namespace
 
-bool varlen_items_fit(int b, int nlev) { return b <= kVarlenMaxSeqs && nlev <= kVarlenMaxBlocks; }
+// its shared memory (2 b + 3 (nlev + 1) ints) must stay within the 64 KiB a HIP kernel gets without
+// an opt-in attribute
+bool varlen_items_fit(int b, int nlev) {
+  return b > 0 && nlev > 0 && b <= kVarlenMaxSeqs && nlev <= kVarlenMaxBlocks &&
+         (2ll * b + 3ll * (nlev + 1)) * (long long)sizeof(int) <= 65536;
+}
 
 uint32_t* build_varlen_items(const int* cu, int b, int nh, int gdiv, int rows, int nlev, bool reverse,
                              long long max_items, hipStream_t stream) {
