@@ -80,17 +80,15 @@ def test_asm_forward_refit_at_the_diagonal(asm_text):
     heap = Heap(16 << 20)
     aq, ak, av = heap.put(q16), heap.put(k16), heap.put(v16)
     ao, alse = heap.alloc(s * d * 2), heap.alloc(s * 4)
-    tab = emu_fwd.sched_table(1, 1, 1, 2)
-    asch = heap.put(tab)
-    kw = dict(q=aq, k=ak, v=av, o=ao, lse=alse, sched=asch, cuq=0, cuk=0, rng=0, seed=0, off=0,
+    kw = dict(q=aq, k=ak, v=av, o=ao, lse=alse, sched=0, cuq=0, cuk=0, rng=0, seed=0, off=0,
               q_batch=s * d * 2, k_batch=s * d * 2, v_batch=s * d * 2, o_batch=s * d * 2, q_row=d * 2, kv_row=d * 2,
               o_row=d * 2, q_head=d * 2, k_head=d * 2, v_head=d * 2, o_head=d * 2, sq=s, sk=s, lse_pitch=s, h=1,
               c=float(np.float32(d ** -0.5 * 1.4426950408889634)), flags=0,
-              n_items=len(tab), grid=len(tab))
+              n_items=2, grid=2, dec=emu_fwd.fwd_item_decode(1, 1, 1, 2))
     akarg = heap.put(np.frombuffer(emu_fwd.pack_args(**kw), dtype=np.uint8))
     emu = Emu(asm_text, "fa_fwd_asm_d128_f16_causal", heap)
     emu.trace_labels = ["refit"]
-    for L in range(len(tab)):
+    for L in range(2):
         emu.run_wg(L, akarg)
     assert any("refit_a" in n for _, n in emu.trace) and any("refit_b" in n for _, n in emu.trace)
     o = f16_to_f32(heap.get(ao, s * d * 2).view(np.uint16)).reshape(1, s, 1, d)

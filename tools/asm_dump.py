@@ -57,7 +57,7 @@ def gpu(point, lib):
 
 def cpu(point):
     from asm_emu import Emu, Heap
-    from emu_fwd import pack_args, sched_table
+    from emu_fwd import fwd_item_decode, pack_args
     env = dict(os.environ, FA_GEN_DUMP=point)
     text = subprocess.run([sys.executable, os.path.join(ROOT, "xhy-flash-attention_amd", "csrc", "asm", "gen_fwd.py")],
                           check=True, capture_output=True, text=True, env=env).stdout
@@ -68,13 +68,11 @@ def cpu(point):
     alse = heap.alloc(B * H * SQ * 4)
     arng = heap.alloc(16)
     adump = heap.alloc(DUMP_WORDS * 4)
-    tab = sched_table(B, H, HK, (SQ + 255) // 256)
-    asch = heap.put(tab)
-    kw = dict(q=aq, k=ak, v=av, o=ao, lse=alse, sched=asch, cuq=0, cuk=0, rng=arng, seed=adump, off=0,
+    kw = dict(q=aq, k=ak, v=av, o=ao, lse=alse, sched=0, cuq=0, cuk=0, rng=arng, seed=adump, off=0,
               q_batch=SQ * H * D * 2, k_batch=SK * HK * D * 2, v_batch=SK * HK * D * 2, o_batch=SQ * H * D * 2,
               q_row=H * D * 2, kv_row=HK * D * 2, o_row=H * D * 2, q_head=D * 2, k_head=D * 2, v_head=D * 2,
               o_head=D * 2, sq=SQ, sk=SK, lse_pitch=SQ, h=H, c=float(np.float32(D ** -0.5 * 1.4426950408889634)), flags=0,
-              n_items=1, grid=1)
+              n_items=1, grid=1, dec=fwd_item_decode(B * H, H, H // HK, (SQ + 255) // 256))
     akarg = heap.put(np.frombuffer(pack_args(**kw), dtype=np.uint8))
     emu = Emu(text, f"fa_fwd_asm_d128_bf16_{'causal' if CAUSAL else 'full'}", heap)
     emu.run_wg(0, akarg)

@@ -438,12 +438,14 @@ class Emu:
             y = self.ssrc64(w, a[1]) if a[1] in ("vcc",) or a[1].startswith("s[") else int(a[1], 0)
             w.scc = (x == y) if op == "s_cmp_eq_u64" else (x != y)
             return
-        if op == "s_and_b64" or op == "s_lshl_b64":
+        if op in ("s_and_b64", "s_lshl_b64", "s_lshr_b64"):
             x = self.ssrc64(w, a[1])
             if op == "s_and_b64":
                 r = x & self.ssrc64(w, a[2])
+            elif op == "s_lshl_b64":
+                r = (x << (self.ssrc(w, a[2]) & 63)) & (2 ** 64 - 1)
             else:
-                r = (x << self.ssrc(w, a[2])) & (2 ** 64 - 1)
+                r = x >> (self.ssrc(w, a[2]) & 63)
             if a[0] == "vcc":
                 w.vcc = np.array([(r >> i) & 1 for i in range(64)], dtype=bool)
             else:

@@ -14,6 +14,8 @@ import numpy as np
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, os.path.join(ROOT, "tools"))
+sys.path.insert(0, os.path.join(ROOT, "xhy-flash-attention_amd", "csrc", "asm"))
+from isa import dkdv_item_decode  # noqa: E402
 from asm_emu import Emu, Heap, bf16_to_f32, f16_to_f32, f32_to_bf16, f32_to_f16  # noqa: E402
 
 GEN = os.path.join(ROOT, "xhy-flash-attention_amd", "csrc", "asm", "gen_bwd.py")
@@ -25,25 +27,6 @@ def asm_text():
     return subprocess.run([sys.executable, GEN], check=True, capture_output=True, text=True).stdout
 
 
-def sched_table(b, nh_grid, hk, h, nblk, reduce):
-    """workgroup -> (bidb | hx << 16, kvh | kblock << 16), heaviest key block first, XCD-grouped as
-    fa_common.h xcd_order"""
-    nbh = b * nh_grid
-    tab = np.zeros((nbh * nblk, 2), dtype=np.uint32)
-    g = h // hk
-    for L in range(nbh * nblk):
-        if nbh % 8 == 0:
-            i = L >> 3
-            hl, blk = divmod(i, nblk)
-            bh = hl * 8 + (L & 7)
-        else:
-            blk, bh = divmod(L, nbh)
-        bidb, hx = divmod(bh, nh_grid)
-        kvh = hx if reduce else hx // g
-        tab[L] = (bidb | (hx << 16), kvh | (blk << 16))
-    return tab
-
-
 def pack_args(**kw):
     out = struct.pack("<10Q", kw["q"], kw["k"], kw["v"], kw["do"], kw["dk"], kw["dv"], kw["lsed"], kw["sched"],
                       kw["cuq"], kw["cuk"])
@@ -52,7 +35,8 @@ def pack_args(**kw):
     out += struct.pack("<6i", kw["q_head"], kw["k_head"], kw["v_head"], kw["do_head"], kw["dk_head"], kw["dv_head"])
     out += struct.pack("<6i", kw["sq"], kw["sk"], kw["h"], kw["ng"], kw["nh"], kw["group"])
     out += struct.pack("<ffiiQ", kw["c"], kw["scale"], kw["flags"], 0, 0)
-    assert len(out) == 224, len(out)
+    out += struct.pack("<10I", *kw["dec"])
+    assert len(out) == 264, len(out)
     return out
 
 
@@ -119,9 +103,9 @@ def run(b=1, sq=200, sk=200, h=2, hk=1, causal=True, bf16=True, reduce=True, see
     alsed = heap.put(lsed)
     nblk = (sk + BKN - 1) // BKN
     red = reduce and g > 1
-    tab = sched_table(b, nh_out, hk, h, nblk, red)
-    asch = heap.put(tab)
-    kw = dict(q=aq, k=ak, v=av, do=ado, dk=adk, dv=adv, lsed=alsed, sched=asch, cuq=0, cuk=0,
+    n_items = b * nh_out * nblk
+    kw = dict(q=aq, k=ak, v=av, do=ado, dk=adk, dv=adv, lsed=alsed, sched=0, cuq=0, cuk=0,
+              dec=dkdv_item_decode(b * nh_out, nh_out, 1 if red else g, nblk),
               q_batch=sq * h * D * 2, k_batch=sk * hk * D * 2, v_batch=sk * hk * D * 2, do_batch=sq * h * D * 2,
               dk_batch=sk * nh_out * D * 2, dv_batch=sk * nh_out * D * 2,
               q_row=h * D * 2, k_row=hk * D * 2, v_row=hk * D * 2, do_row=h * D * 2, dk_row=nh_out * D * 2,
@@ -132,7 +116,7 @@ def run(b=1, sq=200, sk=200, h=2, hk=1, causal=True, bf16=True, reduce=True, see
     text = text or asm_text()
     name = f"fa_bwd_dkdv_asm_d128_{'bf16' if bf16 else 'f16'}_{'causal' if causal else 'full'}"
     emu = Emu(text, name, heap)
-    for L in range(len(tab)):
+    for L in range(n_items):
         emu.run_wg(L, akarg)
     dk = dec(heap.get(adk, b * sk * nh_out * D * 2).view(np.uint16)).reshape(b, sk, nh_out, D).astype(np.float64)
     dv = dec(heap.get(adv, b * sk * nh_out * D * 2).view(np.uint16)).reshape(b, sk, nh_out, D).astype(np.float64)

@@ -16,7 +16,8 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, os.path.join(ROOT, "tools"))
 from asm_emu import Emu, Heap, bf16_to_f32, f16_to_f32, f32_to_bf16, f32_to_f16  # noqa: E402
 from emu_bwd import reference as bwd_reference  # noqa: E402
-from emu_fwd import sched_table  # noqa: E402
+sys.path.insert(0, os.path.join(ROOT, "xhy-flash-attention_amd", "csrc", "asm"))
+from isa import fwd_item_decode  # noqa: E402
 
 GEN = os.path.join(ROOT, "xhy-flash-attention_amd", "csrc", "asm", "gen_dq.py")
 D = 128
@@ -35,7 +36,8 @@ def pack_args(**kw):
     out += struct.pack("<5i", kw["q_head"], kw["k_head"], kw["v_head"], kw["do_head"], kw["dq_head"])
     out += struct.pack("<7i", kw["sq"], kw["sk"], kw["lse_pitch"], kw["dsum_pitch"], kw["h"], kw["hk"], kw["flags"])
     out += struct.pack("<ff", kw["c"], kw["scale"])
-    assert len(out) == 184, len(out)
+    out += struct.pack("<10I", *kw["dec"])
+    assert len(out) == 224, len(out)
     return out
 
 
@@ -58,7 +60,8 @@ def reference_dq(q, k, v, do, causal, scale):
     return lse, dsum, dq
 
 
-def run(b=1, sq=300, sk=300, h=2, hk=1, causal=True, bf16=True, seed=0, text=None, verbose=True):
+def run(b=1, sq=300, sk=300, h=2, hk=1, causal=True, bf16=True, seed=0, text=None, verbose=True, hp=0):
+    """hp: heads per XCD group of the work order (0: head-fastest)"""
     rng = np.random.default_rng(seed)
     q = rng.standard_normal((b, sq, h, D)).astype(np.float32)
     k = rng.standard_normal((b, sk, hk, D)).astype(np.float32)
@@ -79,9 +82,9 @@ def run(b=1, sq=300, sk=300, h=2, hk=1, causal=True, bf16=True, seed=0, text=Non
     heap.get(adq, b * sq * h * D * 2)[:] = 0xAB
     alse, ads = heap.put(lse32), heap.put(ds32)
     nmb = (sq + BM - 1) // BM
-    tab = sched_table(b, h, hk, nmb)
-    asch = heap.put(tab)
-    kw = dict(q=aq, k=ak, v=av, do=ado, dq=adq, lse=alse, dsum=ads, sched=asch, cuq=0, cuk=0,
+    n_items = b * h * nmb
+    kw = dict(q=aq, k=ak, v=av, do=ado, dq=adq, lse=alse, dsum=ads, sched=0, cuq=0, cuk=0,
+              dec=fwd_item_decode(b * h, h, h // hk, nmb, hp),
               q_batch=sq * h * D * 2, kv_batch=sk * hk * D * 2, do_batch=sq * h * D * 2, dq_batch=sq * h * D * 2,
               q_row=h * D * 2, kv_row=hk * D * 2, do_row=h * D * 2, dq_row=h * D * 2,
               q_head=D * 2, k_head=D * 2, v_head=D * 2, do_head=D * 2, dq_head=D * 2,
@@ -91,7 +94,7 @@ def run(b=1, sq=300, sk=300, h=2, hk=1, causal=True, bf16=True, seed=0, text=Non
     text = text or asm_text()
     name = f"fa_bwd_dq_asm_d128_{'bf16' if bf16 else 'f16'}_{'causal' if causal else 'full'}"
     emu = Emu(text, name, heap)
-    for L in range(len(tab)):
+    for L in range(n_items):
         emu.run_wg(L, akarg)
     dq = dec(heap.get(adq, b * sq * h * D * 2).view(np.uint16)).reshape(b, sq, h, D).astype(np.float64)
     e = np.abs(dq - dq_ref).max() / max(np.abs(dq_ref).max(), 1e-9)

@@ -2,7 +2,7 @@
 """Runs the generated assembly forward (csrc/asm/gen_fwd.py) in the CPU emulator (tools/asm_emu.py)
 on small inputs and compares O / LSE with a float64 reference (dev / test tool).
 
-    python tools/emu_fwd.py [--b 1 --sq 300 --sk 300 --h 2 --hk 1 --causal --fp16 --varlen 100,250]
+    python tools/emu_fwd.py [--b 1 --sq 300 --sk 300 --h 2 --hk 1 --full --fp16 --grid G --hp HP]
 """
 import argparse
 import os
@@ -14,7 +14,9 @@ import numpy as np
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, os.path.join(ROOT, "tools"))
+sys.path.insert(0, os.path.join(ROOT, "xhy-flash-attention_amd", "csrc", "asm"))
 from asm_emu import Emu, Heap, bf16_to_f32, f16_to_f32, f32_to_bf16, f32_to_f16  # noqa: E402
+from isa import fwd_item_decode  # noqa: E402
 
 GEN = os.path.join(ROOT, "xhy-flash-attention_amd", "csrc", "asm", "gen_fwd.py")
 D = 128
@@ -25,18 +27,6 @@ def asm_text():
     return subprocess.run([sys.executable, GEN], check=True, capture_output=True, text=True).stdout
 
 
-def sched_table(b, h, hk, nmb):
-    nbh = b * h
-    tab = np.zeros((nbh * nmb, 2), dtype=np.uint32)
-    for L in range(nbh * nmb):
-        m_idx, bh = divmod(L, nbh)
-        mb = nmb - 1 - m_idx
-        bidb, head = divmod(bh, h)
-        kvh = head // (h // hk)
-        tab[L] = (bidb | (head << 16), kvh | (mb << 16))
-    return tab
-
-
 def pack_args(**kw):
     head = struct.pack("<11Q4q", kw["q"], kw["k"], kw["v"], kw["o"], kw["lse"], kw["sched"], kw["cuq"], kw["cuk"],
                        kw["rng"], kw["seed"], kw["off"], kw["q_batch"], kw["k_batch"], kw["v_batch"], kw["o_batch"])
@@ -44,8 +34,8 @@ def pack_args(**kw):
     tail = struct.pack("<11i", kw["q_row"], kw["kv_row"], kw["o_row"], kw["q_head"], kw["k_head"], kw["v_head"],
                        kw["o_head"], kw["sq"], kw["sk"], kw["lse_pitch"], kw["h"])
     tail += struct.pack("<fiiii", kw["c"], kw["flags"], kw["n_items"], kw["grid"], 0)
-    out = head + tail
-    assert len(out) == 184, len(out)
+    out = head + tail + struct.pack("<10I", *kw["dec"])
+    assert len(out) == 224, len(out)
     return out
 
 
@@ -72,8 +62,9 @@ def reference(q, k, v, causal, scale, seqs_q=None, seqs_k=None):
 
 
 def run(b=1, sq=300, sk=300, h=2, hk=1, causal=True, bf16=True, seed=0, big=None, text=None, verbose=True,
-        grid=None, d=128):
-    """grid: workgroups of the persistent item loop (default: one per item); d: head dim (128, 64)"""
+        grid=None, d=128, hp=0):
+    """grid: workgroups of the persistent item loop (default: one per item); d: head dim (128, 64);
+    hp: heads per XCD group of the work order (0: head-fastest)"""
     D = d
     rng = np.random.default_rng(seed)
     q = rng.standard_normal((b, sq, h, D)).astype(np.float32)
@@ -92,18 +83,17 @@ def run(b=1, sq=300, sk=300, h=2, hk=1, causal=True, bf16=True, seed=0, big=None
     heap.get(ao, b * sq * h * D * 2)[:] = 0xAB   # poison
     alse = heap.alloc(b * h * sq * 4)
     nmb = (sq + BM - 1) // BM
-    tab = sched_table(b, h, hk, nmb)
-    asch = heap.put(tab)
-    kw = dict(q=aq, k=ak, v=av, o=ao, lse=alse, sched=asch, cuq=0, cuk=0, rng=0, seed=0, off=0,
+    n_items = b * h * nmb
+    kw = dict(q=aq, k=ak, v=av, o=ao, lse=alse, sched=0, cuq=0, cuk=0, rng=0, seed=0, off=0,
               q_batch=sq * h * D * 2, k_batch=sk * hk * D * 2, v_batch=sk * hk * D * 2, o_batch=sq * h * D * 2,
               q_row=h * D * 2, kv_row=hk * D * 2, o_row=h * D * 2, q_head=D * 2, k_head=D * 2, v_head=D * 2,
               o_head=D * 2, sq=sq, sk=sk, lse_pitch=sq, h=h, c=float(np.float32(scale * 1.4426950408889634)), flags=0,
-              n_items=len(tab), grid=grid or len(tab))
+              n_items=n_items, grid=grid or n_items, dec=fwd_item_decode(b * h, h, h // hk, nmb, hp))
     akarg = heap.put(np.frombuffer(pack_args(**kw), dtype=np.uint8))
     text = text or asm_text()
     name = f"fa_fwd_asm_d{D}_{'bf16' if bf16 else 'f16'}_{'causal' if causal else 'full'}"
     emu = Emu(text, name, heap)
-    for L in range(grid or len(tab)):
+    for L in range(grid or n_items):
         emu.run_wg(L, akarg)
     o = dec(heap.get(ao, b * sq * h * D * 2).view(np.uint16)).reshape(b, sq, h, D).astype(np.float64)
     lse = heap.get(alse, b * h * sq * 4).view(np.float32).reshape(b, h, sq).astype(np.float64)
@@ -129,5 +119,6 @@ if __name__ == "__main__":
     ap.add_argument("--seed", type=int, default=0)
     ap.add_argument("--grid", type=int, default=None)
     ap.add_argument("--d", type=int, default=128)
+    ap.add_argument("--hp", type=int, default=0)
     a = ap.parse_args()
-    run(a.b, a.sq, a.sk, a.h, a.hk, not a.full, not a.fp16, a.seed, a.big, grid=a.grid, d=a.d)
+    run(a.b, a.sq, a.sk, a.h, a.hk, not a.full, not a.fp16, a.seed, a.big, grid=a.grid, d=a.d, hp=a.hp)

@@ -41,7 +41,7 @@ import sys
 
 sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
 from isa import (ACCR, ACCW, BARRIER, BRANCH, DMA, LABEL, LDS, MFMA, PERM, RFL, SALU, SMEM, SOPP,  # noqa: E402
-                 TRANS, VALU, VLOAD, VSTORE, WAIT, Inst, add_waits, ar, fix_hazards, label, nop, rtxt,
+                 TRANS, VALU, VLOAD, VSTORE, WAIT, Inst, add_waits, ar, fix_hazards, item_decode_ops, label, nop, rtxt,
                  schedule, sr, vr)
 
 D = 128
@@ -130,7 +130,8 @@ S_WAVE = 48
 S_TMP = 49                           # 49..55 (the prologue keeps kernargs in 56..101)
 NSGPR = 102
 
-KARG_SIZE = 224
+KARG_SIZE = 264
+DEC_OFF = 224    # fa_params.h ItemDecode (40 bytes) after BwdAsmArgs' 224
 
 # dev A/B switches, read when the .s is generated (tools/asm_variant.sh)
 OPT_WIN = int(os.environ.get("FA_GBW_WIN", "16"))     # an A fragment may be read up to WIN MFMAs ahead
@@ -438,15 +439,15 @@ class K:
         ins += [I("v_lshrrev_b32_e32 v1, 6, v0", VALU, rd=vr(0), wr=vr(1)),
                 I(f"v_readfirstlane_b32 s{S_WAVE}, v1", RFL, rd=vr(1), wr=sr(S_WAVE)),
                 I(f"v_and_b32_e32 v{V_LANE}, 63, v0", VALU, rd=vr(0), wr=vr(V_LANE))]
-        # schedule entry: (bidb | hx << 16, kvh | kblock << 16)
-        ins += [I(f"s_lshl_b32 s{T0}, s2, 3", SALU, rd=sr(2), wr=sr(T0)),
-                I(f"s_load_dwordx2 s[{T1}:{T2}], s[{Psch}:{Psch + 1}], s{T0}", SMEM, rd=sr(Psch, 2) + sr(T0), wr=sr(T1, 2)),
+        # the work order (fa_params.h ItemDecode) into s[36:45] (free until the geometry):
+        # (bidb, hx, kvh, key block) of this workgroup
+        ins += [I(f"s_load_dwordx8 s[36:43], s[0:1], {DEC_OFF}", SMEM),
+                I(f"s_load_dwordx2 s[44:45], s[0:1], {DEC_OFF + 32}", SMEM),
                 I("s_waitcnt lgkmcnt(0)", WAIT)]
         BIDB, HX, KVH, KB = 24, 25, 26, 27      # S_N .. S_Q0V, set at the end
-        ins += [I(f"s_and_b32 s{BIDB}, s{T1}, 0xffff", SALU, rd=sr(T1), wr=sr(BIDB)),
-                I(f"s_lshr_b32 s{HX}, s{T1}, 16", SALU, rd=sr(T1), wr=sr(HX)),
-                I(f"s_and_b32 s{KVH}, s{T2}, 0xffff", SALU, rd=sr(T2), wr=sr(KVH)),
-                I(f"s_lshr_b32 s{KB}, s{T2}, 16", SALU, rd=sr(T2), wr=sr(KB))]
+        ins += item_decode_ops(L=2, M=36, pa=T1, pb=T3, t=T5, u=T6, o_blk=KB, reverse=False)
+        ins += [I(f"s_mov_b32 s{BIDB}, s{T3}", SALU), I(f"s_mov_b32 s{HX}, s{T6}", SALU),
+                I(f"s_mov_b32 s{KVH}, s{T1}", SALU)]
         # varlen geometry (BlockInfo, block_info.h:14-31): 64-bit byte offsets of row 0 of this sequence;
         # seqlens into SQ / SK
         QOFF, DOOFF, KOFF, VOFF, DKOFF, DVOFF = (34, 35), (36, 37), (38, 39), (40, 41), (42, 43), (44, 45)

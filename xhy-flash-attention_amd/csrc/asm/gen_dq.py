@@ -32,7 +32,7 @@ import sys
 
 sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
 from isa import (ACCR, ACCW, BARRIER, BRANCH, DMA, LABEL, LDS, MFMA, PERM, RFL, SALU, SMEM, SOPP,  # noqa: E402
-                 TRANS, VALU, VLOAD, VSTORE, WAIT, Inst, add_waits, ar, fix_hazards, label, nop, rtxt,
+                 TRANS, VALU, VLOAD, VSTORE, WAIT, Inst, add_waits, ar, fix_hazards, item_decode_ops, label, nop, rtxt,
                  schedule, sr, vr)
 
 D = 128
@@ -114,7 +114,8 @@ S_WAVE = 30
 S_TMP = 31                     # 31..39
 NSGPR = 102
 
-KARG_SIZE = 184
+KARG_SIZE = 224
+DEC_OFF = 184    # fa_params.h ItemDecode (40 bytes) after DqAsmArgs' 184
 
 
 class K:
@@ -317,14 +318,14 @@ class K:
                 I("v_lshrrev_b32_e32 v1, 6, v0", VALU, rd=vr(0), wr=vr(1)),
                 I(f"v_readfirstlane_b32 s{S_WAVE}, v1", RFL, rd=vr(1), wr=sr(S_WAVE)),
                 I(f"v_and_b32_e32 v{V_LANE}, 63, v0", VALU, rd=vr(0), wr=vr(V_LANE)),
-                I(f"s_lshl_b32 s{T[0]}, s2, 3", SALU, rd=sr(2), wr=sr(T[0])),
-                I(f"s_load_dwordx2 s[{T[1]}:{T[2]}], s[{Psch}:{Psch + 1}], s{T[0]}", SMEM, rd=sr(Psch, 2) + sr(T[0]), wr=sr(T[1], 2)),
+                # the work order (fa_params.h ItemDecode) into s[40:49] (free until the geometry)
+                I(f"s_load_dwordx8 s[40:47], s[0:1], {DEC_OFF}", SMEM),
+                I(f"s_load_dwordx2 s[48:49], s[0:1], {DEC_OFF + 32}", SMEM),
                 I("s_waitcnt lgkmcnt(0)", WAIT)]
         BIDB, HEAD, KVH, MB = S_N, S_NLAST, S_MASK0, S_KV32     # temporaries until the loop state
-        ins += [I(f"s_and_b32 s{BIDB}, s{T[1]}, 0xffff", SALU, rd=sr(T[1]), wr=sr(BIDB)),
-                I(f"s_lshr_b32 s{HEAD}, s{T[1]}, 16", SALU, rd=sr(T[1]), wr=sr(HEAD)),
-                I(f"s_and_b32 s{KVH}, s{T[2]}, 0xffff", SALU, rd=sr(T[2]), wr=sr(KVH)),
-                I(f"s_lshr_b32 s{MB}, s{T[2]}, 16", SALU, rd=sr(T[2]), wr=sr(MB))]
+        ins += item_decode_ops(L=2, M=40, pa=T[1], pb=T[3], t=T[5], u=T[6], o_blk=MB, reverse=True)
+        ins += [I(f"s_mov_b32 s{BIDB}, s{T[3]}", SALU), I(f"s_mov_b32 s{HEAD}, s{T[6]}", SALU),
+                I(f"s_mov_b32 s{KVH}, s{T[1]}", SALU)]
         # varlen geometry (block_info.h:14-31): byte offsets of row 0 of this sequence (Q-side: Q, dO,
         # dQ; K-side: K and V share it, k_row == v_row and the batch strides are equal)
         QOFF, DOOFF, DQOFF, KOFF = (40, 41), (42, 43), (44, 45), (46, 47)

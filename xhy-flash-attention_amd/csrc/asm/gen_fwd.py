@@ -41,7 +41,7 @@ import sys
 sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
 from isa import (ACCR, ACCW, BARRIER, BRANCH, DMA, LABEL, LDS, MFMA, NOP, PERM, RFL, SALU, SMEM, SOPP,  # noqa: E402
                  TRANS, VALU, VLOAD, VSTORE, WAIT, Counters, Inst, add_waits, ar, fix_hazards, label, nop,
-                 rtxt, schedule, sr, vr)
+                 item_decode_ops, rtxt, schedule, sr, vr)
 
 BN = 64               # keys per K/V tile
 BM = 256              # query rows per workgroup
@@ -143,7 +143,8 @@ S_WD = 85         # wave + m0 / 64: a diagonal tile t is visible to this wave (u
 S_M0R = 101       # 256 m_block of the item being set up (prologue temp)
 NSGPR = 102
 
-KARG_SIZE = 184
+KARG_SIZE = 224
+DEC_OFF = 184    # fa_params.h ItemDecode (40 bytes) after FwdAsmArgs' 184
 
 # dev A/B switches, read when the .s is generated (tools/asm_variant.sh)
 OPT_NOZERO = os.environ.get("FA_GEN_NOZERO") == "1"          # never zero K/V record counts
@@ -151,6 +152,22 @@ OPT_NODIAG = os.environ.get("FA_GEN_NODIAG") == "1"          # causal diagonal: 
 OPT_PLAIN_SNAKE = os.environ.get("FA_GEN_PLAIN_SNAKE") == "1"  # snake reversal over single workgroups
 OPT_BUDGET = int(os.environ.get("FA_GEN_BUDGET", "24"))        # filler issue cycles per MFMA gap
 OPT_ZERO_NOP = int(os.environ.get("FA_GEN_ZERO_NOP", "0"))    # s_nop 15 x N before zeroing them
+OPT_SHIFT = int(os.environ.get("FA_GEN_SHIFT", "0"))          # s_nop 0 x N at the kernel entry (code placement)
+OPT_ALIGN = int(os.environ.get("FA_GEN_ALIGN", "0"))          # .p2align N before each step body (code placement)
+# dev clock / cycle stamps: every wave stores {s_memtime, s_memrealtime} at its start and end, the
+# tiles and items it ran, HW_ID, XCC_ID to the buffer passed as the `seed` kernarg (tools/fwd_stamps.py)
+OPT_STAMP = os.environ.get("FA_GEN_STAMP") in ("1", "2")
+# FA_GEN_STAMP=2 also sums, per wave, the cycles of each step's compute, its vmcnt/lgkmcnt wait and
+# its barrier wait (s_memtime around the step-end wait and barrier; perturbs the schedule a little)
+OPT_STEPSTAMP = os.environ.get("FA_GEN_STAMP") == "2"
+V_SSUM = 240      # 240..244: compute, wait, barrier sums, step count, last barrier exit
+# latency-aware gap scheduling (isa.schedule lat=): "valu,trans,lds,mfma" result latencies in cycles
+_lat = os.environ.get("FA_GEN_LAT")
+OPT_LAT = None
+if _lat:
+    _v = [int(x) for x in _lat.split(",")]
+    OPT_LAT = {VALU: _v[0], PERM: _v[0], TRANS: _v[1], LDS: _v[2], MFMA: _v[3]}
+V_STAMP = 232     # 232..237: start memtime lo / hi, realtime lo / hi, tiles, items
 # debug: at the named point, workgroup 0 stores every register of each wave (and wave 0 the LDS) to
 # the buffer whose address is passed as the `seed` kernarg, then ends (tools/asm_dump.py)
 OPT_DUMP = os.environ.get("FA_GEN_DUMP")
@@ -320,7 +337,7 @@ class K:
         for f in range(8):
             for h in range(2):
                 fx.append(self.vread(f, f % 8, h, key=-80 + 2 * f + h, earliest=max(0, NX - 18 + 2 * f) if not last else None))
-        xs = schedule(mx, fx, budget=OPT_BUDGET) if mx else schedule([], fx)
+        xs = schedule(mx, fx, budget=OPT_BUDGET, lat=OPT_LAT) if mx else schedule([], fx)
         # ---------------- phase Y
         my = []
         for i in range(NY):
@@ -393,9 +410,31 @@ class K:
                Inst(f"s_sub_u32 s{t + 2}, s{S_VOFF}, {NSLOT * TILE}", SALU, rd=sr(S_VOFF), wr=sr(t + 2) + [("scc", 0)], key=801),
                Inst(f"s_cmp_ge_u32 s{S_VOFF}, {VBASE + NSLOT * TILE}", SALU, rd=sr(S_VOFF), wr=[("scc", 0)], key=802),
                Inst(f"s_cselect_b32 s{S_VOFF}, s{t + 2}, s{S_VOFF}", SALU, rd=sr(t + 2) + sr(S_VOFF) + [("scc", 0)], wr=sr(S_VOFF), key=803)]
-        ys = schedule(my, fy, budget=OPT_BUDGET)
+        ys = schedule(my, fy, budget=OPT_BUDGET, lat=OPT_LAT)
         body = xs + ys
-        if not last:
+        if not last and OPT_STEPSTAMP:
+            A, B, t0 = S_TMP, S_TMP + 2, V_T
+            body += [Inst(f"s_add_u32 s{S_N}, s{S_N}, 1", SALU, rd=sr(S_N), wr=sr(S_N) + [("scc", 0)]),
+                     Inst(f"s_add_u32 s{S_N0}, s{S_N0}, {BN}", SALU, rd=sr(S_N0), wr=sr(S_N0) + [("scc", 0)]),
+                     Inst(f"s_memtime s[{A}:{A + 1}]", SMEM),
+                     Inst(f"s_waitcnt vmcnt({2 * NP}) lgkmcnt(0)", WAIT),
+                     Inst(f"s_memtime s[{B}:{B + 1}]", SMEM),
+                     Inst(f"v_mov_b32_e32 v{t0}, s{A}", VALU),
+                     Inst("s_waitcnt lgkmcnt(0)", WAIT),
+                     Inst(f"v_mov_b32_e32 v{t0 + 1}, s{B}", VALU),
+                     Inst("s_barrier", BARRIER),
+                     Inst(f"s_memtime s[{A}:{A + 1}]", SMEM),
+                     Inst("s_waitcnt lgkmcnt(0)", WAIT),
+                     Inst(f"v_mov_b32_e32 v{t0 + 2}, s{A}", VALU),
+                     Inst(f"v_sub_u32_e32 v{t0 + 3}, v{t0}, v{V_SSUM + 4}", VALU),
+                     Inst(f"v_add_u32_e32 v{V_SSUM}, v{V_SSUM}, v{t0 + 3}", VALU),
+                     Inst(f"v_sub_u32_e32 v{t0 + 3}, v{t0 + 1}, v{t0}", VALU),
+                     Inst(f"v_add_u32_e32 v{V_SSUM + 1}, v{V_SSUM + 1}, v{t0 + 3}", VALU),
+                     Inst(f"v_sub_u32_e32 v{t0 + 3}, v{t0 + 2}, v{t0 + 1}", VALU),
+                     Inst(f"v_add_u32_e32 v{V_SSUM + 2}, v{V_SSUM + 2}, v{t0 + 3}", VALU),
+                     Inst(f"v_add_u32_e32 v{V_SSUM + 3}, 1, v{V_SSUM + 3}", VALU),
+                     Inst(f"v_mov_b32_e32 v{V_SSUM + 4}, v{t0 + 2}", VALU)]
+        elif not last:
             # tiles <= n+3 landed in every wave (K(n+3) is prefetched in the next step's phase Y)
             body += [Inst(f"s_add_u32 s{S_N}, s{S_N}, 1", SALU, rd=sr(S_N), wr=sr(S_N) + [("scc", 0)]),
                      Inst(f"s_add_u32 s{S_N0}, s{S_N0}, {BN}", SALU, rd=sr(S_N0), wr=sr(S_N0) + [("scc", 0)]),
@@ -614,6 +653,15 @@ class K:
         ins += [I("v_lshrrev_b32_e32 v1, 6, v0", VALU, rd=vr(0), wr=vr(1)),
                 I(f"v_readfirstlane_b32 s{S_WAVE}, v1", RFL, rd=vr(1), wr=sr(S_WAVE)),
                 I(f"v_and_b32_e32 v{V_LANE}, 63, v0", VALU, rd=vr(0), wr=vr(V_LANE))]
+        if OPT_STAMP:
+            ins += [I(f"s_memtime s[{T0}:{T0 + 1}]", SMEM, wr=sr(T0, 2)),
+                    I(f"s_memrealtime s[{T0 + 2}:{T0 + 3}]", SMEM, wr=sr(T0 + 2, 2)),
+                    I("s_waitcnt lgkmcnt(0)", WAIT)]
+            ins += [I(f"v_mov_b32_e32 v{V_STAMP + i}, s{T0 + i}", VALU, rd=sr(T0 + i), wr=vr(V_STAMP + i)) for i in range(4)]
+            ins += [I(f"v_mov_b32_e32 v{V_STAMP + 4}, 0", VALU, wr=vr(V_STAMP + 4)),
+                    I(f"v_mov_b32_e32 v{V_STAMP + 5}, 0", VALU, wr=vr(V_STAMP + 5))]
+            ins += [I(f"v_mov_b32_e32 v{V_SSUM + i}, 0", VALU) for i in range(4)]
+            ins += [I(f"v_mov_b32_e32 v{V_SSUM + 4}, s{T0}", VALU)]
         # rng_state (block 0, wave 0): {seed, offset}; lanes >= 1 fall outside the 16-byte record
         l_norng = self.lab("norng")
         Prng, Pseed, Poff = A["Prng"], A["Pseed"], A["Poff"]
@@ -746,15 +794,26 @@ class K:
             ins += self.item_pos(S_SWT, 1)
             ins += [I(f"s_cmp_ge_u32 s{S_SWT}, s{S_NITEMS}", SALU), I(f"s_cbranch_scc1 {l_none}", BRANCH)]
         Psch = A["Psch"]
+        # scalars: bidb (T2), head (T3), kvh (S_N), m_block (S_N0) -- temporarily
+        BIDB, HEAD, KVH, MB = T2, T3, S_N, S_N0
+        # fixed length: computed from the item index (fa_params.h ItemDecode, dwords at DEC_OFF into
+        # s[88:97], free until the geometry below); varlen with a device-built list (flags bit 1): its
+        # entry (bidb | head << 16, kvh | m_block << 16)
+        l_tab, l_dec = self.lab("tab"), self.lab("dec")
+        ins += [I(f"s_bitcmp1_b32 s{A['FL']}, 1", SALU), I(f"s_cbranch_scc1 {l_tab}", BRANCH),
+                I(f"s_load_dwordx8 s[88:95], s[0:1], {DEC_OFF}", SMEM),
+                I(f"s_load_dwordx2 s[96:97], s[0:1], {DEC_OFF + 32}", SMEM),
+                I("s_waitcnt lgkmcnt(0)", WAIT)]
+        ins += item_decode_ops(L=S_SWT, M=88, pa=T0, pb=T2, t=S_N, u=S_M0R, o_blk=MB, reverse=True)
+        ins += [I(f"s_mov_b32 s{HEAD}, s{S_M0R}", SALU), I(f"s_mov_b32 s{KVH}, s{T0}", SALU),
+                I(f"s_branch {l_dec}", BRANCH), label(l_tab)]
         ins += [I(f"s_lshl_b32 s{T0}, s{S_SWT}, 3", SALU, rd=sr(S_SWT), wr=sr(T0)),
                 I(f"s_load_dwordx2 s[{T0}:{T1}], s[{Psch}:{Psch + 1}], s{T0}", SMEM, rd=sr(Psch, 2) + sr(T0), wr=sr(T0, 2)),
                 I("s_waitcnt lgkmcnt(0)", WAIT)]
-        # scalars: bidb (T2), head (T3), kvh (S_N), m_block (S_N0) -- temporarily
-        BIDB, HEAD, KVH, MB = T2, T3, S_N, S_N0
         ins += [I(f"s_and_b32 s{BIDB}, s{T0}, 0xffff", SALU, rd=sr(T0), wr=sr(BIDB)),
                 I(f"s_lshr_b32 s{HEAD}, s{T0}, 16", SALU, rd=sr(T0), wr=sr(HEAD)),
                 I(f"s_and_b32 s{KVH}, s{T1}, 0xffff", SALU, rd=sr(T1), wr=sr(KVH)),
-                I(f"s_lshr_b32 s{MB}, s{T1}, 16", SALU, rd=sr(T1), wr=sr(MB))]
+                I(f"s_lshr_b32 s{MB}, s{T1}, 16", SALU, rd=sr(T1), wr=sr(MB)), label(l_dec)]
         # varlen geometry (BlockInfo, block_info.h:14-31): 64-bit byte offsets (lo, hi) of row 0 of
         # this sequence in Q, O and K/V; seqlens in SQ / SK (overwritten in place)
         QOFF, OOFF, KOFF = (86, 87), (88, 89), (90, 91)
@@ -862,6 +921,9 @@ class K:
         ins += [I(f"s_max_i32 s{T0}, s{T0}, 0", SALU, rd=sr(T0), wr=sr(T0)),
                 I(f"s_add_u32 s{T0}, s{T0}, {BN - 1}", SALU, rd=sr(T0), wr=sr(T0)),
                 I(f"s_lshr_b32 s{nb}, s{T0}, 6", SALU, rd=sr(T0), wr=sr(nb))]
+        if not nxt and OPT_STAMP:
+            ins += [I(f"v_add_u32_e32 v{V_STAMP + 4}, s{S_NBLK}, v{V_STAMP + 4}", VALU),
+                    I(f"v_add_u32_e32 v{V_STAMP + 5}, 1, v{V_STAMP + 5}", VALU)]
         if not nxt:
             ins += [I(f"s_lshr_b32 s{S_WD}, s{M0R}, 6", SALU, rd=sr(M0R), wr=sr(S_WD)),
                     I(f"s_add_u32 s{S_WD}, s{S_WD}, s{S_WAVE}", SALU, rd=sr(S_WD) + sr(S_WAVE), wr=sr(S_WD)),
@@ -947,6 +1009,9 @@ class K:
         row max, P(0, a); then into the step loop"""
         I = Inst
         ins = [I(f"s_waitcnt vmcnt({2 * NP})", WAIT), I("s_barrier", BARRIER)]
+        if OPT_STEPSTAMP:
+            ins += [I(f"s_memtime s[{S_TMP}:{S_TMP + 1}]", SMEM), I("s_waitcnt lgkmcnt(0)", WAIT),
+                    I(f"v_mov_b32_e32 v{V_SSUM + 4}, s{S_TMP}", VALU)]
         ins += self.dump("pro_lds")
         ins += [I(f"v_add_u32_e32 v{V_KB0}, s{S_KOFF}, v{V_RB0}", VALU, rd=sr(S_KOFF) + vr(V_RB0), wr=vr(V_KB0)),
                 I(f"v_add_u32_e32 v{V_KB1}, s{S_KOFF}, v{V_RB1}", VALU, rd=sr(S_KOFF) + vr(V_RB1), wr=vr(V_KB1))]
@@ -1055,6 +1120,7 @@ class K:
             return out
 
         tailpad = [nop(15)]   # block entries: every predecessor ends with a barrier / branch; pad anyway
+        code += [nop(0) for _ in range(OPT_SHIFT)]
         emit_block(self.entry())
         emit_block(self.item_start(L["cold"], L["coldw"], L["warm"], L["skip"], L["tile0"], l_epi, l_end), pre=tailpad)
         code.append(label(L["tile0"]))
@@ -1123,6 +1189,28 @@ class K:
                  I(f"s_cmp_eq_u32 s{S_WARM}, 1", SALU), I(f"s_cbranch_scc1 {L['warm']}", BRANCH),
                  I(f"s_branch {L['coldw']}", BRANCH)]
         code.append(label(l_end))
+        if OPT_STAMP:
+            T0 = S_TMP
+            st = [I("s_waitcnt vmcnt(0) lgkmcnt(0)", WAIT),
+                  I(f"s_memtime s[{T0}:{T0 + 1}]", SMEM), I(f"s_memrealtime s[{T0 + 2}:{T0 + 3}]", SMEM),
+                  I("s_load_dwordx2 s[52:53], s[0:1], 0x48", SMEM),
+                  I("s_getreg_b32 s44, hwreg(HW_REG_HW_ID)", SALU), I("s_getreg_b32 s45, hwreg(HW_REG_XCC_ID)", SALU),
+                  I("s_waitcnt lgkmcnt(0)", WAIT)]
+            st += [I(f"v_mov_b32_e32 v{i}, s{T0 + i}", VALU) for i in range(4)]
+            st += [I("v_mov_b32_e32 v4, s44", VALU), I("v_mov_b32_e32 v5, s45", VALU),
+                   I("v_mov_b32_e32 v6, s2", VALU), I(f"v_mov_b32_e32 v7, s{S_WAVE}", VALU),
+                   I("s_cmp_eq_u64 s[52:53], 0", SALU), I("s_cselect_b32 s54, 0, 0x7fffffff", SALU),
+                   I("s_mov_b32 s55, 0x20000", SALU), I("s_and_b32 s53, s53, 0xffff", SALU),
+                   I("s_lshl_b32 s46, s2, 2", SALU), I(f"s_add_u32 s46, s46, s{S_WAVE}", SALU),
+                   I("s_lshl_b32 s46, s46, 7", SALU),
+                   I("v_mov_b32_e32 v8, 0", VALU), nop(4)]
+            st += [I(f"buffer_store_dwordx4 v[{V_STAMP}:{V_STAMP + 3}], v8, s[52:55], s46 offen", VSTORE),
+                   I("buffer_store_dwordx4 v[0:3], v8, s[52:55], s46 offen offset:16", VSTORE),
+                   I(f"buffer_store_dwordx2 v[{V_STAMP + 4}:{V_STAMP + 5}], v8, s[52:55], s46 offen offset:32", VSTORE),
+                   I("buffer_store_dwordx4 v[4:7], v8, s[52:55], s46 offen offset:48", VSTORE),
+                   I(f"buffer_store_dwordx4 v[{V_SSUM}:{V_SSUM + 3}], v8, s[52:55], s46 offen offset:64", VSTORE),
+                   I("s_waitcnt vmcnt(0)", WAIT)]
+            code.extend(st)
         code.append(I("s_endpgm", SOPP))
         for rb in refits:
             code.extend(rb)
@@ -1140,6 +1228,9 @@ class K:
         nm = 0
         for ins in code:
             if ins.kind == LABEL:
+                if OPT_ALIGN and any(f"_{k}" in ins.text for k in ("fast0_", "fast1_", "masked0_", "masked1_",
+                                                                     "diag0_", "diag1_", "dead0_", "dead1_")):
+                    out.append(f"\t.p2align {OPT_ALIGN}")
                 out.append(ins.text)
             else:
                 out.append("\t" + ins.text)

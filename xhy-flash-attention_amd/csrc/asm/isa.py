@@ -225,13 +225,18 @@ def add_waits(insts, ctr=None):
 # ------------------------------------------------------------------------------------------------
 # gap scheduler: fixed MFMA sequence, filler ops placed into the gaps between them
 # ------------------------------------------------------------------------------------------------
-def schedule(mfmas, fillers, budget=24, pre=(), tail_budget=None):
+def schedule(mfmas, fillers, budget=24, pre=(), tail_budget=None, lat=None):
     """Place `fillers` (Inst with deps / key / earliest / deadline) into the gaps of `mfmas`.
 
     Gap g follows MFMA g (gap -1 precedes the first MFMA).  Per gap, fillers are added in priority
     order while their issue cost fits `budget` cycles; an op is eligible once its deps are placed and
     placing it needs no wait states (checked against the instructions already emitted).  Ops whose
     deadline is the next MFMA are forced in.  What is left after the last MFMA is appended.
+
+    lat (optional): result latencies {kind: cycles}.  The scheduler then keeps an issue-time estimate
+    (fillers at their issue cost, MFMAs paced 32 cycles apart) and a ready time per register; among
+    the eligible fillers of a gap it takes, in priority order, the first whose operands are ready, and
+    only when none is, the one that stalls least (the stall counts against the gap's budget).
     """
     out = []
     hist = list(pre)
@@ -245,6 +250,27 @@ def schedule(mfmas, fillers, budget=24, pre=(), tail_budget=None):
     remaining = list(fillers)
     remaining.sort(key=lambda x: x.key)
 
+    clk = [0, -32]          # issue-time estimate, start of the last MFMA
+    ready = {}
+
+    def stall(op):
+        if lat is None:
+            return 0
+        return max([0] + [ready.get(r, 0) - clk[0] for r in op.rd])
+
+    def account(op):
+        if lat is None:
+            return
+        start = clk[0] + stall(op)
+        if op.kind == MFMA:
+            start = max(start, clk[1] + 32)
+            clk[1] = start
+        clk[0] = start + op.cost
+        lt = lat.get(op.kind)
+        if lt is not None:
+            for r in op.wr:
+                ready[r] = start + lt
+
     def eligible(op, g, force=False):
         if any(id(d) not in placed for d in op.deps):
             return False
@@ -255,6 +281,7 @@ def schedule(mfmas, fillers, budget=24, pre=(), tail_budget=None):
         return True
 
     def emit(op):
+        account(op)
         out.append(op)
         hist.append(op)
         placed.add(id(op))
@@ -287,15 +314,24 @@ def schedule(mfmas, fillers, budget=24, pre=(), tail_budget=None):
                 continue
             if cap is not None and used >= cap:
                 break
+            best = None
             for op in remaining:
                 if cap is not None and used + op.cost > cap and used > 0:
                     continue
                 if eligible(op, g):
-                    remaining.remove(op)
-                    emit(op)
-                    used += op.cost
-                    progress = True
+                    st = stall(op)
+                    if best is None or st < best[0]:
+                        best = (st, op)
+                    if st == 0:
+                        break
+            if best is not None:
+                st, op = best
+                if cap is not None and st and used + st + op.cost > cap and used > 0:
                     break
+                remaining.remove(op)
+                emit(op)
+                used += op.cost + st
+                progress = True
             if not progress:
                 break
 
@@ -319,3 +355,94 @@ def schedule(mfmas, fillers, budget=24, pre=(), tail_budget=None):
         if not progress:
             raise RuntimeError("scheduler: dependency cycle among " + ", ".join(map(str, remaining[:5])))
     return out
+
+
+# ------------------------------------------------------------------------------------------------
+# work-order decode (fa_params.h ItemDecode): item index -> (block, batch, head, kv head), in SALU
+# ------------------------------------------------------------------------------------------------
+def item_decode_ops(L, M, pa, pb, t, u, o_blk, reverse):
+    """SALU ops computing, from the item index in s[L] and the ItemDecode dwords in s[M..M+9]
+    (mag PG HP H G, div PG HP H G, shifts, xs | (nblk - 1) << 8):
+        i = L >> xs;  gi = i / PG, r = i - gi PG;  blk = r / HP, hr = r - blk HP
+        bh = ((gi HP + hr) << xs) + (L & (2^xs - 1));  bidb = bh / H, head = bh - bidb H;  kvh = head / G
+    Each q = n / d is s_mul_i32 / s_mul_hi_u32 by the magic number and one s_lshr_b64 by its shift.
+    pa, pb: even-aligned SGPR pairs, t, u: SGPRs (temporaries); s[o_blk] gets nblk - 1 - blk
+    (reverse) or blk and must not be one of pa, pb, t, u, L, M.  Results: bidb in s[pb], head in s[u],
+    kvh in s[pa]."""
+    a0, a1 = pa, pa + 1
+    b0, b1 = pb, pb + 1
+    mPG, mHP, mH, mG, dPG, dHP, dH, dG, SH, XN = (M + i for i in range(10))
+    I = Inst
+    ops = [I(f"s_and_b32 s{t}, s{XN}, 0xff", SALU),                           # xs
+           I(f"s_lshr_b32 s{u}, s{L}, s{t}", SALU),                           # i
+           I(f"s_mul_i32 s{a0}, s{u}, s{mPG}", SALU), I(f"s_mul_hi_u32 s{a1}, s{u}, s{mPG}", SALU),
+           I(f"s_lshr_b64 s[{a0}:{a1}], s[{a0}:{a1}], s{SH}", SALU),          # gi
+           I(f"s_mul_i32 s{a1}, s{a0}, s{dPG}", SALU), I(f"s_sub_u32 s{u}, s{u}, s{a1}", SALU),   # r
+           I(f"s_mul_i32 s{a0}, s{a0}, s{dHP}", SALU),                        # gi HP
+           I(f"s_lshr_b32 s{a1}, s{SH}, 8", SALU),
+           I(f"s_mul_i32 s{b0}, s{u}, s{mHP}", SALU), I(f"s_mul_hi_u32 s{b1}, s{u}, s{mHP}", SALU),
+           I(f"s_lshr_b64 s[{b0}:{b1}], s[{b0}:{b1}], s{a1}", SALU),          # blk
+           I(f"s_mul_i32 s{a1}, s{b0}, s{dHP}", SALU), I(f"s_sub_u32 s{u}, s{u}, s{a1}", SALU),   # hr
+           I(f"s_add_u32 s{a0}, s{a0}, s{u}", SALU),                          # hl
+           I(f"s_lshl_b32 s{a0}, s{a0}, s{t}", SALU),
+           I(f"s_lshl_b32 s{u}, 1, s{t}", SALU), I(f"s_sub_u32 s{u}, s{u}, 1", SALU),
+           I(f"s_and_b32 s{u}, s{L}, s{u}", SALU), I(f"s_add_u32 s{a0}, s{a0}, s{u}", SALU)]  # bh
+    if reverse:
+        ops += [I(f"s_lshr_b32 s{o_blk}, s{XN}, 8", SALU), I(f"s_sub_u32 s{o_blk}, s{o_blk}, s{b0}", SALU)]
+    else:
+        ops += [I(f"s_mov_b32 s{o_blk}, s{b0}", SALU)]
+    ops += [I(f"s_lshr_b32 s{t}, s{SH}, 16", SALU),
+            I(f"s_mul_i32 s{b0}, s{a0}, s{mH}", SALU), I(f"s_mul_hi_u32 s{b1}, s{a0}, s{mH}", SALU),
+            I(f"s_lshr_b64 s[{b0}:{b1}], s[{b0}:{b1}], s{t}", SALU),          # bidb
+            I(f"s_mul_i32 s{u}, s{b0}, s{dH}", SALU), I(f"s_sub_u32 s{u}, s{a0}, s{u}", SALU),     # head
+            I(f"s_lshr_b32 s{t}, s{SH}, 24", SALU),
+            I(f"s_mul_i32 s{a0}, s{u}, s{mG}", SALU), I(f"s_mul_hi_u32 s{a1}, s{u}, s{mG}", SALU),
+            I(f"s_lshr_b64 s[{a0}:{a1}], s[{a0}:{a1}], s{t}", SALU)]          # kvh
+    return ops
+
+
+def item_decode_ref(L, dec):
+    """Python restatement of item_decode_ops (tests): dec = the 10 ItemDecode dwords"""
+    mag, dv, sh, xn = dec[0:4], dec[4:8], dec[8], dec[9]
+    xs, nb1 = xn & 0xFF, xn >> 8
+
+    def div(n, k):
+        return ((n * mag[k]) >> ((sh >> (8 * k)) & 63)) & 0xFFFFFFFF
+    i = L >> xs
+    gi = div(i, 0)
+    r = i - gi * dv[0]
+    blk = div(r, 1)
+    hr = r - blk * dv[1]
+    bh = ((gi * dv[1] + hr) << xs) + (L & ((1 << xs) - 1))
+    bidb = div(bh, 2)
+    head = bh - bidb * dv[2]
+    return blk, nb1, bidb, head, div(head, 3)
+
+
+def magic_div(d):
+    """fa_params.h magic_div: (mag, sh) with n / d == (n * mag) >> sh for 0 <= n < 2^31"""
+    l = 0
+    while (1 << l) < d:
+        l += 1
+    return ((1 << (31 + l)) // d + 1) & 0xFFFFFFFF, 31 + l
+
+
+def make_item_decode(xs, pg, hp, h, g, nblk):
+    """fa_params.h make_item_decode: the 10 ItemDecode dwords"""
+    m = [magic_div(x) for x in (pg, hp, h, g)]
+    return [x[0] for x in m] + [pg, hp, h, g, m[0][1] | m[1][1] << 8 | m[2][1] << 16 | m[3][1] << 24,
+                                xs | (nblk - 1) << 8]
+
+
+def fwd_item_decode(nbh, h, g, nblk, hp=0):
+    """fa_params.h fwd_item_decode (forward / dQ order)"""
+    if nbh % 8 == 0 and hp > 0 and (nbh >> 3) % hp == 0:
+        return make_item_decode(3, hp * nblk, hp, h, g, nblk)
+    return make_item_decode(0, 0x7FFFFFFF, nbh, h, g, nblk)
+
+
+def dkdv_item_decode(nbh, h_grid, g, nblk):
+    """fa_params.h dkdv_item_decode (dK / dV order)"""
+    if nbh % 8 == 0:
+        return make_item_decode(3, nblk, 1, h_grid, g, nblk)
+    return make_item_decode(0, 0x7FFFFFFF, nbh, h_grid, g, nblk)

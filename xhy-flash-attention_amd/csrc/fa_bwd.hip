@@ -1198,23 +1198,21 @@ void launch_bwd(const BwdParams& p_in, bool is_bf16, hipStream_t stream) {
   p.lsed = nullptr;
   p.lsed_ng = (p.s.seqlen_q + 31) / 32;
   const bool asm_dkdv = bwd_asm_applicable(p);
-  void* ws = nullptr;
+  StreamScratch ws;
   p.lse_s = p.dq_accum;
   if (p.lse_s == nullptr || asm_dkdv) {
-    keep_pool_memory();
     const size_t bytes = asm_dkdv ? (size_t)p.s.b * p.s.h * p.lsed_ng * 64 * sizeof(float)
                                   : (size_t)p.s.b * p.s.h * p.seqlen_q_rounded * sizeof(float);
-    if (hipMallocAsync(&ws, bytes, stream) != hipSuccess)
+    if (!ws.alloc(bytes, stream))
       throw std::runtime_error("flash_attn_bwd: hipMallocAsync of the LSE scratch failed");
     if (asm_dkdv) {
-      p.lsed = static_cast<float*>(ws);
+      p.lsed = static_cast<float*>(ws.p);
       if (p.lse_s == nullptr) p.lse_s = p.lsed;   // (not read on this path)
     } else {
-      p.lse_s = static_cast<float*>(ws);
+      p.lse_s = static_cast<float*>(ws.p);
     }
   }
   if (is_bf16) launch_bwd_t<true>(p, stream); else launch_bwd_t<false>(p, stream);
-  if (ws != nullptr) (void)hipFreeAsync(ws, stream);
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) throw std::runtime_error(std::string("flash_attn_bwd launch: ") + hipGetErrorString(e));
 }

@@ -9,23 +9,23 @@
 // scratch), and the dQ kernel is unchanged.  Everything else -- and this path when it is switched
 // off (FLASH_ATTN_MI355X_BWD_ASM=0 or knob 3) -- runs bwd_dkdv_kernel (fa_bwd.hip).
 //
-// Work order: a per-shape table maps workgroup -> (batch, head, kv head, 128-key block) in the HIP
-// kernel's xcd_order (heaviest causal key block first, the blocks of one head on one XCD).
+// Work order: each workgroup computes its (batch, head, kv head, 128-key block) from its index in the
+// HIP kernel's xcd_order (heaviest causal key block first, the blocks of one head on one XCD) with
+// the magic-number divisions of fa_params.h ItemDecode: no table, no host->device copy, nothing
+// cached per shape, so a launch is graph-capturable and varlen shapes cost nothing new.
 //
 // The dQ kernel (same operand coverage; K and V must share their row and batch strides) replaces
 // bwd_dq_kernel: 256-row query blocks in the forward's work order (xcd_order_grouped with the
-// launcher's dq_head_group), reading LSE and D (softmax_d) directly.  FLASH_ATTN_MI355X_DQ_ASM=0 (or
+// launcher's dq_head_group, computed in the kernel as above), reading LSE and D (softmax_d) directly.  FLASH_ATTN_MI355X_DQ_ASM=0 (or
 // knob 4) keeps bwd_dq_kernel.
 #include <hip/hip_runtime.h>
 
+#include <cstddef>
 #include <cstdint>
 #include <cstring>
-#include <map>
 #include <mutex>
 #include <stdexcept>
 #include <string>
-#include <tuple>
-#include <vector>
 
 #include "fa_params.h"
 
@@ -49,8 +49,9 @@ struct BwdAsmArgs {
   int32_t flags;    // bit 0: varlen_padded_input, bit 1: dK / dV reduced over the GQA group
   int32_t pad;
   void* stamps;     // dev timeline buffer (a generator build with FA_GBW_STAMP=1 writes it), else unused
+  ItemDecode dec;   // the work order, computed in the kernel from the workgroup index
 };
-static_assert(sizeof(BwdAsmArgs) == 224, "BwdAsmArgs layout");
+static_assert(sizeof(BwdAsmArgs) == 264 && offsetof(BwdAsmArgs, dec) == 224, "BwdAsmArgs layout");
 
 // must match the kernarg loads of gen_dq.py (K.prologue) and KARG_SIZE
 struct DqAsmArgs {
@@ -62,8 +63,9 @@ struct DqAsmArgs {
   int32_t sq, sk, lse_pitch, dsum_pitch, h, hk;
   int32_t flags;    // bit 0: varlen_padded_input
   float c, scale;
+  ItemDecode dec;   // the work order, computed in the kernel from the workgroup index
 };
-static_assert(sizeof(DqAsmArgs) == 184, "DqAsmArgs layout");
+static_assert(sizeof(DqAsmArgs) == 224 && offsetof(DqAsmArgs, dec) == 184, "DqAsmArgs layout");
 
 constexpr int kMaxDev = 64;
 constexpr int kBkn = 128;   // keys per workgroup
@@ -71,8 +73,6 @@ struct DevModule {
   hipModule_t mod = nullptr, mod_dq = nullptr;
   hipFunction_t fn[4] = {};      // dK/dV [bf16 causal, bf16 full, f16 causal, f16 full]
   hipFunction_t fn_dq[4] = {};   // dQ, the same order
-  std::map<std::tuple<int, int, int, int>, uint32_t*> tables;
-  std::map<std::tuple<int, int, int, int, int>, uint32_t*> dq_tables;
 };
 std::mutex g_mu;
 DevModule g_dev[kMaxDev];
@@ -96,61 +96,6 @@ DevModule& module_for(int dev) {
     for (int i = 0; i < 4; ++i) check(hipModuleGetFunction(&m.fn_dq[i], m.mod_dq, kDqNames[i]), kDqNames[i]);
   }
   return m;
-}
-
-// workgroup -> (bidb | head << 16, kvh | m_block << 16): the forward's order (fa_common.h
-// xcd_order_grouped, heaviest causal query block first)
-std::vector<uint32_t> build_dq_table(int b, int h, int hk, int nmb, int hp) {
-  const int nbh = b * h;
-  const long long n = (long long)nbh * nmb;
-  std::vector<uint32_t> t((size_t)n * 2);
-  const int g = h / hk;
-  for (long long L = 0; L < n; ++L) {
-    int bh, blk;
-    if ((nbh & 7) == 0 && hp > 0 && ((nbh >> 3) % hp) == 0) {
-      const long long i = L >> 3;
-      const long long per_group = (long long)hp * nmb;
-      const long long gi = i / per_group;
-      const long long r = i - gi * per_group;
-      blk = (int)(r / hp);
-      const long long hl = gi * hp + (r - (long long)blk * hp);
-      bh = (int)(hl * 8 + (L & 7));
-    } else {
-      blk = (int)(L / nbh);
-      bh = (int)(L - (long long)blk * nbh);
-    }
-    const int mb = nmb - 1 - blk;
-    const int bidb = bh / h, head = bh - bidb * h;
-    t[2 * L] = (uint32_t)bidb | ((uint32_t)head << 16);
-    t[2 * L + 1] = (uint32_t)(head / g) | ((uint32_t)mb << 16);
-  }
-  return t;
-}
-
-// workgroup -> (bidb | hx << 16, kvh | kblock << 16): fa_common.h xcd_order over nbh = b * heads
-// of dK / dV and nblk key blocks (block 0, the longest causal sweep, first)
-std::vector<uint32_t> build_table(int b, int nh_grid, int h, int hk, int nblk, bool reduce) {
-  const long long nbh = (long long)b * nh_grid;
-  const long long n = nbh * nblk;
-  std::vector<uint32_t> t((size_t)n * 2);
-  const int g = h / hk;
-  for (long long L = 0; L < n; ++L) {
-    long long bh, blk;
-    if ((nbh & 7) == 0) {
-      const long long i = L >> 3;
-      const long long hl = i / nblk;
-      blk = i - hl * nblk;
-      bh = hl * 8 + (L & 7);
-    } else {
-      blk = L / nbh;
-      bh = L - blk * nbh;
-    }
-    const int bidb = (int)(bh / nh_grid), hx = (int)(bh - (long long)bidb * nh_grid);
-    const int kvh = reduce ? hx : hx / g;
-    t[2 * L] = (uint32_t)bidb | ((uint32_t)hx << 16);
-    t[2 * L + 1] = (uint32_t)kvh | ((uint32_t)blk << 16);
-  }
-  return t;
 }
 
 bool fits32(int64_t x) { return x >= 0 && x < (1ll << 31); }
@@ -188,27 +133,14 @@ void launch_bwd_dkdv_asm(const BwdParams& p, bool is_bf16, hipStream_t stream) {
   int dev = 0;
   check(hipGetDevice(&dev), "hipGetDevice");
   hipFunction_t fn;
-  uint32_t* table;
   {
     std::lock_guard<std::mutex> lk(g_mu);
-    DevModule& m = module_for(dev);
-    fn = m.fn[(is_bf16 ? 0 : 2) + (s.causal ? 0 : 1)];
-    const int red = p.gqa_reduce ? 1 : 0;
-    auto key = std::make_tuple(s.b, nh_grid * 2 + red, s.h * 65536 + s.hk, nblk);
-    auto it = m.tables.find(key);
-    if (it == m.tables.end()) {
-      std::vector<uint32_t> t = build_table(s.b, nh_grid, s.h, s.hk, nblk, p.gqa_reduce);
-      uint32_t* d = nullptr;
-      check(hipMalloc(&d, t.size() * sizeof(uint32_t)), "hipMalloc (schedule table)");
-      check(hipMemcpy(d, t.data(), t.size() * sizeof(uint32_t), hipMemcpyHostToDevice), "hipMemcpy (schedule table)");
-      it = m.tables.emplace(key, d).first;
-    }
-    table = it->second;
+    fn = module_for(dev).fn[(is_bf16 ? 0 : 2) + (s.causal ? 0 : 1)];
   }
   BwdAsmArgs a;
   std::memset(&a, 0, sizeof(a));
   a.q = p.q; a.k = p.k; a.v = p.v; a.dout = p.dout; a.dk = p.dk; a.dv = p.dv;
-  a.lsed = p.lsed; a.sched = table; a.cu_q = s.cu_seqlens_q; a.cu_k = s.cu_seqlens_k;
+  a.lsed = p.lsed; a.sched = nullptr; a.cu_q = s.cu_seqlens_q; a.cu_k = s.cu_seqlens_k;
   a.q_batch = 2 * p.q_batch; a.k_batch = 2 * p.k_batch; a.v_batch = 2 * p.v_batch;
   a.do_batch = 2 * p.do_batch; a.dk_batch = 2 * p.dk_batch; a.dv_batch = 2 * p.dv_batch;
   a.q_row = (int32_t)(2 * p.q_row); a.k_row = (int32_t)(2 * p.k_row); a.v_row = (int32_t)(2 * p.v_row);
@@ -221,6 +153,7 @@ void launch_bwd_dkdv_asm(const BwdParams& p, bool is_bf16, hipStream_t stream) {
   a.c = s.scale_log2; a.scale = s.scale;
   a.flags = (s.varlen_padded_input ? 1 : 0) | (p.gqa_reduce ? 2 : 0);
   a.stamps = g_stamps;
+  a.dec = dkdv_item_decode(s.b * nh_grid, nh_grid, p.gqa_reduce ? 1 : s.h / s.hk, nblk);
   size_t sz = sizeof(a);
   void* cfg[] = {HIP_LAUNCH_PARAM_BUFFER_POINTER, &a, HIP_LAUNCH_PARAM_BUFFER_SIZE, &sz, HIP_LAUNCH_PARAM_END};
   check(hipModuleLaunchKernel(fn, (unsigned)nwg, 1, 1, 256, 1, 1, 0, stream, nullptr, cfg), "hipModuleLaunchKernel");
@@ -251,26 +184,14 @@ void launch_bwd_dq_asm(const BwdParams& p, bool is_bf16, hipStream_t stream) {
   int dev = 0;
   check(hipGetDevice(&dev), "hipGetDevice");
   hipFunction_t fn;
-  uint32_t* table;
   {
     std::lock_guard<std::mutex> lk(g_mu);
-    DevModule& m = module_for(dev);
-    fn = m.fn_dq[(is_bf16 ? 0 : 2) + (s.causal ? 0 : 1)];
-    auto key = std::make_tuple(s.b, s.h, s.hk, nmb, p.dq_head_group);
-    auto it = m.dq_tables.find(key);
-    if (it == m.dq_tables.end()) {
-      std::vector<uint32_t> t = build_dq_table(s.b, s.h, s.hk, nmb, p.dq_head_group);
-      uint32_t* d = nullptr;
-      check(hipMalloc(&d, t.size() * sizeof(uint32_t)), "hipMalloc (dQ schedule table)");
-      check(hipMemcpy(d, t.data(), t.size() * sizeof(uint32_t), hipMemcpyHostToDevice), "hipMemcpy (dQ schedule table)");
-      it = m.dq_tables.emplace(key, d).first;
-    }
-    table = it->second;
+    fn = module_for(dev).fn_dq[(is_bf16 ? 0 : 2) + (s.causal ? 0 : 1)];
   }
   DqAsmArgs a;
   std::memset(&a, 0, sizeof(a));
   a.q = p.q; a.k = p.k; a.v = p.v; a.dout = p.dout; a.dq = p.dq;
-  a.lse = p.lse; a.dsum = p.dsum; a.sched = table; a.cu_q = s.cu_seqlens_q; a.cu_k = s.cu_seqlens_k;
+  a.lse = p.lse; a.dsum = p.dsum; a.sched = nullptr; a.cu_q = s.cu_seqlens_q; a.cu_k = s.cu_seqlens_k;
   a.q_batch = 2 * p.q_batch; a.kv_batch = 2 * p.k_batch; a.do_batch = 2 * p.do_batch; a.dq_batch = 2 * p.dq_batch;
   a.q_row = (int32_t)(2 * p.q_row); a.kv_row = (int32_t)(2 * p.k_row); a.do_row = (int32_t)(2 * p.do_row);
   a.dq_row = (int32_t)(2 * p.dq_row);
@@ -280,6 +201,7 @@ void launch_bwd_dq_asm(const BwdParams& p, bool is_bf16, hipStream_t stream) {
   a.h = s.h; a.hk = s.hk;
   a.flags = s.varlen_padded_input ? 1 : 0;
   a.c = s.scale_log2; a.scale = s.scale;
+  a.dec = fwd_item_decode(s.b * s.h, s.h, s.h / s.hk, nmb, p.dq_head_group);
   size_t sz = sizeof(a);
   void* cfg[] = {HIP_LAUNCH_PARAM_BUFFER_POINTER, &a, HIP_LAUNCH_PARAM_BUFFER_SIZE, &sz, HIP_LAUNCH_PARAM_END};
   check(hipModuleLaunchKernel(fn, (unsigned)nwg, 1, 1, 256, 1, 1, 0, stream, nullptr, cfg), "hipModuleLaunchKernel (dQ)");

@@ -424,19 +424,6 @@ __device__ inline void xcd_order_grouped(int L, int nbh, int nblk, int hp, int& 
   }
 }
 
-// Keep blocks freed by hipFreeAsync in the device's default pool across synchronisations, so the
-// launchers' per-call scratch (split-KV partials, backward LSE rows) does not hit the driver.
-inline void keep_pool_memory() {
-  static bool done = false;
-  if (done) return;
-  int dev = 0;
-  hipMemPool_t pool;
-  if (hipGetDevice(&dev) == hipSuccess && hipDeviceGetDefaultMemPool(&pool, dev) == hipSuccess) {
-    uint64_t thr = UINT64_MAX;
-    (void)hipMemPoolSetAttribute(pool, hipMemPoolAttrReleaseThreshold, &thr);
-  }
-  done = true;
-}
 
 // Heads per group for xcd_order_grouped on a causal grid of nbh heads x nblk blocks whose block b
 // costs ~(b + 1) units: the heaviest block (nblk units) must fit in 1/G of a CU's share of the work,

@@ -713,7 +713,7 @@ void launch_fwd(const FwdParams& p_in, bool is_bf16, hipStream_t stream) {
   // disables it (tests compare both paths).
   // GQA packing on top (decode with grouped heads): the query heads of a kv head are packed as
   // extra rows when seqlen_q * group fits one query block, so K/V are streamed once per kv head.
-  void* ws = nullptr;
+  StreamScratch ws;
   p.n_split = 0;   // 0: the ordinary launch
   p.pack_g = 1;
   {
@@ -745,17 +745,15 @@ void launch_fwd(const FwdParams& p_in, bool is_bf16, hipStream_t stream) {
       p.acc_d = (p.s.d + 31) / 32 * 32;
       const size_t rows = (size_t)p.n_split * p.s.b * p.s.h * p.s.seqlen_q;
       const size_t bytes = rows * p.acc_d * sizeof(float) + rows * sizeof(float);
-      keep_pool_memory();
-      if (hipMallocAsync(&ws, bytes, stream) != hipSuccess)
+      if (!ws.alloc(bytes, stream))
         throw std::runtime_error("flash_attn_fwd: hipMallocAsync of the split-KV scratch failed");
-      p.o_acc = static_cast<float*>(ws);
+      p.o_acc = static_cast<float*>(ws.p);
       p.lse_acc = p.o_acc + rows * p.acc_d;
     }
   }
   if (p.p_out != nullptr && (p.p_rows > 65535 * 4 || p.s.b * p.s.h > 65535))
     throw std::runtime_error("flash_attn_fwd: return_softmax grid too large");
   if (is_bf16) dispatch_fwd<true>(p, stream); else dispatch_fwd<false>(p, stream);
-  if (ws != nullptr) (void)hipFreeAsync(ws, stream);
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) throw std::runtime_error(std::string("flash_attn_fwd launch: ") + hipGetErrorString(e));
 }

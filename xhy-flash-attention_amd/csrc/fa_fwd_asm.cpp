@@ -10,20 +10,20 @@
 // and its four kernels are launched with hipModuleLaunchKernel on the caller's stream; kernel
 // arguments are one packed struct (FwdAsmArgs, the layout gen_fwd.py's prologue reads).
 //
-// Work order: a per-shape table maps workgroup -> (batch, head, kv head, query block), built on the
-// host in the HIP kernel's order (heaviest causal block first, heads fastest, xcd_order_grouped for
-// K/V streams beyond the Infinity Cache) and cached in device memory per (device, shape).
+// Work order: the kernel computes each item (batch, head, kv head, query block) from its index in the
+// HIP kernel's order (heaviest causal block first, heads fastest, xcd_order_grouped for K/V streams
+// beyond the Infinity Cache) with the magic-number divisions of fa_params.h ItemDecode -- no table,
+// no host->device copy, nothing cached per shape.  Varlen launches take a list built on the device
+// (varlen_items_kernel, below).
 #include <hip/hip_runtime.h>
 
 #include <cstdint>
 #include <cstdlib>
+#include <cstddef>
 #include <cstring>
-#include <map>
 #include <mutex>
 #include <stdexcept>
 #include <string>
-#include <tuple>
-#include <vector>
 
 #include "fa_params.h"
 
@@ -46,19 +46,20 @@ struct FwdAsmArgs {
   int32_t n_items;  // entries of the work table
   int32_t grid;     // workgroups: workgroup w runs items r G + (r odd ? G - 1 - w : w), r = 0, 1, ...
   int32_t pad;
+  ItemDecode dec;   // the work order, computed in the kernel from the item index (flags bit 1 clear)
 };
-static_assert(sizeof(FwdAsmArgs) == 184, "FwdAsmArgs layout");
+static_assert(sizeof(FwdAsmArgs) == 224 && offsetof(FwdAsmArgs, dec) == 184, "FwdAsmArgs layout");
 
 constexpr int kMaxDev = 64;
 struct DevModule {
   hipModule_t mod = nullptr;
   hipFunction_t fn[8] = {};   // d 128 then d 64: [bf16 causal, bf16 full, f16 causal, f16 full]
   int cus = 0;
-  std::map<std::tuple<int, int, int, int, int>, uint32_t*> tables;
 };
 std::mutex g_mu;
 DevModule g_dev[kMaxDev];
 int g_enabled = -1;   // -1: not read yet
+void* g_stamps = nullptr;   // flash_attn_debug_fwd_stamps (a generator build with FA_GEN_STAMP=1 writes it)
 
 const char* kNames[8] = {"fa_fwd_asm_d128_bf16_causal", "fa_fwd_asm_d128_bf16_full",
                          "fa_fwd_asm_d128_f16_causal", "fa_fwd_asm_d128_f16_full",
@@ -78,34 +79,6 @@ DevModule& module_for(int dev) {
     check(hipDeviceGetAttribute(&m.cus, hipDeviceAttributeMultiprocessorCount, dev), "hipDeviceGetAttribute");
   }
   return m;
-}
-
-// workgroup -> (bidb | head << 16, kvh | m_block << 16), the order of xcd_order_grouped (fa_common.h)
-std::vector<uint32_t> build_table(int b, int h, int hk, int nmb, int hp) {
-  const int nbh = b * h;
-  const long long n = (long long)nbh * nmb;
-  std::vector<uint32_t> t((size_t)n * 2);
-  const int g = h / hk;
-  for (long long L = 0; L < n; ++L) {
-    int bh, blk;
-    if ((nbh & 7) == 0 && hp > 0 && ((nbh >> 3) % hp) == 0) {
-      const long long i = L >> 3;
-      const long long per_group = (long long)hp * nmb;
-      const long long gi = i / per_group;
-      const long long r = i - gi * per_group;
-      blk = (int)(r / hp);
-      const long long hl = gi * hp + (r - (long long)blk * hp);
-      bh = (int)(hl * 8 + (L & 7));
-    } else {
-      blk = (int)(L / nbh);
-      bh = (int)(L - (long long)blk * nbh);
-    }
-    const int mb = nmb - 1 - blk;   // heaviest causal query block first
-    const int bidb = bh / h, head = bh - bidb * h;
-    t[2 * L] = (uint32_t)bidb | ((uint32_t)head << 16);
-    t[2 * L + 1] = (uint32_t)(head / g) | ((uint32_t)mb << 16);
-  }
-  return t;
 }
 
 bool fits32(int64_t x) { return x >= 0 && x < (1ll << 31); }
@@ -177,20 +150,17 @@ bool varlen_items_fit(int b, int nlev) {
          (2ll * b + 3ll * (nlev + 1)) * (long long)sizeof(int) <= 65536;
 }
 
-uint32_t* build_varlen_items(const int* cu, int b, int nh, int gdiv, int rows, int nlev, bool reverse,
-                             long long max_items, hipStream_t stream) {
-  uint32_t* tab = nullptr;
-  check(hipMallocAsync(reinterpret_cast<void**>(&tab), (size_t)(2 * max_items + 2) * sizeof(uint32_t), stream),
-        "hipMallocAsync (varlen work list)");
+uint32_t* build_varlen_items(StreamScratch& buf, const int* cu, int b, int nh, int gdiv, int rows, int nlev,
+                             bool reverse, long long max_items, hipStream_t stream) {
+  if (!buf.alloc((size_t)(2 * max_items + 2) * sizeof(uint32_t), stream))
+    throw std::runtime_error("flash_attn_fwd (asm path): hipMallocAsync (varlen work list) failed");
+  uint32_t* tab = static_cast<uint32_t*>(buf.p);
   const size_t shm = (size_t)(2 * b + 3 * (nlev + 1)) * sizeof(int);
   hipLaunchKernelGGL(varlen_items_kernel, dim3(1), dim3(1024), shm, stream, cu, b, nh, gdiv, rows, nlev,
                      reverse ? 1 : 0, tab);
   check(hipGetLastError(), "varlen_items_kernel");
   return tab;
 }
-
-namespace {
-}  // namespace
 
 void fwd_asm_enable(int on) {
   std::lock_guard<std::mutex> lk(g_mu);
@@ -233,41 +203,30 @@ bool launch_fwd_asm(const FwdParams& p, bool is_bf16, hipStream_t stream) {
   // blocks past each sequence); the XCD-grouped order (head_group > 0) is built for one item per
   // workgroup and keeps G = items.
   hipFunction_t fn;
-  uint32_t* table = nullptr;
   int cus = 0;
   const bool persist = knob(kKnobFwdPersist) != 0 && p.head_group == 0;
-  const bool dev_list = persist && s.cu_seqlens_q != nullptr && varlen_items_fit(s.b, p.num_m_blocks);
+  // (the list kernel indexes its entries with int: at most 2^28 items)
+  const bool dev_list = persist && s.cu_seqlens_q != nullptr && varlen_items_fit(s.b, p.num_m_blocks) &&
+                        nwg <= (1ll << 28);
   {
     std::lock_guard<std::mutex> lk(g_mu);
     DevModule& m = module_for(dev);
     fn = m.fn[(s.d == 64 ? 4 : 0) + (is_bf16 ? 0 : 2) + (s.causal ? 0 : 1)];
     cus = m.cus;
-    if (!dev_list) {   // host table, cached per shape
-      auto key = std::make_tuple(s.b, s.h, s.hk, p.num_m_blocks, p.head_group);
-      auto it = m.tables.find(key);
-      if (it == m.tables.end()) {
-        std::vector<uint32_t> t = build_table(s.b, s.h, s.hk, p.num_m_blocks, p.head_group);
-        uint32_t* d = nullptr;
-        check(hipMalloc(&d, t.size() * sizeof(uint32_t)), "hipMalloc (schedule table)");
-        check(hipMemcpy(d, t.data(), t.size() * sizeof(uint32_t), hipMemcpyHostToDevice), "hipMemcpy (schedule table)");
-        it = m.tables.emplace(key, d).first;
-      }
-      table = it->second;
-    }
   }
-  uint32_t* vtab = nullptr;   // device-built varlen work list (stream-ordered allocation)
-  if (dev_list) {
-    vtab = build_varlen_items(s.cu_seqlens_q, s.b, s.h, s.h / s.hk, 256, p.num_m_blocks, false, nwg, stream);
-    table = vtab;
-  }
+  StreamScratch vbuf;          // device-built varlen work list (stream-ordered allocation)
+  uint32_t* vtab = dev_list ? build_varlen_items(vbuf, s.cu_seqlens_q, s.b, s.h, s.h / s.hk, 256, p.num_m_blocks,
+                                                 false, nwg, stream)
+                            : nullptr;
   long long grid = nwg;
   if (persist && cus > 0 && nwg > cus && (dev_list || s.cu_seqlens_q == nullptr)) grid = cus;
   FwdAsmArgs a;
   std::memset(&a, 0, sizeof(a));
   a.q = p.q; a.k = p.k; a.v = p.v; a.o = p.o; a.lse = p.lse;
-  a.sched = table;
+  a.sched = vtab;
   a.cu_q = s.cu_seqlens_q; a.cu_k = s.cu_seqlens_k;
   a.rng = p.rng_state; a.seed = p.seed; a.offset = p.offset;
+  if (g_stamps != nullptr) a.seed = (uint64_t)(uintptr_t)g_stamps;   // dev stamp build only
   a.q_batch = 2 * p.q_batch; a.k_batch = 2 * p.k_batch; a.v_batch = 2 * p.v_batch; a.o_batch = 2 * p.o_batch;
   a.q_row = (int32_t)q_row; a.kv_row = (int32_t)kv_row; a.o_row = (int32_t)o_row;
   a.q_head = (int32_t)q_head; a.k_head = (int32_t)k_head; a.v_head = (int32_t)v_head; a.o_head = (int32_t)o_head;
@@ -276,10 +235,10 @@ bool launch_fwd_asm(const FwdParams& p, bool is_bf16, hipStream_t stream) {
   a.flags = (s.varlen_padded_input ? 1 : 0) | (vtab != nullptr ? 2 : 0);
   a.n_items = (int32_t)nwg;
   a.grid = (int32_t)grid;
+  a.dec = fwd_item_decode(s.b * s.h, s.h, s.h / s.hk, p.num_m_blocks, p.head_group);
   size_t sz = sizeof(a);
   void* cfg[] = {HIP_LAUNCH_PARAM_BUFFER_POINTER, &a, HIP_LAUNCH_PARAM_BUFFER_SIZE, &sz, HIP_LAUNCH_PARAM_END};
   check(hipModuleLaunchKernel(fn, (unsigned)grid, 1, 1, 256, 1, 1, 0, stream, nullptr, cfg), "hipModuleLaunchKernel");
-  if (vtab != nullptr) check(hipFreeAsync(vtab, stream), "hipFreeAsync (varlen work list)");
   return true;
 }
 
@@ -288,6 +247,9 @@ bool launch_fwd_asm(const FwdParams& p, bool is_bf16, hipStream_t stream) {
 // Test / A-B hook: 0 routes every forward to fwd_kernel (HIP), 1 lets launch_fwd use the assembly
 // kernel where it applies (the default; FLASH_ATTN_MI355X_FWD_ASM=0 sets 0 at the first launch).
 extern "C" void flash_attn_fwd_use_asm(int on) { fa::fwd_asm_enable(on); }
+// Dev hook: the clock / cycle stamp buffer of a stamp build of the forward (tools/fwd_stamps.py);
+// NULL off.  It travels in the `seed` kernarg (the assembly path has no dropout).
+extern "C" void flash_attn_debug_fwd_stamps(void* buf) { fa::g_stamps = buf; }
 // Test / A-B hook: 0 (default) runs the backward's dQ kernel after dK/dV on the caller's stream,
 // 1..3 overlap them on two streams (fa_bwd.hip run_bwd lists the modes).
 extern "C" void flash_attn_bwd_overlap(int mode) { fa::bwd_overlap_enable(mode); }

@@ -139,15 +139,16 @@ struct RotaryParams {
 
 // Host launchers (fa_fwd.hip / fa_bwd.hip).  Throw std::runtime_error on invalid configuration.
 void launch_fwd(const FwdParams& p, bool is_bf16, hipStream_t stream);
-// fa_fwd_asm.cpp: the assembly forward (d = 128, no dropout / mask); false when it does not apply
+// fa_fwd_asm.cpp: the assembly forward (d = 128 or 64, no dropout / mask / split-KV); false when it
+// does not apply
 bool launch_fwd_asm(const FwdParams& p, bool is_bf16, hipStream_t stream);
 void fwd_asm_enable(int on);
 void launch_bwd(const BwdParams& p, bool is_bf16, hipStream_t stream);
-void bwd_overlap_enable(int mode);
+void bwd_overlap_enable(int mode);                                  // fa_bwd.hip: dQ / dK-dV stream overlap mode (default 0: off)
 bool bwd_asm_applicable(const BwdParams& p);                        // fa_bwd_asm.cpp
 void launch_bwd_dkdv_asm(const BwdParams& p, bool is_bf16, hipStream_t stream);
 bool dq_asm_applicable(const BwdParams& p);                         // fa_bwd_asm.cpp
-void launch_bwd_dq_asm(const BwdParams& p, bool is_bf16, hipStream_t stream);   // fa_bwd.hip: dQ / dK-dV stream overlap mode (default 0: off)
+void launch_bwd_dq_asm(const BwdParams& p, bool is_bf16, hipStream_t stream);
 void launch_reduced_scores(const ReducedParams& p, bool is_bf16, hipStream_t stream);
 void launch_rotary(const RotaryParams& p, bool interleaved, bool conj, bool is_bf16, hipStream_t stream);
 
@@ -174,10 +175,96 @@ enum Knob { kKnobNoSplitKv = 0 /* FLASH_ATTN_MI355X_NO_SPLITKV: 1 = never split 
 int knob(int id);
 void set_knob(int id, int value);
 
+// Work order of the assembly kernels, computed in the kernel from the workgroup's item index L (no
+// table, no host->device copy, nothing cached per shape: graph-capturable, the reference's launch
+// path makes no copies either, flash_bwd_launch_template.h:49-88).  The orders are fa_common.h's:
+//   i = L >> xs, lo = L & (2^xs - 1);  gi = i / PG, r = i % PG;  blk = r / HP, hr = r % HP;
+//   bh = ((gi HP + hr) << xs) + lo;  bidb = bh / H, head = bh % H;  kvh = head / G
+// forward / dQ (xcd_order_grouped, heaviest causal block first): xs = 3, PG = hp nblk, HP = hp when
+// the heads group per XCD, else xs = 0, PG = 2^31 - 1, HP = b h (block-major, heads fastest); the
+// query block is nblk - 1 - blk.  dK / dV (xcd_order: the key blocks of a head on one XCD):
+// xs = 3, PG = nblk, HP = 1 when b h % 8 == 0, else as the forward's head-fastest form; block = blk.
+// Each division is a multiply-high by a host-computed magic number, exact for 0 <= n < 2^31
+// (Granlund-Montgomery): q = (n * mag) >> sh with sh = 31 + ceil(log2 d), mag = 2^sh / d + 1.
+struct MagicDiv {
+  uint32_t mag, sh;
+};
+inline MagicDiv magic_div(uint32_t d) {
+  uint32_t l = 0;
+  while ((1ull << l) < d) ++l;
+  return {(uint32_t)((1ull << (31 + l)) / d + 1), 31 + l};
+}
+// kernarg tail of the three assembly kernels (40 bytes; gen_*.py item_decode_ops)
+struct ItemDecode {
+  uint32_t mag[4];   // PG, HP, H, G
+  uint32_t div[4];
+  uint32_t shifts;   // sh(PG) | sh(HP) << 8 | sh(H) << 16 | sh(G) << 24
+  uint32_t xs_nb1;   // xs | (nblk - 1) << 8
+};
+static_assert(sizeof(ItemDecode) == 40, "ItemDecode layout");
+inline ItemDecode make_item_decode(int xs, uint32_t pg, uint32_t hp, uint32_t h, uint32_t g, int nblk) {
+  ItemDecode d;
+  const uint32_t dv[4] = {pg, hp, h, g};
+  d.shifts = 0;
+  for (int i = 0; i < 4; ++i) {
+    const MagicDiv m = magic_div(dv[i]);
+    d.mag[i] = m.mag;
+    d.div[i] = dv[i];
+    d.shifts |= m.sh << (8 * i);
+  }
+  d.xs_nb1 = (uint32_t)xs | ((uint32_t)(nblk - 1) << 8);
+  return d;
+}
+// the forward / dQ order over nbh = b h (query) heads and nblk query blocks, hp heads per XCD group
+// (0: head-fastest); the dK / dV order over nbh = b heads_grid and nblk key blocks
+inline ItemDecode fwd_item_decode(int nbh, int h, int g, int nblk, int hp) {
+  if ((nbh & 7) == 0 && hp > 0 && ((nbh >> 3) % hp) == 0)
+    return make_item_decode(3, (uint32_t)hp * (uint32_t)nblk, (uint32_t)hp, (uint32_t)h, (uint32_t)g, nblk);
+  return make_item_decode(0, 0x7fffffffu, (uint32_t)nbh, (uint32_t)h, (uint32_t)g, nblk);
+}
+inline ItemDecode dkdv_item_decode(int nbh, int h_grid, int g, int nblk) {
+  if ((nbh & 7) == 0) return make_item_decode(3, (uint32_t)nblk, 1u, (uint32_t)h_grid, (uint32_t)g, nblk);
+  return make_item_decode(0, 0x7fffffffu, (uint32_t)nbh, (uint32_t)h_grid, (uint32_t)g, nblk);
+}
+
+// Keep blocks freed by hipFreeAsync in the device's default pool across synchronisations, so the
+// launchers' per-call scratch (split-KV partials, backward LSE rows, varlen work lists) does not hit
+// the driver (once per device).
+inline void keep_pool_memory() {
+  static bool done[64] = {};
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64 || done[dev]) return;
+  hipMemPool_t pool;
+  if (hipDeviceGetDefaultMemPool(&pool, dev) == hipSuccess) {
+    uint64_t thr = UINT64_MAX;
+    (void)hipMemPoolSetAttribute(pool, hipMemPoolAttrReleaseThreshold, &thr);
+  }
+  done[dev] = true;
+}
+
+// A stream-ordered scratch allocation, freed on its stream when it leaves scope -- also when a
+// launch in between throws.
+struct StreamScratch {
+  void* p = nullptr;
+  hipStream_t s = nullptr;
+  StreamScratch() = default;
+  StreamScratch(const StreamScratch&) = delete;
+  StreamScratch& operator=(const StreamScratch&) = delete;
+  ~StreamScratch() {
+    if (p != nullptr) (void)hipFreeAsync(p, s);
+  }
+  // allocates `bytes` on `stream`; false on failure (the caller throws)
+  bool alloc(size_t bytes, hipStream_t stream) {
+    keep_pool_memory();
+    s = stream;
+    return hipMallocAsync(&p, bytes, stream) == hipSuccess;
+  }
+};
+
 // Varlen work lists built on the device (fa_fwd_asm.cpp varlen_items_kernel): stream-ordered
-// allocation of 2 max_items + 2 dwords, [count, 0, entries...]; the caller frees it with hipFreeAsync.
+// allocation (in `buf`, freed when it leaves scope) of 2 max_items + 2 dwords, [count, 0, entries...].
 bool varlen_items_fit(int b, int nlev);
-uint32_t* build_varlen_items(const int* cu, int b, int nh, int gdiv, int rows, int nlev, bool reverse,
-                             long long max_items, hipStream_t stream);
+uint32_t* build_varlen_items(StreamScratch& buf, const int* cu, int b, int nh, int gdiv, int rows, int nlev,
+                             bool reverse, long long max_items, hipStream_t stream);
 
 }  // namespace fa
