@@ -115,3 +115,86 @@ def test_lds_dma_preceded_by_five_wait_states():
     assert n_dma > 0, "no LDS-DMA found: disassembly format changed?"
     assert not bad, f"{len(bad)} LDS-DMA without the s_nop 4 guard, e.g. {bad[:3]}"
     assert not window, f"VALU SGPR writes inside the hazard window: {window[:3]}"
+
+
+# ------------------------------------------------------------------------------------------------
+# the assembly kernels (csrc/asm/gen_*.py), re-checked by a hazard table that shares no code with
+# the generators' wait-state inserter (csrc/asm/isa.py): tools/hazard_check.py
+# ------------------------------------------------------------------------------------------------
+sys_path_tools = os.path.join(ROOT, "tools")
+
+PLANTED = """
+	.amdgcn_target "amdgcn-amd-amdhsa--gfx950"
+	.text
+	.globl fa_fwd_asm_planted
+	.p2align 8
+	.type fa_fwd_asm_planted,@function
+fa_fwd_asm_planted:
+	v_cvt_pk_bf16_f32 v0, v1, v2
+	v_mfma_f32_32x32x16_bf16 v[16:31], v[0:3], v[4:7], 0
+	s_nop 15
+	v_cvt_pk_bf16_f32 v0, v1, v2
+	s_nop 1
+	v_mfma_f32_32x32x16_bf16 a[0:15], v[0:3], v[4:7], 0
+	v_mfma_f32_32x32x16_bf16 a[0:15], v[0:3], v[4:7], a[0:15]
+	s_nop 10
+	v_accvgpr_read_b32 v40, a15
+	s_nop 15
+	s_mov_b32 m0, s5
+	buffer_load_dwordx4 v1, s[8:11], 0 offen lds
+	v_readfirstlane_b32 s8, v3
+	s_nop 2
+	buffer_load_dwordx4 v1, s[8:11], 0 offen lds
+	v_exp_f32_e32 v9, v9
+	v_add_f32_e32 v10, v9, v10
+	v_mov_b32_e32 v50, v51
+	s_cbranch_scc1 .Lt
+	s_nop 15
+	s_nop 15
+.Lt:
+	v_mfma_f32_32x32x16_bf16 v[60:75], v[50:53], v[4:7], 0
+	s_endpgm
+.Lend:
+	.size fa_fwd_asm_planted, .Lend-fa_fwd_asm_planted
+"""
+
+
+def test_hazard_checker_catches_planted_hazards(tmp_path):
+    """every rule of the independent checker fires on a planted violation -- the last one only
+    along the taken branch (the fall-through path is padded)"""
+    import sys
+    sys.path.insert(0, sys_path_tools)
+    import hazard_check as hc
+
+    if not os.path.exists(OBJDUMP):
+        pytest.skip("llvm-objdump missing")
+    src, obj = tmp_path / "t.s", tmp_path / "t.o"
+    src.write_text(PLANTED)
+    subprocess.run(["/opt/rocm/lib/llvm/bin/clang", "-x", "assembler", "-target", "amdgcn-amd-amdhsa",
+                    "-mcpu=gfx950", "-c", str(src), "-o", str(obj)], check=True)
+    txt = subprocess.run([OBJDUMP, "-d", "--mcpu=gfx950", str(obj)], capture_output=True, text=True, check=True).stdout
+    (name, ins), = hc.parse(txt).items()
+    bad = hc.check_kernel(name, ins)
+    rules = sorted({b.split("rule ")[1].split()[0] for b in bad})
+    assert rules == sorted(["valu->mfma", "mfma->access", "m0->lds_dma", "valu_sgpr->vmem", "trans->valu"]), bad
+    # the chained accumulation (C == D) is not a violation; the branch path is
+    assert not any("a[0:15], v[0:3], v[4:7], a[0:15]` 0" in b for b in bad)
+    assert any("v[60:75]" in b for b in bad)
+
+
+def test_shipped_assembly_kernels_hazard_free():
+    """every kernel of the three embedded code objects, every control-flow path"""
+    import sys
+    sys.path.insert(0, sys_path_tools)
+    import hazard_check as hc
+
+    if not os.path.exists(LIB) or not os.path.exists(OBJDUMP):
+        pytest.skip("library not built or llvm-objdump missing")
+    res = hc.check_library(LIB)
+    names = sorted(res)
+    assert len([n for n in names if n.startswith("fa_fwd_asm_")]) == 8, names
+    assert len([n for n in names if n.startswith("fa_bwd_dkdv_asm_")]) == 4, names
+    assert len([n for n in names if n.startswith("fa_bwd_dq_asm_")]) == 4, names
+    for n, (count, bad) in res.items():
+        assert count > 1000, (n, count)
+        assert not bad, f"{n}: {len(bad)} violations, e.g. {bad[:3]}"
