@@ -27,7 +27,7 @@ def main(path, b=4, s=8192, h=16):
     lib.flash_attn_debug_bwd_stamps.argtypes = [ctypes.c_void_p]
     m._lib = lib
     nwg = b * h * (s // 128)
-    buf = torch.zeros(nwg * 8, dtype=torch.int32, device="cuda")
+    buf = torch.zeros(nwg * 16, dtype=torch.int32, device="cuda")
     q, k, v, do = (torch.randn(b, s, h, 128, device="cuda", dtype=torch.bfloat16) for _ in range(4))
     scale = 128 ** -0.5
     res = m.fwd(q, k, v, None, 0.0, scale, True, False, None)
@@ -36,7 +36,7 @@ def main(path, b=4, s=8192, h=16):
         m.bwd(do, q, k, v, res[0], res[5], None, None, None, 0.0, scale, True, None, res[7])
         torch.cuda.synchronize()
     lib.flash_attn_debug_bwd_stamps(ctypes.c_void_p(0))
-    a = buf.cpu().numpy().view(np.uint32).reshape(nwg, 8)
+    a = buf.cpu().numpy().view(np.uint32).reshape(nwg, 16)
     start = a[:, 0].astype(np.int64) | (a[:, 1].astype(np.int64) << 32)
     end = a[:, 5].astype(np.int64) | (a[:, 6].astype(np.int64) << 32)
     hwid, xcc = a[:, 2], a[:, 3]
@@ -63,6 +63,12 @@ def main(path, b=4, s=8192, h=16):
     # report the distribution)
     d = end - start
     print("WG duration percentiles (ticks): " + ", ".join(f"p{p} {np.percentile(d, p):.0f}" for p in (1, 10, 50, 90, 99)))
+    loop = a[:, 8].astype(np.int64) | (a[:, 9].astype(np.int64) << 32)
+    epi = a[:, 10].astype(np.int64) | (a[:, 11].astype(np.int64) << 32)
+    ok = (loop > 0) & (epi > 0)
+    pro_t, epi_t = (loop - start)[ok], (end - epi)[ok]
+    print(f"prologue (start -> first step) median {np.median(pro_t):.0f} ticks, epilogue median {np.median(epi_t):.0f};"
+          f" per CU {np.sum(pro_t) / len(busy) / span:.3f} / {np.sum(epi_t) / len(busy) / span:.3f} of the span")
 
 
 if __name__ == "__main__":

@@ -139,7 +139,8 @@ OPT_LEAD = int(os.environ.get("FA_GBW_LEAD", "2"))    # ... and at least LEAD MF
 # dev timeline: every workgroup stores {start, end} s_memtime, HW_ID, XCC_ID, id at the `stamps`
 # kernarg address + 32 id (tools/bwd_stamps.py)
 OPT_STAMP = os.environ.get("FA_GBW_STAMP") == "1"
-V_STAMP = 164          # 164..167: start lo / hi, HW_ID, XCC_ID (with OPT_STAMP)
+V_STAMP = 164          # 164..177: start lo / hi, HW_ID, XCC_ID, wg, end lo / hi, wave, -, -, loop start lo / hi,
+                       # epilogue start lo / hi (with OPT_STAMP)
 
 
 class K:
@@ -745,6 +746,9 @@ class K:
         # wait: Q / dO(0) (phase -1), Q / dO(1) (its tail prefetches fragments of 1), LSE / D(0, 1)
         # landed; younger than Q / dO(1): L3, Q2, L4, Q3, L5, Q4, L6, Q5, L7 = 21
         pro += [Inst("s_waitcnt vmcnt(21)", WAIT), Inst("s_barrier", BARRIER)]
+        if OPT_STAMP:
+            pro += [Inst(f"s_memtime s[{S_TMP + 1}:{S_TMP + 2}]", SMEM), Inst("s_waitcnt lgkmcnt(0)", WAIT),
+                    Inst(f"v_mov_b32_e32 v{V_STAMP + 10}, s{S_TMP + 1}", VALU), Inst(f"v_mov_b32_e32 v{V_STAMP + 11}, s{S_TMP + 2}", VALU)]
         emit(pro)
         # phase -1: chain starts of subtiles 0 (-> buffers 0) and 1 (-> 1), S / dP(0)
         ph = [Inst(f"s_mov_b32 s{S_SROW}, 0", SALU, wr=sr(S_SROW)),
@@ -808,7 +812,12 @@ class K:
         code.append(label(l_tail))
         emit(self.tail(), pre=pad)
         code.append(label(l_epi))
-        emit([nop(15)] + self.epilogue(), pre=pad)
+        stamp_epi = []
+        if OPT_STAMP:
+            stamp_epi = [Inst(f"s_memtime s[{S_TMP + 1}:{S_TMP + 2}]", SMEM), Inst("s_waitcnt lgkmcnt(0)", WAIT),
+                         Inst(f"v_mov_b32_e32 v{V_STAMP + 12}, s{S_TMP + 1}", VALU),
+                         Inst(f"v_mov_b32_e32 v{V_STAMP + 13}, s{S_TMP + 2}", VALU)]
+        emit([nop(15)] + stamp_epi + self.epilogue(), pre=pad)
         code.append(label(self.lab_end))
         if OPT_STAMP:
             I = Inst
@@ -821,9 +830,10 @@ class K:
                   I("s_cmp_eq_u64 s[52:53], 0", SALU), I("s_cselect_b32 s54, 0, 0x7fffffff", SALU),
                   I("s_mov_b32 s55, 0x20000", SALU),
                   I("s_and_b32 s53, s53, 0xffff", SALU),
-                  I(f"v_lshlrev_b32_e32 v{V_STAMP + 8}, 5, v{V_STAMP + 4}", VALU), nop(4),
+                  I(f"v_lshlrev_b32_e32 v{V_STAMP + 8}, 6, v{V_STAMP + 4}", VALU), nop(4),
                   I(f"buffer_store_dwordx4 v[{V_STAMP}:{V_STAMP + 3}], v{V_STAMP + 8}, s[52:55], 0 offen", VSTORE),
                   I(f"buffer_store_dwordx4 v[{V_STAMP + 4}:{V_STAMP + 7}], v{V_STAMP + 8}, s[52:55], 0 offen offset:16", VSTORE),
+                  I(f"buffer_store_dwordx4 v[{V_STAMP + 10}:{V_STAMP + 13}], v{V_STAMP + 8}, s[52:55], 0 offen offset:32", VSTORE),
                   I("s_waitcnt vmcnt(0)", WAIT)]
             code.extend(st)
         code.append(Inst("s_endpgm", SOPP))
