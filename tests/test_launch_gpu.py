@@ -94,7 +94,14 @@ def test_graph_capture_varlen_fwd_bwd_bitwise():
     for _ in range(2):
         g.replay()
     torch.cuda.synchronize()
+    # softmax_lse is (b, h, max_seqlen): rows past a sequence's length are never written (the
+    # reference allocates it with torch::empty as well), so only the written rows are compared
+    valid = torch.zeros(len(lens), 1, max(lens), dtype=torch.bool, device="cuda")
+    for i, n in enumerate(lens):
+        valid[i, :, :n] = True
     for name, a, e in zip(("out", "lse", "dq", "dk", "dv"), outs, eager):
+        if name == "lse":
+            a, e = a.masked_select(valid), e.masked_select(valid)
         assert torch.equal(a, e), name
 
 

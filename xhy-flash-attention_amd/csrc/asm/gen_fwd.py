@@ -263,13 +263,15 @@ class K:
             ops.append(Inst(f"v_fma_f32 v{reg}, v{reg}, s{S_C}, v{V_NEGMC[j]}", VALU, rd=vr(reg) + sr(S_C) + vr(V_NEGMC[j]),
                             wr=vr(reg), key=k + kk + 1))
             ops.append(Inst(f"v_exp_f32_e32 v{reg}, v{reg}", TRANS, rd=vr(reg), wr=vr(reg), key=k + kk + 2))
-            if e == 0:
-                a = Inst(f"v_mov_b32_e32 v{V_PS[j]}, v{reg}", VALU, rd=vr(reg), wr=vr(V_PS[j]), key=k + kk + 3)
-            else:
+            if e == 1:    # (p1 + p0: the first two terms in one add, no copy of p0)
+                a = Inst(f"v_add_f32_e32 v{V_PS[j]}, v{reg}, v{reg - 1}", VALU, rd=vr(reg) + vr(reg - 1),
+                         wr=vr(V_PS[j]), key=k + kk + 3)
+            elif e > 1:
                 a = Inst(f"v_add_f32_e32 v{V_PS[j]}, v{reg}, v{V_PS[j]}", VALU, rd=vr(reg) + vr(V_PS[j]),
                          wr=vr(V_PS[j]), key=k + kk + 3)
-            last_sum = a
-            ops.append(a)
+            if e > 0:
+                last_sum = a
+                ops.append(a)
             if e % 2 == 1:
                 kkf = 2 * st + (g >> 3)
                 w = (g & 7) >> 1
