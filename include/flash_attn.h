@@ -422,11 +422,12 @@ void flash_attn_timing_read(int kernel_id, double * total_ms, long * count);
  * 2 XCD head-grouping threshold in MiB of streamed K/V (FLASH_ATTN_MI355X_XCD_GROUP_MIN_MIB,
  * default 256), 3 / 4 assembly dK/dV / dQ kernels (FLASH_ATTN_MI355X_BWD_ASM / _DQ_ASM, default 1),
  * 5 persistent assembly forward, one workgroup per CU walking the item list
- * (FLASH_ATTN_MI355X_FWD_PERSIST, default 1; 0 = one workgroup per item).  Each is read from its
+ * (FLASH_ATTN_MI355X_FWD_PERSIST, default 1; 0 = one workgroup per item), 6 the same for the
+ * assembly dK/dV and dQ kernels (FLASH_ATTN_MI355X_BWD_PERSIST, default 1).  Each is read from its
  * environment variable once, at first use. */
 void flash_attn_set_knob(int id, int value);
 int flash_attn_get_knob(int id);
-/* 0 routes every forward to the HIP kernel, 1 (default) lets head dim 128 take the assembly
+/* 0 routes every forward to the HIP kernel, 1 (default) lets head dim 128 and 64 take the assembly
  * kernel (FLASH_ATTN_MI355X_FWD_ASM=0 sets 0). */
 void flash_attn_fwd_use_asm(int on);
 /* Backward dQ / dK-dV stream overlap: 0 (default) serial on the caller's stream, 1 dQ on a second

@@ -42,6 +42,18 @@ def test_asm_dkdv_in_emulator(asm_text, b, sq, sk, h, hk, causal, bf16, reduce):
     assert ek <= tol and ev <= tol, (ek, ev)
 
 
+@pytest.mark.timeout(900)
+@pytest.mark.parametrize("b,sq,sk,h,hk,causal,reduce,grid", [
+    (1, 200, 300, 2, 1, True, True, 1),      # one workgroup walks all 3 key blocks (+ causal skips)
+    (2, 150, 130, 4, 2, False, False, 3),    # 16 items over 3 workgroups, snake rounds
+    (1, 100, 260, 8, 8, True, False, 8),     # G % 8 == 0: reversal over groups of 8; empty items
+])
+def test_asm_dkdv_persistent_loop(asm_text, b, sq, sk, h, hk, causal, reduce, grid):
+    """the persistent item loop (fa_bwd_asm.cpp, knob 6): fewer workgroups than items"""
+    ek, ev, *_ = emu_bwd.run(b, sq, sk, h, hk, causal, True, reduce, seed=3, text=asm_text, verbose=False, grid=grid)
+    assert ek <= 1e-2 and ev <= 1e-2, (ek, ev)
+
+
 def test_generated_dkdv_kernels_are_hazard_free():
     spec = importlib.util.spec_from_file_location(
         "asm_isa", os.path.join(ROOT, "xhy-flash-attention_amd", "csrc", "asm", "isa.py"))
@@ -85,6 +97,17 @@ def test_asm_dq_in_emulator(dq_text, b, sq, sk, h, hk, causal, bf16):
     import emu_dq
     e, *_ = emu_dq.run(b, sq, sk, h, hk, causal, bf16, seed=0, text=dq_text, verbose=False)
     assert e <= (1e-2 if bf16 else 2e-3), e
+
+
+@pytest.mark.timeout(900)
+@pytest.mark.parametrize("b,sq,sk,h,hk,causal,grid", [
+    (1, 600, 600, 2, 1, True, 1),       # one workgroup walks 6 items (3 query blocks x 2 heads)
+    (2, 300, 200, 4, 2, False, 3),      # 16 items over 3 workgroups, snake rounds
+])
+def test_asm_dq_persistent_loop(dq_text, b, sq, sk, h, hk, causal, grid):
+    import emu_dq
+    e, *_ = emu_dq.run(b, sq, sk, h, hk, causal, True, seed=4, text=dq_text, verbose=False, grid=grid)
+    assert e <= 1e-2, e
 
 
 def test_generated_dq_kernels_assemble_shape():

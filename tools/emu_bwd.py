@@ -36,7 +36,8 @@ def pack_args(**kw):
     out += struct.pack("<6i", kw["sq"], kw["sk"], kw["h"], kw["ng"], kw["nh"], kw["group"])
     out += struct.pack("<ffiiQ", kw["c"], kw["scale"], kw["flags"], 0, 0)
     out += struct.pack("<10I", *kw["dec"])
-    assert len(out) == 264, len(out)
+    out += struct.pack("<ii", kw["n_items"], kw["grid"])
+    assert len(out) == 272, len(out)
     return out
 
 
@@ -71,7 +72,9 @@ def reference(q, k, v, do, causal, scale):
     return lse, dsum, dk, dv
 
 
-def run(b=1, sq=200, sk=200, h=2, hk=1, causal=True, bf16=True, reduce=True, seed=0, text=None, verbose=True):
+def run(b=1, sq=200, sk=200, h=2, hk=1, causal=True, bf16=True, reduce=True, seed=0, text=None, verbose=True,
+        grid=None):
+    """grid: workgroups of the persistent item loop (default: one per item)"""
     rng = np.random.default_rng(seed)
     q = rng.standard_normal((b, sq, h, D)).astype(np.float32)
     k = rng.standard_normal((b, sk, hk, D)).astype(np.float32)
@@ -105,7 +108,8 @@ def run(b=1, sq=200, sk=200, h=2, hk=1, causal=True, bf16=True, reduce=True, see
     red = reduce and g > 1
     n_items = b * nh_out * nblk
     kw = dict(q=aq, k=ak, v=av, do=ado, dk=adk, dv=adv, lsed=alsed, sched=0, cuq=0, cuk=0,
-              dec=dkdv_item_decode(b * nh_out, nh_out, 1 if red else g, nblk),
+              dec=dkdv_item_decode(b * nh_out, nh_out, 1 if red else g, nblk), n_items=n_items,
+              grid=grid or n_items,
               q_batch=sq * h * D * 2, k_batch=sk * hk * D * 2, v_batch=sk * hk * D * 2, do_batch=sq * h * D * 2,
               dk_batch=sk * nh_out * D * 2, dv_batch=sk * nh_out * D * 2,
               q_row=h * D * 2, k_row=hk * D * 2, v_row=hk * D * 2, do_row=h * D * 2, dk_row=nh_out * D * 2,
@@ -116,7 +120,7 @@ def run(b=1, sq=200, sk=200, h=2, hk=1, causal=True, bf16=True, reduce=True, see
     text = text or asm_text()
     name = f"fa_bwd_dkdv_asm_d128_{'bf16' if bf16 else 'f16'}_{'causal' if causal else 'full'}"
     emu = Emu(text, name, heap)
-    for L in range(n_items):
+    for L in range(grid or n_items):
         emu.run_wg(L, akarg)
     dk = dec(heap.get(adk, b * sk * nh_out * D * 2).view(np.uint16)).reshape(b, sk, nh_out, D).astype(np.float64)
     dv = dec(heap.get(adv, b * sk * nh_out * D * 2).view(np.uint16)).reshape(b, sk, nh_out, D).astype(np.float64)

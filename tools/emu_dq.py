@@ -37,7 +37,8 @@ def pack_args(**kw):
     out += struct.pack("<7i", kw["sq"], kw["sk"], kw["lse_pitch"], kw["dsum_pitch"], kw["h"], kw["hk"], kw["flags"])
     out += struct.pack("<ff", kw["c"], kw["scale"])
     out += struct.pack("<10I", *kw["dec"])
-    assert len(out) == 224, len(out)
+    out += struct.pack("<ii", kw["n_items"], kw["grid"])
+    assert len(out) == 232, len(out)
     return out
 
 
@@ -60,8 +61,9 @@ def reference_dq(q, k, v, do, causal, scale):
     return lse, dsum, dq
 
 
-def run(b=1, sq=300, sk=300, h=2, hk=1, causal=True, bf16=True, seed=0, text=None, verbose=True, hp=0):
-    """hp: heads per XCD group of the work order (0: head-fastest)"""
+def run(b=1, sq=300, sk=300, h=2, hk=1, causal=True, bf16=True, seed=0, text=None, verbose=True, hp=0, grid=None):
+    """hp: heads per XCD group of the work order (0: head-fastest); grid: workgroups of the
+    persistent item loop (default: one per item)"""
     rng = np.random.default_rng(seed)
     q = rng.standard_normal((b, sq, h, D)).astype(np.float32)
     k = rng.standard_normal((b, sk, hk, D)).astype(np.float32)
@@ -84,7 +86,7 @@ def run(b=1, sq=300, sk=300, h=2, hk=1, causal=True, bf16=True, seed=0, text=Non
     nmb = (sq + BM - 1) // BM
     n_items = b * h * nmb
     kw = dict(q=aq, k=ak, v=av, do=ado, dq=adq, lse=alse, dsum=ads, sched=0, cuq=0, cuk=0,
-              dec=fwd_item_decode(b * h, h, h // hk, nmb, hp),
+              dec=fwd_item_decode(b * h, h, h // hk, nmb, hp), n_items=n_items, grid=grid or n_items,
               q_batch=sq * h * D * 2, kv_batch=sk * hk * D * 2, do_batch=sq * h * D * 2, dq_batch=sq * h * D * 2,
               q_row=h * D * 2, kv_row=hk * D * 2, do_row=h * D * 2, dq_row=h * D * 2,
               q_head=D * 2, k_head=D * 2, v_head=D * 2, do_head=D * 2, dq_head=D * 2,
@@ -94,7 +96,7 @@ def run(b=1, sq=300, sk=300, h=2, hk=1, causal=True, bf16=True, seed=0, text=Non
     text = text or asm_text()
     name = f"fa_bwd_dq_asm_d128_{'bf16' if bf16 else 'f16'}_{'causal' if causal else 'full'}"
     emu = Emu(text, name, heap)
-    for L in range(n_items):
+    for L in range(grid or n_items):
         emu.run_wg(L, akarg)
     dq = dec(heap.get(adq, b * sq * h * D * 2).view(np.uint16)).reshape(b, sq, h, D).astype(np.float64)
     e = np.abs(dq - dq_ref).max() / max(np.abs(dq_ref).max(), 1e-9)

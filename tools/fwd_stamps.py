@@ -91,6 +91,9 @@ def main():
             for i, nm in ((16, "compute"), (17, "vmwait"), (18, "barrier")):
                 row[f"{nm}_per_step_med"] = float(np.median(a[:, i] / np.maximum(steps, 1)))
             row["steps_med"] = float(np.median(steps))
+            items = np.maximum(a[:, 9], 1)
+            for i, nm in ((20, "tile0"), (21, "last_step"), (22, "epilogue"), (23, "item_start")):
+                row[f"{nm}_per_item_med"] = float(np.median(a[:, i] / items))
         rows.append(row)
         print(" ".join(f"{k}={v:.4g}" if isinstance(v, float) else f"{k}={v}" for k, v in row.items()), flush=True)
 

@@ -41,7 +41,7 @@ import sys
 
 sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
 from isa import (ACCR, ACCW, BARRIER, BRANCH, DMA, LABEL, LDS, MFMA, PERM, RFL, SALU, SMEM, SOPP,  # noqa: E402
-                 TRANS, VALU, VLOAD, VSTORE, WAIT, Inst, add_waits, ar, fix_hazards, item_decode_ops, label, nop, rtxt,
+                 TRANS, VALU, VLOAD, VSTORE, WAIT, Inst, add_waits, ar, fix_hazards, item_decode_ops, item_pos_ops, label, nop, rtxt,
                  schedule, sr, vr)
 
 D = 128
@@ -130,8 +130,9 @@ S_WAVE = 48
 S_TMP = 49                           # 49..55 (the prologue keeps kernargs in 56..101)
 NSGPR = 102
 
-KARG_SIZE = 264
+KARG_SIZE = 272
 DEC_OFF = 224    # fa_params.h ItemDecode (40 bytes) after BwdAsmArgs' 224
+NITEMS_OFF = 264  # n_items, grid (persistent item loop)
 
 # dev A/B switches, read when the .s is generated (tools/asm_variant.sh)
 OPT_WIN = int(os.environ.get("FA_GBW_WIN", "16"))     # an A fragment may be read up to WIN MFMAs ahead
@@ -139,6 +140,8 @@ OPT_LEAD = int(os.environ.get("FA_GBW_LEAD", "2"))    # ... and at least LEAD MF
 # dev timeline: every workgroup stores {start, end} s_memtime, HW_ID, XCC_ID, id at the `stamps`
 # kernarg address + 32 id (tools/bwd_stamps.py)
 OPT_STAMP = os.environ.get("FA_GBW_STAMP") == "1"
+V_ROUND = 184          # round r of the persistent item loop (uniform)
+S_ITEM = 28            # the item index, until the sweep geometry takes the register (S_QF)
 V_STAMP = 164          # 164..177: start lo / hi, HW_ID, XCC_ID, wg, end lo / hi, wave, -, -, loop start lo / hi,
                        # epilogue start lo / hi (with OPT_STAMP)
 
@@ -427,7 +430,7 @@ class K:
                     I(f"s_getreg_b32 s{S_TMP + 4}, hwreg(HW_REG_XCC_ID)", SALU, wr=sr(S_TMP + 4)),
                     I("s_waitcnt lgkmcnt(0)", WAIT)]
             ins += [I(f"v_mov_b32_e32 v{V_STAMP + i}, s{S_TMP + 1 + i}", VALU, rd=sr(S_TMP + 1 + i), wr=vr(V_STAMP + i)) for i in range(4)]
-            ins += [I(f"v_mov_b32_e32 v{V_STAMP + 4}, s2", VALU, rd=sr(2), wr=vr(V_STAMP + 4))]
+            ins += [I(f"v_mov_b32_e32 v{V_STAMP + 4}, s{S_ITEM}", VALU, rd=sr(S_ITEM), wr=vr(V_STAMP + 4))]
         P = lambda i: ka + i   # noqa: E731
         Pq, Pk, Pv, Pdo, Pdk, Pdv, Pl, Psch, Pcq, Pck = (P(2 * i) for i in range(10))
         Bq, Bk, Bv, Bdo, Bdk, Bdv = (P(20 + 2 * i) for i in range(6))
@@ -437,16 +440,13 @@ class K:
         H, NG, NHS, GRP = 20, 21, 22, 23
         FLG = 3
         T0, T1, T2, T3, T4, T5, T6 = (S_TMP + i for i in range(7))
-        ins += [I("v_lshrrev_b32_e32 v1, 6, v0", VALU, rd=vr(0), wr=vr(1)),
-                I(f"v_readfirstlane_b32 s{S_WAVE}, v1", RFL, rd=vr(1), wr=sr(S_WAVE)),
-                I(f"v_and_b32_e32 v{V_LANE}, 63, v0", VALU, rd=vr(0), wr=vr(V_LANE))]
         # the work order (fa_params.h ItemDecode) into s[36:45] (free until the geometry):
         # (bidb, hx, kvh, key block) of this workgroup
         ins += [I(f"s_load_dwordx8 s[36:43], s[0:1], {DEC_OFF}", SMEM),
                 I(f"s_load_dwordx2 s[44:45], s[0:1], {DEC_OFF + 32}", SMEM),
                 I("s_waitcnt lgkmcnt(0)", WAIT)]
         BIDB, HX, KVH, KB = 24, 25, 26, 27      # S_N .. S_Q0V, set at the end
-        ins += item_decode_ops(L=2, M=36, pa=T1, pb=T3, t=T5, u=T6, o_blk=KB, reverse=False)
+        ins += item_decode_ops(L=S_ITEM, M=36, pa=T1, pb=T3, t=T5, u=T6, o_blk=KB, reverse=False)
         ins += [I(f"s_mov_b32 s{BIDB}, s{T3}", SALU), I(f"s_mov_b32 s{HX}, s{T6}", SALU),
                 I(f"s_mov_b32 s{KVH}, s{T1}", SALU)]
         # varlen geometry (BlockInfo, block_info.h:14-31): 64-bit byte offsets of row 0 of this sequence;
@@ -485,7 +485,7 @@ class K:
         N0, KW0 = T4, T5
         ins += [I(f"s_lshl_b32 s{N0}, s{KB}, 7", SALU, rd=sr(KB), wr=sr(N0)),
                 I(f"s_cmp_ge_i32 s{N0}, s{SK}", SALU, rd=sr(N0) + sr(SK), wr=[("scc", 0)]),
-                I(f"s_cbranch_scc1 {self.lab_end}", BRANCH),
+                I(f"s_cbranch_scc1 {self.lab_next}", BRANCH),
                 I(f"s_lshl_b32 s{KW0}, s{S_WAVE}, 5", SALU, rd=sr(S_WAVE), wr=sr(KW0)),
                 I(f"s_add_u32 s{KW0}, s{KW0}, s{N0}", SALU, rd=sr(KW0) + sr(N0), wr=sr(KW0))]
         # dK / dV head: the kv head (reduced GQA, flags bit 1) or the query head
@@ -733,6 +733,7 @@ class K:
     # ------------------------------------------------------------------ whole kernel
     def build(self):
         self.lab_end = self.lab("end")
+        self.lab_next = self.lab("next")
         self.ool = []         # out-of-line blocks (head wraps)
         l_epi = self.lab("epi")
         code = []
@@ -742,14 +743,31 @@ class K:
             out, _ = fix_hazards(out, pre=pre)
             code.extend(out)
 
-        pro = self.prologue(l_epi) + self.prologue_dma()
+        # once per workgroup: wave index, lane, round 0
+        emit([Inst("v_lshrrev_b32_e32 v1, 6, v0", VALU, rd=vr(0), wr=vr(1)),
+              Inst(f"v_readfirstlane_b32 s{S_WAVE}, v1", RFL, rd=vr(1), wr=sr(S_WAVE)),
+              Inst(f"v_and_b32_e32 v{V_LANE}, 63, v0", VALU, rd=vr(0), wr=vr(V_LANE)),
+              Inst(f"v_mov_b32_e32 v{V_ROUND}, 0", VALU, wr=vr(V_ROUND))])
+        # persistent item loop (fa_bwd_asm.cpp, knob 6): workgroup w runs items r G + (r odd ? rev(w) :
+        # w); G = n_items runs one item per workgroup.  The barrier keeps every wave's LDS reads of
+        # the previous item ahead of the DMA of this one.
+        l_item = self.lab("item")
+        code.append(label(l_item))
+        T0, T1, T2, T3, T4 = (S_TMP + i for i in range(5))
+        head = [Inst("s_barrier", BARRIER),
+                Inst(f"s_load_dwordx2 s[{T1}:{T2}], s[0:1], {NITEMS_OFF}", SMEM),     # n_items, grid
+                Inst(f"v_readfirstlane_b32 s{T0}, v{V_ROUND}", RFL),
+                Inst("s_waitcnt lgkmcnt(0)", WAIT)]
+        head += item_pos_ops(S_ITEM, T0, 2, T2, T3, T4)
+        head += [Inst(f"s_cmp_ge_u32 s{S_ITEM}, s{T1}", SALU), Inst(f"s_cbranch_scc1 {self.lab_end}", BRANCH)]
+        pro = head + self.prologue(l_epi) + self.prologue_dma()
         # wait: Q / dO(0) (phase -1), Q / dO(1) (its tail prefetches fragments of 1), LSE / D(0, 1)
         # landed; younger than Q / dO(1): L3, Q2, L4, Q3, L5, Q4, L6, Q5, L7 = 21
         pro += [Inst("s_waitcnt vmcnt(21)", WAIT), Inst("s_barrier", BARRIER)]
         if OPT_STAMP:
             pro += [Inst(f"s_memtime s[{S_TMP + 1}:{S_TMP + 2}]", SMEM), Inst("s_waitcnt lgkmcnt(0)", WAIT),
                     Inst(f"v_mov_b32_e32 v{V_STAMP + 10}, s{S_TMP + 1}", VALU), Inst(f"v_mov_b32_e32 v{V_STAMP + 11}, s{S_TMP + 2}", VALU)]
-        emit(pro)
+        emit(pro, pre=[nop(15)])
         # phase -1: chain starts of subtiles 0 (-> buffers 0) and 1 (-> 1), S / dP(0)
         ph = [Inst(f"s_mov_b32 s{S_SROW}, 0", SALU, wr=sr(S_SROW)),
               Inst(f"s_mov_b32 s{S_STR}, {RING - 2 * SLOT}", SALU, wr=sr(S_STR)),   # slot of subtile -2
@@ -818,6 +836,8 @@ class K:
                          Inst(f"v_mov_b32_e32 v{V_STAMP + 12}, s{S_TMP + 1}", VALU),
                          Inst(f"v_mov_b32_e32 v{V_STAMP + 13}, s{S_TMP + 2}", VALU)]
         emit([nop(15)] + stamp_epi + self.epilogue(), pre=pad)
+        code.append(label(self.lab_next))
+        code += [Inst(f"v_add_u32_e32 v{V_ROUND}, 1, v{V_ROUND}", VALU), Inst(f"s_branch {l_item}", BRANCH)]
         code.append(label(self.lab_end))
         if OPT_STAMP:
             I = Inst

@@ -32,7 +32,7 @@ import sys
 
 sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
 from isa import (ACCR, ACCW, BARRIER, BRANCH, DMA, LABEL, LDS, MFMA, PERM, RFL, SALU, SMEM, SOPP,  # noqa: E402
-                 TRANS, VALU, VLOAD, VSTORE, WAIT, Inst, add_waits, ar, fix_hazards, item_decode_ops, label, nop, rtxt,
+                 TRANS, VALU, VLOAD, VSTORE, WAIT, Inst, add_waits, ar, fix_hazards, item_decode_ops, item_pos_ops, label, nop, rtxt,
                  schedule, sr, vr)
 
 D = 128
@@ -112,10 +112,13 @@ S_MASK0 = 28                   # first masked step (causal), else a large value
 S_KV32 = 29                    # 32 rows of K / V (bytes)
 S_WAVE = 30
 S_TMP = 31                     # 31..39
+S_ROUND = 100                  # round r of the persistent item loop
+S_ITEM = 101                   # the item index
 NSGPR = 102
 
-KARG_SIZE = 224
+KARG_SIZE = 232
 DEC_OFF = 184    # fa_params.h ItemDecode (40 bytes) after DqAsmArgs' 184
+NITEMS_OFF = 224  # n_items, grid (persistent item loop)
 
 
 class K:
@@ -315,15 +318,13 @@ class K:
         SQ, SK, LP, DPt, NH, NHK, FLG = (P(37 + i) for i in range(7))
         T = [S_TMP + i for i in range(9)]
         ins += [I(f"s_load_dwordx2 s[{S_C}:{S_SCALE}], s[0:1], 0xb0", SMEM, rd=sr(0, 2), wr=sr(S_C, 2)),
-                I("v_lshrrev_b32_e32 v1, 6, v0", VALU, rd=vr(0), wr=vr(1)),
-                I(f"v_readfirstlane_b32 s{S_WAVE}, v1", RFL, rd=vr(1), wr=sr(S_WAVE)),
-                I(f"v_and_b32_e32 v{V_LANE}, 63, v0", VALU, rd=vr(0), wr=vr(V_LANE)),
+                I(f"v_mov_b32_e32 v1, s{S_WAVE}", VALU, rd=sr(S_WAVE), wr=vr(1)),     # (v0, v1: S^T tiles in the loop)
                 # the work order (fa_params.h ItemDecode) into s[40:49] (free until the geometry)
                 I(f"s_load_dwordx8 s[40:47], s[0:1], {DEC_OFF}", SMEM),
                 I(f"s_load_dwordx2 s[48:49], s[0:1], {DEC_OFF + 32}", SMEM),
                 I("s_waitcnt lgkmcnt(0)", WAIT)]
         BIDB, HEAD, KVH, MB = S_N, S_NLAST, S_MASK0, S_KV32     # temporaries until the loop state
-        ins += item_decode_ops(L=2, M=40, pa=T[1], pb=T[3], t=T[5], u=T[6], o_blk=MB, reverse=True)
+        ins += item_decode_ops(L=S_ITEM, M=40, pa=T[1], pb=T[3], t=T[5], u=T[6], o_blk=MB, reverse=True)
         ins += [I(f"s_mov_b32 s{BIDB}, s{T[3]}", SALU), I(f"s_mov_b32 s{HEAD}, s{T[6]}", SALU),
                 I(f"s_mov_b32 s{KVH}, s{T[1]}", SALU)]
         # varlen geometry (block_info.h:14-31): byte offsets of row 0 of this sequence (Q-side: Q, dO,
@@ -361,7 +362,7 @@ class K:
         M0R, NROW = T[4], T[5]
         ins += [I(f"s_lshl_b32 s{M0R}, s{MB}, 8", SALU, rd=sr(MB), wr=sr(M0R)),
                 I(f"s_cmp_ge_i32 s{M0R}, s{SQ}", SALU, rd=sr(M0R) + sr(SQ), wr=[("scc", 0)]),
-                I(f"s_cbranch_scc1 {self.lab_end}", BRANCH),
+                I(f"s_cbranch_scc1 {self.lab_next}", BRANCH),
                 I(f"s_sub_u32 s{NROW}, s{SQ}, s{M0R}", SALU, rd=sr(SQ) + sr(M0R), wr=sr(NROW)),
                 I(f"s_min_u32 s{NROW}, s{NROW}, {BM}", SALU, rd=sr(NROW), wr=sr(NROW))]
 
@@ -538,6 +539,7 @@ class K:
     # ------------------------------------------------------------------ whole kernel
     def build(self):
         self.lab_end = self.lab("end")
+        self.lab_next = self.lab("next")
         l_epi = self.lab("epi")
         code = []
 
@@ -546,12 +548,28 @@ class K:
             out, _ = fix_hazards(out, pre=pre)
             code.extend(out)
 
-        pro = self.prologue(l_epi)
+        # once per workgroup: wave index, lane, round 0
+        emit([Inst("v_lshrrev_b32_e32 v1, 6, v0", VALU, rd=vr(0), wr=vr(1)),
+              Inst(f"v_readfirstlane_b32 s{S_WAVE}, v1", RFL, rd=vr(1), wr=sr(S_WAVE)),
+              Inst(f"v_and_b32_e32 v{V_LANE}, 63, v0", VALU, rd=vr(0), wr=vr(V_LANE)),
+              Inst(f"s_mov_b32 s{S_ROUND}, 0", SALU)])
+        # persistent item loop (fa_bwd_asm.cpp, knob 6): workgroup w runs items r G + (r odd ? rev(w) :
+        # w); G = n_items runs one item per workgroup.  The barrier keeps every wave's LDS reads of
+        # the previous item ahead of the DMA of this one.
+        l_item = self.lab("item")
+        code.append(label(l_item))
+        T0, T1, T2, T3 = (S_TMP + i for i in range(4))
+        head = [Inst("s_barrier", BARRIER),
+                Inst(f"s_load_dwordx2 s[{T0 + 1}:{T0 + 2}], s[0:1], {NITEMS_OFF}", SMEM),
+                Inst("s_waitcnt lgkmcnt(0)", WAIT)]
+        head += item_pos_ops(S_ITEM, S_ROUND, 2, T0 + 2, T0, T0 + 3)
+        head += [Inst(f"s_cmp_ge_u32 s{S_ITEM}, s{T0 + 1}", SALU), Inst(f"s_cbranch_scc1 {self.lab_end}", BRANCH)]
+        pro = head + self.prologue(l_epi)
         for _ in range(KQ):
             pro += self.dma_subtile()
         # K / V(0) and (1) landed (phase -1 reads 0, its tail prefetches 1): 16 younger DMAs
         pro += [Inst("s_waitcnt vmcnt(16)", WAIT), Inst("s_barrier", BARRIER)]
-        emit(pro)
+        emit(pro, pre=[nop(15)])
         # phase -1: S^T / dP^T(0) -> buffers 0
         # -LSE log2 e (LSE = +inf -> -inf: P = 0); the loads landed with the prologue's wait
         ph = [Inst(f"v_mul_f32_e32 v{V_NLC[j]}, 0xbfb8aa3b, v{V_NLC[j]}", VALU, rd=vr(V_NLC[j]), wr=vr(V_NLC[j]), key=-500)
@@ -612,6 +630,8 @@ class K:
         emit(self.tail(), pre=pad)
         code.append(label(l_epi))
         emit([nop(15)] + self.epilogue(), pre=pad)
+        code.append(label(self.lab_next))
+        code += [Inst(f"s_add_u32 s{S_ROUND}, s{S_ROUND}, 1", SALU), Inst(f"s_branch {l_item}", BRANCH)]
         code.append(label(self.lab_end))
         code.append(Inst("s_endpgm", SOPP))
         return code

@@ -160,7 +160,8 @@ OPT_STAMP = os.environ.get("FA_GEN_STAMP") in ("1", "2")
 # FA_GEN_STAMP=2 also sums, per wave, the cycles of each step's compute, its vmcnt/lgkmcnt wait and
 # its barrier wait (s_memtime around the step-end wait and barrier; perturbs the schedule a little)
 OPT_STEPSTAMP = os.environ.get("FA_GEN_STAMP") == "2"
-V_SSUM = 240      # 240..244: compute, wait, barrier sums, step count, last barrier exit
+V_SSUM = 240      # 240..244: compute, wait, barrier sums, step count, last stamp;
+                  # 246..249: item phases: tile 0, last step, epilogue, item start (geometry .. tile 0's barrier)
 # latency-aware gap scheduling (isa.schedule lat=): "valu,trans,lds,mfma" result latencies in cycles
 _lat = os.environ.get("FA_GEN_LAT")
 OPT_LAT = None
@@ -188,6 +189,17 @@ class K:
     def lab(self, s):
         self.uid += 1
         return f".L{self.name}_{s}_{self.uid}"
+
+    def stamp_point(self, acc):
+        """(FA_GEN_STAMP=2) v[V_SSUM + acc] += now - last stamp; last stamp = now"""
+        if not OPT_STEPSTAMP:
+            return []
+        t0 = V_T
+        return [Inst(f"s_memtime s[{S_TMP}:{S_TMP + 1}]", SMEM), Inst("s_waitcnt lgkmcnt(0)", WAIT),
+                Inst(f"v_mov_b32_e32 v{t0}, s{S_TMP}", VALU),
+                Inst(f"v_sub_u32_e32 v{t0 + 1}, v{t0}, v{V_SSUM + 4}", VALU),
+                Inst(f"v_add_u32_e32 v{V_SSUM + acc}, v{V_SSUM + acc}, v{t0 + 1}", VALU),
+                Inst(f"v_mov_b32_e32 v{V_SSUM + 4}, v{t0}", VALU)]
 
     # ------------------------------------------------------------------ instruction builders
     def mfma_s(self, st_reg, kslot, j, ks, first, bias=None):
@@ -662,7 +674,7 @@ class K:
             ins += [I(f"v_mov_b32_e32 v{V_STAMP + i}, s{T0 + i}", VALU, rd=sr(T0 + i), wr=vr(V_STAMP + i)) for i in range(4)]
             ins += [I(f"v_mov_b32_e32 v{V_STAMP + 4}, 0", VALU, wr=vr(V_STAMP + 4)),
                     I(f"v_mov_b32_e32 v{V_STAMP + 5}, 0", VALU, wr=vr(V_STAMP + 5))]
-            ins += [I(f"v_mov_b32_e32 v{V_SSUM + i}, 0", VALU) for i in range(4)]
+            ins += [I(f"v_mov_b32_e32 v{V_SSUM + i}, 0", VALU) for i in (0, 1, 2, 3, 6, 7, 8, 9)]
             ins += [I(f"v_mov_b32_e32 v{V_SSUM + 4}, s{T0}", VALU)]
         # rng_state (block 0, wave 0): {seed, offset}; lanes >= 1 fall outside the 16-byte record
         l_norng = self.lab("norng")
@@ -1011,9 +1023,7 @@ class K:
         row max, P(0, a); then into the step loop"""
         I = Inst
         ins = [I(f"s_waitcnt vmcnt({2 * NP})", WAIT), I("s_barrier", BARRIER)]
-        if OPT_STEPSTAMP:
-            ins += [I(f"s_memtime s[{S_TMP}:{S_TMP + 1}]", SMEM), I("s_waitcnt lgkmcnt(0)", WAIT),
-                    I(f"v_mov_b32_e32 v{V_SSUM + 4}, s{S_TMP}", VALU)]
+        ins += self.stamp_point(9)
         ins += self.dump("pro_lds")
         ins += [I(f"v_add_u32_e32 v{V_KB0}, s{S_KOFF}, v{V_RB0}", VALU, rd=sr(S_KOFF) + vr(V_RB0), wr=vr(V_KB0)),
                 I(f"v_add_u32_e32 v{V_KB1}, s{S_KOFF}, v{V_RB1}", VALU, rd=sr(S_KOFF) + vr(V_RB1), wr=vr(V_KB1))]
@@ -1051,6 +1061,7 @@ class K:
         ins += sm
         ins += [Inst(f"v_mov_b32_e32 v{V_L[0]}, v{V_PS[0]}", VALU, rd=vr(V_PS[0]), wr=vr(V_L[0]))]
         ins += self.dump("pro_end")
+        ins += self.stamp_point(6)
         # V reads tile 0 (slot S_KOFF); S_KOFF -> tile 1 (the LAST step's refit takes S_KOFF - TILE)
         ins += [I(f"s_add_u32 s{S_VOFF}, s{S_KOFF}, {VBASE}", SALU),
                 I(f"s_add_u32 s{S_KOFF}, s{S_KOFF}, {TILE}", SALU),
@@ -1171,7 +1182,7 @@ class K:
         emit_block(m1, pre=tailpad)
         code += [I(f"s_branch {L['sel0']}", BRANCH)]
         code.append(label(L["last0"]))
-        emit_block(la0 + self.dump("l0_end"), pre=tailpad)
+        emit_block(self.stamp_point(0) + la0 + self.dump("l0_end"), pre=tailpad)
         code += [I(f"s_branch {l_epi}", BRANCH)]
         if self.causal:
             for par, body in ((0, dg0), (1, dg1)):
@@ -1183,9 +1194,9 @@ class K:
                 emit_block(body, pre=tailpad)
                 code += [I(f"s_branch {L['sel%d' % (1 - par)]}", BRANCH)]
         code.append(label(L["last1"]))
-        emit_block(la1, pre=tailpad)
+        emit_block(self.stamp_point(0) + la1, pre=tailpad)
         code.append(label(l_epi))
-        emit_block([nop(15)] + self.epilogue(), pre=tailpad)
+        emit_block([nop(15)] + self.stamp_point(7) + self.epilogue() + self.stamp_point(8), pre=tailpad)
         # next item of this workgroup: warm when the DMA stream already runs into it
         code += [I(f"s_add_u32 s{S_ROUND}, s{S_ROUND}, 1", SALU),
                  I(f"s_cmp_eq_u32 s{S_WARM}, 1", SALU), I(f"s_cbranch_scc1 {L['warm']}", BRANCH),
@@ -1211,6 +1222,7 @@ class K:
                    I(f"buffer_store_dwordx2 v[{V_STAMP + 4}:{V_STAMP + 5}], v8, s[52:55], s46 offen offset:32", VSTORE),
                    I("buffer_store_dwordx4 v[4:7], v8, s[52:55], s46 offen offset:48", VSTORE),
                    I(f"buffer_store_dwordx4 v[{V_SSUM}:{V_SSUM + 3}], v8, s[52:55], s46 offen offset:64", VSTORE),
+                   I(f"buffer_store_dwordx4 v[{V_SSUM + 6}:{V_SSUM + 9}], v8, s[52:55], s46 offen offset:80", VSTORE),
                    I("s_waitcnt vmcnt(0)", WAIT)]
             code.extend(st)
         code.append(I("s_endpgm", SOPP))

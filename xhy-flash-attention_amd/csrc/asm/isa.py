@@ -446,3 +446,26 @@ def dkdv_item_decode(nbh, h_grid, g, nblk):
     if nbh % 8 == 0:
         return make_item_decode(3, nblk, 1, h_grid, g, nblk)
     return make_item_decode(0, 0x7FFFFFFF, nbh, h_grid, g, nblk)
+
+
+def item_pos_ops(dst, r, w, grid, t, u):
+    """persistent item loop: s[dst] = r G + (r odd ? rev(w) : w), G = s[grid], w = s[w], r = s[r]
+    (snake order over the heaviest-first item list, so each pair of rounds pairs heavy and light
+    items); rev(w) = G - 8 - (w & ~7) + (w & 7) when G % 8 == 0 -- the reversal runs over groups of 8
+    workgroups, so workgroup w stays on the items of the XCD it runs on (w mod 8) -- else G - 1 - w.
+    t, u: temporaries (distinct from dst, r, w, grid)"""
+    I = Inst
+    return [I(f"s_and_b32 s{u}, s{w}, 7", SALU),
+            I(f"s_lshl_b32 s{u}, s{u}, 1", SALU),
+            I(f"s_sub_u32 s{t}, s{grid}, 8", SALU),
+            I(f"s_sub_u32 s{t}, s{t}, s{w}", SALU),
+            I(f"s_add_u32 s{t}, s{t}, s{u}", SALU),                  # G - 8 - (w & ~7) + (w & 7)
+            I(f"s_sub_u32 s{u}, s{grid}, 1", SALU),
+            I(f"s_sub_u32 s{u}, s{u}, s{w}", SALU),                  # G - 1 - w
+            I(f"s_and_b32 s{dst}, s{grid}, 7", SALU),
+            I(f"s_cmp_lg_u32 s{dst}, 0", SALU),
+            I(f"s_cselect_b32 s{t}, s{u}, s{t}", SALU),              # rev(w)
+            I(f"s_bitcmp1_b32 s{r}, 0", SALU),
+            I(f"s_cselect_b32 s{t}, s{t}, s{w}", SALU),              # odd round: rev(w)
+            I(f"s_mul_i32 s{dst}, s{r}, s{grid}", SALU),
+            I(f"s_add_u32 s{dst}, s{dst}, s{t}", SALU)]

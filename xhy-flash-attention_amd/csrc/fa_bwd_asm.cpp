@@ -49,9 +49,11 @@ struct BwdAsmArgs {
   int32_t flags;    // bit 0: varlen_padded_input, bit 1: dK / dV reduced over the GQA group
   int32_t pad;
   void* stamps;     // dev timeline buffer (a generator build with FA_GBW_STAMP=1 writes it), else unused
-  ItemDecode dec;   // the work order, computed in the kernel from the workgroup index
+  ItemDecode dec;   // the work order, computed in the kernel from the item index
+  int32_t n_items;  // items (batch x heads x key blocks)
+  int32_t grid;     // workgroups: workgroup w runs items r G + (r odd ? rev(w) : w), r = 0, 1, ...
 };
-static_assert(sizeof(BwdAsmArgs) == 264 && offsetof(BwdAsmArgs, dec) == 224, "BwdAsmArgs layout");
+static_assert(sizeof(BwdAsmArgs) == 272 && offsetof(BwdAsmArgs, dec) == 224, "BwdAsmArgs layout");
 
 // must match the kernarg loads of gen_dq.py (K.prologue) and KARG_SIZE
 struct DqAsmArgs {
@@ -63,9 +65,11 @@ struct DqAsmArgs {
   int32_t sq, sk, lse_pitch, dsum_pitch, h, hk;
   int32_t flags;    // bit 0: varlen_padded_input
   float c, scale;
-  ItemDecode dec;   // the work order, computed in the kernel from the workgroup index
+  ItemDecode dec;   // the work order, computed in the kernel from the item index
+  int32_t n_items;  // items (batch x heads x query blocks)
+  int32_t grid;     // workgroups (persistent item loop, as BwdAsmArgs)
 };
-static_assert(sizeof(DqAsmArgs) == 224 && offsetof(DqAsmArgs, dec) == 184, "DqAsmArgs layout");
+static_assert(sizeof(DqAsmArgs) == 232 && offsetof(DqAsmArgs, dec) == 184, "DqAsmArgs layout");
 
 constexpr int kMaxDev = 64;
 constexpr int kBkn = 128;   // keys per workgroup
@@ -73,6 +77,7 @@ struct DevModule {
   hipModule_t mod = nullptr, mod_dq = nullptr;
   hipFunction_t fn[4] = {};      // dK/dV [bf16 causal, bf16 full, f16 causal, f16 full]
   hipFunction_t fn_dq[4] = {};   // dQ, the same order
+  int cus = 0;
 };
 std::mutex g_mu;
 DevModule g_dev[kMaxDev];
@@ -94,6 +99,7 @@ DevModule& module_for(int dev) {
     for (int i = 0; i < 4; ++i) check(hipModuleGetFunction(&m.fn[i], m.mod, kNames[i]), kNames[i]);
     check(hipModuleLoadData(&m.mod_dq, fa_dq_asm_co), "hipModuleLoadData (dQ)");
     for (int i = 0; i < 4; ++i) check(hipModuleGetFunction(&m.fn_dq[i], m.mod_dq, kDqNames[i]), kDqNames[i]);
+    check(hipDeviceGetAttribute(&m.cus, hipDeviceAttributeMultiprocessorCount, dev), "hipDeviceGetAttribute");
   }
   return m;
 }
@@ -133,10 +139,16 @@ void launch_bwd_dkdv_asm(const BwdParams& p, bool is_bf16, hipStream_t stream) {
   int dev = 0;
   check(hipGetDevice(&dev), "hipGetDevice");
   hipFunction_t fn;
+  int cus = 0;
   {
     std::lock_guard<std::mutex> lk(g_mu);
-    fn = module_for(dev).fn[(is_bf16 ? 0 : 2) + (s.causal ? 0 : 1)];
+    DevModule& m = module_for(dev);
+    fn = m.fn[(is_bf16 ? 0 : 2) + (s.causal ? 0 : 1)];
+    cus = m.cus;
   }
+  // persistent grid (knob 6, default on): one workgroup per CU (151 KiB of LDS allows one) walking the
+  // heaviest-first item list in snake order -- no workgroup dispatch between items
+  const long long grid = (knob(kKnobBwdPersist) != 0 && cus > 0 && nwg > cus) ? cus : nwg;
   BwdAsmArgs a;
   std::memset(&a, 0, sizeof(a));
   a.q = p.q; a.k = p.k; a.v = p.v; a.dout = p.dout; a.dk = p.dk; a.dv = p.dv;
@@ -154,9 +166,11 @@ void launch_bwd_dkdv_asm(const BwdParams& p, bool is_bf16, hipStream_t stream) {
   a.flags = (s.varlen_padded_input ? 1 : 0) | (p.gqa_reduce ? 2 : 0);
   a.stamps = g_stamps;
   a.dec = dkdv_item_decode(s.b * nh_grid, nh_grid, p.gqa_reduce ? 1 : s.h / s.hk, nblk);
+  a.n_items = (int32_t)nwg;
+  a.grid = (int32_t)grid;
   size_t sz = sizeof(a);
   void* cfg[] = {HIP_LAUNCH_PARAM_BUFFER_POINTER, &a, HIP_LAUNCH_PARAM_BUFFER_SIZE, &sz, HIP_LAUNCH_PARAM_END};
-  check(hipModuleLaunchKernel(fn, (unsigned)nwg, 1, 1, 256, 1, 1, 0, stream, nullptr, cfg), "hipModuleLaunchKernel");
+  check(hipModuleLaunchKernel(fn, (unsigned)grid, 1, 1, 256, 1, 1, 0, stream, nullptr, cfg), "hipModuleLaunchKernel");
 }
 
 bool dq_asm_applicable(const BwdParams& p) {
@@ -184,10 +198,17 @@ void launch_bwd_dq_asm(const BwdParams& p, bool is_bf16, hipStream_t stream) {
   int dev = 0;
   check(hipGetDevice(&dev), "hipGetDevice");
   hipFunction_t fn;
+  int cus = 0;
   {
     std::lock_guard<std::mutex> lk(g_mu);
-    fn = module_for(dev).fn_dq[(is_bf16 ? 0 : 2) + (s.causal ? 0 : 1)];
+    DevModule& m = module_for(dev);
+    fn = m.fn_dq[(is_bf16 ? 0 : 2) + (s.causal ? 0 : 1)];
+    cus = m.cus;
   }
+  // persistent grid (knob 6): one workgroup per CU walking the heaviest-first list in snake order;
+  // the XCD-grouped order (dq_head_group > 0) keeps one item per workgroup, as the forward does
+  const long long grid =
+      (knob(kKnobBwdPersist) != 0 && p.dq_head_group == 0 && cus > 0 && nwg > cus) ? cus : nwg;
   DqAsmArgs a;
   std::memset(&a, 0, sizeof(a));
   a.q = p.q; a.k = p.k; a.v = p.v; a.dout = p.dout; a.dq = p.dq;
@@ -202,9 +223,11 @@ void launch_bwd_dq_asm(const BwdParams& p, bool is_bf16, hipStream_t stream) {
   a.flags = s.varlen_padded_input ? 1 : 0;
   a.c = s.scale_log2; a.scale = s.scale;
   a.dec = fwd_item_decode(s.b * s.h, s.h, s.h / s.hk, nmb, p.dq_head_group);
+  a.n_items = (int32_t)nwg;
+  a.grid = (int32_t)grid;
   size_t sz = sizeof(a);
   void* cfg[] = {HIP_LAUNCH_PARAM_BUFFER_POINTER, &a, HIP_LAUNCH_PARAM_BUFFER_SIZE, &sz, HIP_LAUNCH_PARAM_END};
-  check(hipModuleLaunchKernel(fn, (unsigned)nwg, 1, 1, 256, 1, 1, 0, stream, nullptr, cfg), "hipModuleLaunchKernel (dQ)");
+  check(hipModuleLaunchKernel(fn, (unsigned)grid, 1, 1, 256, 1, 1, 0, stream, nullptr, cfg), "hipModuleLaunchKernel (dQ)");
 }
 
 }  // namespace fa

@@ -171,7 +171,9 @@ enum Knob { kKnobNoSplitKv = 0 /* FLASH_ATTN_MI355X_NO_SPLITKV: 1 = never split 
             kKnobDqAsm = 4 /* FLASH_ATTN_MI355X_DQ_ASM: 0 = HIP dQ kernel for every call */,
             kKnobFwdPersist = 5 /* FLASH_ATTN_MI355X_FWD_PERSIST: 0 = assembly forward with one
                                    workgroup per item, 1 = one persistent workgroup per CU */,
-            kNumKnobs = 6 };
+            kKnobBwdPersist = 6 /* FLASH_ATTN_MI355X_BWD_PERSIST: the same for the assembly dK/dV and
+                                   dQ kernels */,
+            kNumKnobs = 7 };
 int knob(int id);
 void set_knob(int id, int value);
 
