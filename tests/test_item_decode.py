@@ -121,6 +121,9 @@ def test_forward_grouped_order_in_emulator():
 
     eo, el, *_ = emu_fwd.run(1, 300, 300, 8, 2, True, True, seed=2, verbose=False, d=64, hp=1)
     assert eo <= 1.6e-2 and el <= 1e-5, (eo, el)
+    # ... and walked by a persistent grid of 4 workgroups (snake rounds over the grouped list)
+    eo, el, *_ = emu_fwd.run(1, 600, 600, 8, 2, True, True, seed=5, verbose=False, d=64, hp=1, grid=4)
+    assert eo <= 1.6e-2 and el <= 1e-5, (eo, el)
 
 
 @pytest.mark.timeout(600)
@@ -128,4 +131,6 @@ def test_dq_grouped_order_in_emulator():
     import emu_dq
 
     e, _, _ = emu_dq.run(1, 260, 260, 8, 2, True, True, seed=3, verbose=False, hp=1)
+    assert e <= 2e-2, e
+    e, _, _ = emu_dq.run(1, 520, 520, 8, 2, True, True, seed=6, verbose=False, hp=1, grid=3)
     assert e <= 2e-2, e

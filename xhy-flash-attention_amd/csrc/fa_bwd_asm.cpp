@@ -205,10 +205,8 @@ void launch_bwd_dq_asm(const BwdParams& p, bool is_bf16, hipStream_t stream) {
     fn = m.fn_dq[(is_bf16 ? 0 : 2) + (s.causal ? 0 : 1)];
     cus = m.cus;
   }
-  // persistent grid (knob 6): one workgroup per CU walking the heaviest-first list in snake order;
-  // the XCD-grouped order (dq_head_group > 0) keeps one item per workgroup, as the forward does
-  const long long grid =
-      (knob(kKnobBwdPersist) != 0 && p.dq_head_group == 0 && cus > 0 && nwg > cus) ? cus : nwg;
+  // persistent grid (knob 6): one workgroup per CU walking the item list in snake order
+  const long long grid = (knob(kKnobBwdPersist) != 0 && cus > 0 && nwg > cus) ? cus : nwg;
   DqAsmArgs a;
   std::memset(&a, 0, sizeof(a));
   a.q = p.q; a.k = p.k; a.v = p.v; a.dout = p.dout; a.dq = p.dq;

@@ -200,11 +200,11 @@ bool launch_fwd_asm(const FwdParams& p, bool is_bf16, hipStream_t stream) {
   // light causal blocks and every item after the first starts with its K/V tiles and Q already
   // issued by its predecessor.  Varlen launches take their list from the device
   // (varlen_items_kernel: the host cannot see cu_seqlens, and a host table would hold the empty
-  // blocks past each sequence); the XCD-grouped order (head_group > 0) is built for one item per
-  // workgroup and keeps G = items.
+  // blocks past each sequence).  The XCD-grouped order (head_group > 0: a few heads per XCD, their
+  // query blocks level by level) runs persistent as well for fixed-length launches.
   hipFunction_t fn;
   int cus = 0;
-  const bool persist = knob(kKnobFwdPersist) != 0 && p.head_group == 0;
+  const bool persist = knob(kKnobFwdPersist) != 0 && (p.head_group == 0 || s.cu_seqlens_q == nullptr);
   // (the list kernel indexes its entries with int: at most 2^28 items)
   const bool dev_list = persist && s.cu_seqlens_q != nullptr && varlen_items_fit(s.b, p.num_m_blocks) &&
                         nwg <= (1ll << 28);
