@@ -156,6 +156,10 @@ OPT_SHIFT = int(os.environ.get("FA_GEN_SHIFT", "0"))          # s_nop 0 x N at t
 OPT_ALIGN = int(os.environ.get("FA_GEN_ALIGN", "0"))          # .p2align N before each step body (code placement)
 # dev clock / cycle stamps: every wave stores {s_memtime, s_memrealtime} at its start and end, the
 # tiles and items it ran, HW_ID, XCC_ID to the buffer passed as the `seed` kernarg (tools/fwd_stamps.py)
+OPT_MFZERO = os.environ.get("FA_GEN_MFZERO") == "1"          # zero O with 2 NP MFMAs (zero operands)
+OPT_EPI2 = os.environ.get("FA_GEN_EPI2") == "1"              # epilogue: groups interleaved stage by stage
+OPT_LAST2 = os.environ.get("FA_GEN_LAST2") == "1"            # last step: PV(a) under softmax(b), then PV(b)
+V_ZERO = 228      # 228..231: zeros (MFMA operands of the O zeroing)
 OPT_STAMP = os.environ.get("FA_GEN_STAMP") in ("1", "2")
 # FA_GEN_STAMP=2 also sums, per wave, the cycles of each step's compute, its vmcnt/lgkmcnt wait and
 # its barrier wait (s_memtime around the step-end wait and barrier; perturbs the schedule a little)
@@ -301,6 +305,48 @@ class K:
                    wr=vr(V_L[j]), key=key, deadline=deadline)
         return [cmp, sc, br, add]
 
+    # ------------------------------------------------------------------ the item's last step (no QK)
+    def step_last2(self, p, tag):
+        """the last step (tile n = the item's last, no QK(n+1)): phase X runs PV(n) of q-block a --
+        whose P was made in the previous step -- with softmax(n, b) and its guard in the gaps; phase
+        Y runs PV(n) of q-block b with the next item's Q loads.  (The plain last step runs softmax(n,
+        b) with no MFMA beside it.)  V fragments: phase X reads all 4 NP; at d = 128 phase Y uses
+        the 8 still in the ring first (d-tiles 2, 3) and re-reads those of d-tiles 0, 1."""
+        refits = []
+        nv = 4 * NP
+        mx = [self.mfma_o(0, f // 4, f % 8, PA(p) + 4 * (f % 4)) for f in range(nv)]
+        fx = [Inst(f"v_add_u32_e32 v{V_VB0}, s{S_VOFF}, v{V_TB0}", VALU, rd=sr(S_VOFF) + vr(V_TB0), wr=vr(V_VB0), key=-200),
+              Inst(f"v_add_u32_e32 v{V_VB1}, s{S_VOFF}, v{V_TB1}", VALU, rd=sr(S_VOFF) + vr(V_TB1), wr=vr(V_VB1), key=-200)]
+        for f in range(nv):
+            for h in range(2):
+                fx.append(self.vread(f, f % 8, h, key=-150 + 2 * f + h, earliest=(f - 8 + 1) if f >= 8 else None,
+                                     deadline=max(f - 2, 0)))
+        sm_b, _ = self.softmax_ops(1, SB(p), PB, True, (S_N0, 0), key0=0)
+        fx += sm_b
+        rl_b = self.lab(f"{tag}_refit_b")
+        refits.append(self.refit(1, SB(p), PB, rl_b, tile_add=0, phase="Y"))
+        fx += self.guard_ops(1, rl_b, key=600)
+        xs = schedule(mx, fx, budget=OPT_BUDGET)
+        order = list(range(8, nv)) + list(range(min(8, nv)))
+        my = [self.mfma_o(1, f // 4, f % 8, PB + 4 * (f % 4)) for f in order]
+        fy = []
+        if nv > 8:
+            for f in range(8):
+                for h in range(2):
+                    fy.append(self.vread(f, f % 8, h, key=-150 + 2 * f + h, earliest=f + 1, deadline=8 + f - 2))
+        # Q of the next item (persistent loop): no QK MFMA reads the Q registers from here on
+        for j in range(2):
+            for ks in range(KS):
+                fy.append(Inst(f"buffer_load_dwordx4 {rtxt('a', Q_(j, ks), 4)}, v{V_QOFF[j]}, s[{S_QD2}:{S_QD2 + 3}], 0 offen offset:{32 * ks}",
+                               VLOAD, rd=vr(V_QOFF[j]) + sr(S_QD2, 4), wr=ar(Q_(j, ks), 4), key=900 + 8 * j + ks))
+        t = S_TMP
+        fy += [Inst(f"s_add_u32 s{S_VOFF}, s{S_VOFF}, {TILE}", SALU, rd=sr(S_VOFF), wr=sr(S_VOFF) + [("scc", 0)], key=800),
+               Inst(f"s_sub_u32 s{t + 2}, s{S_VOFF}, {NSLOT * TILE}", SALU, rd=sr(S_VOFF), wr=sr(t + 2) + [("scc", 0)], key=801),
+               Inst(f"s_cmp_ge_u32 s{S_VOFF}, {VBASE + NSLOT * TILE}", SALU, rd=sr(S_VOFF), wr=[("scc", 0)], key=802),
+               Inst(f"s_cselect_b32 s{S_VOFF}, s{t + 2}, s{S_VOFF}", SALU, rd=sr(t + 2) + sr(S_VOFF) + [("scc", 0)], wr=sr(S_VOFF), key=803)]
+        ys = schedule(my, fy, budget=OPT_BUDGET)
+        return xs + ys, refits
+
     # ------------------------------------------------------------------ one pipelined step
     def step(self, p, variant, tag):
         """step n: phase X (QK(n+1) || softmax(n, b)), phase Y (PV(n) || softmax(n+1, a)).
@@ -311,6 +357,8 @@ class K:
         hidden.  Returns (instruction list, refit blocks)."""
         last = variant == "last"
         masked = variant in ("masked", "last")
+        if last and OPT_LAST2:
+            return self.step_last2(p, tag)
 
         def bias(j, st):
             if variant == "dead":
@@ -746,6 +794,8 @@ class K:
         for jj in range(1, NP):
             ins.append(I(f"v_add_u32_e32 v{V_VOFF + jj}, {64 * jj}, v{V_VOFF}", VALU, rd=vr(V_VOFF), wr=vr(V_VOFF + jj)))
         ins += [I(f"v_mov_b32_e32 v{V_NINF}, 0xff800000", VALU, wr=vr(V_NINF))]
+        if OPT_MFZERO:
+            ins += [I(f"v_mov_b32_e32 v{V_ZERO + i}, 0", VALU, wr=vr(V_ZERO + i)) for i in range(4)]
         if self.causal:
             # diagonal mask tiles: element g of a lane holds key (g & 3) + 8 (g >> 2) + 4 hh of the
             # subtile, query r = lane & 31 (v2)
@@ -1011,7 +1061,11 @@ class K:
         I = Inst
         ins = [I(f"s_mov_b32 s{S_N}, 0", SALU, wr=sr(S_N)),
                I(f"s_mov_b32 s{S_N0}, 0", SALU, wr=sr(S_N0))]
-        ins += [I(f"v_accvgpr_write_b32 a{i}, 0", ACCW, wr=ar(i)) for i in range(2 * NP * 16)]
+        if OPT_MFZERO:   # O = 0 x 0 + 0: one MFMA per 16 accumulators instead of 16 v_accvgpr_write
+            ins += [I(f"v_mfma_f32_32x32x16_{self.ty} {rtxt('a', 16 * i, 16)}, {rtxt('v', V_ZERO, 4)}, {rtxt('v', V_ZERO, 4)}, 0",
+                      MFMA, rd=vr(V_ZERO, 4), wr=ar(16 * i, 16)) for i in range(2 * NP)]
+        else:
+            ins += [I(f"v_accvgpr_write_b32 a{i}, 0", ACCW, wr=ar(i)) for i in range(2 * NP * 16)]
         ins += [I(f"v_mov_b32_e32 v{V_L[0]}, 0", VALU, wr=vr(V_L[0])),
                 I(f"v_mov_b32_e32 v{V_L[1]}, 0", VALU, wr=vr(V_L[1])),
                 I(f"v_mov_b32_e32 v{V_NEGMC[0]}, 0", VALU, wr=vr(V_NEGMC[0])),
@@ -1083,6 +1137,8 @@ class K:
 
     # ------------------------------------------------------------------ epilogue
     def epilogue(self):
+        if OPT_EPI2:
+            return self.epilogue2()
         ins = []
         t = 0   # the score registers are free after the last step
         for j in range(2):
@@ -1114,6 +1170,48 @@ class K:
                             Inst(f"v_permlane32_swap_b32_e32 v{w + 1}, v{w + 3}", PERM, rd=vr(w + 1) + vr(w + 3), wr=vr(w + 1) + vr(w + 3))]
                     ins.append(Inst(f"buffer_store_dwordx4 v[{w}:{w + 3}], v{V_OOFF[j]}, s[{S_OD}:{S_OD + 3}], 0 offen offset:{64 * dt + 16 * u}",
                                     VSTORE, rd=vr(w, 4) + vr(V_OOFF[j]) + sr(S_OD, 4)))
+        return ins
+
+    def epilogue2(self):
+        """the epilogue with its 2 NP x 2 groups (q-block, d-tile, column half) in two batches whose
+        stages (AGPR reads, 1 / l scaling, packs, lane-half swaps, stores) are interleaved across the
+        groups, so no instruction waits on its predecessor (registers: the score / pack VGPRs, free
+        after the last step)"""
+        ins = []
+        inv = (140, 141)       # 1 / l per q-block (the LSE math uses 142.. as temporaries)
+        for j in range(2):
+            l, lse, tt = V_L[j], 142, 143
+            ins += self.half_sum(l, tt)
+            ins += [Inst(f"v_rcp_f32_e32 v{inv[j]}, v{l}", TRANS, rd=vr(l), wr=vr(inv[j])),
+                    Inst(f"v_log_f32_e32 v{lse}, v{l}", TRANS, rd=vr(l), wr=vr(lse)),
+                    Inst(f"v_sub_f32_e32 v{lse}, v{lse}, v{V_NEGMC[j]}", VALU, rd=vr(lse) + vr(V_NEGMC[j]), wr=vr(lse)),
+                    Inst(f"v_mul_f32_e32 v{lse}, 0x3f317218, v{lse}", VALU, rd=vr(lse), wr=vr(lse)),
+                    Inst(f"v_cmp_neq_f32_e32 vcc, 0, v{l}", VALU, rd=vr(l), wr=[("vcc", 0)]),
+                    Inst(f"v_cmp_eq_f32_e64 s[{S_TMP}:{S_TMP + 1}], v{l}, v{l}", VALU, rd=vr(l), wr=sr(S_TMP, 2)),
+                    Inst(f"s_and_b64 vcc, vcc, s[{S_TMP}:{S_TMP + 1}]", SALU, rd=sr(S_TMP, 2) + [("vcc", 0)], wr=[("vcc", 0)]),
+                    Inst(f"v_cndmask_b32_e64 v{inv[j]}, 1.0, v{inv[j]}, vcc", VALU, rd=vr(inv[j]) + [("vcc", 0)], wr=vr(inv[j])),
+                    Inst(f"v_mov_b32_e32 v{tt}, 0x7f800000", VALU, wr=vr(tt)),
+                    Inst(f"v_cndmask_b32_e32 v{lse}, v{tt}, v{lse}, vcc", VALU, rd=vr(lse) + vr(tt) + [("vcc", 0)], wr=vr(lse)),
+                    Inst(f"buffer_store_dword v{lse}, v{V_LSEOFF[j]}, s[{S_LD}:{S_LD + 3}], 0 offen", VSTORE,
+                         rd=vr(lse) + vr(V_LSEOFF[j]) + sr(S_LD, 4))]
+        groups = [(j, dt, u) for j in range(2) for dt in range(NP) for u in (0, 2)]
+        nb = 8
+        for b0 in range(0, len(groups), nb):
+            stage = {k: [] for k in range(5)}
+            for gi, (j, dt, u) in enumerate(groups[b0:b0 + nb]):
+                x, w = 12 * gi, 12 * gi + 8
+                o = O_(j, dt) + 4 * u
+                stage[0] += [Inst(f"v_accvgpr_read_b32 v{x + k}, a{o + k}", ACCR, rd=ar(o + k), wr=vr(x + k)) for k in range(8)]
+                stage[1] += [Inst(f"v_mul_f32_e32 v{x + k}, v{x + k}, v{inv[j]}", VALU, rd=vr(x + k) + vr(inv[j]), wr=vr(x + k))
+                             for k in range(8)]
+                stage[2] += [self.cvt(w + 0, x + 0, x + 1), self.cvt(w + 1, x + 2, x + 3),
+                             self.cvt(w + 2, x + 4, x + 5), self.cvt(w + 3, x + 6, x + 7)]
+                stage[3] += [Inst(f"v_permlane32_swap_b32_e32 v{w}, v{w + 2}", PERM, rd=vr(w) + vr(w + 2), wr=vr(w) + vr(w + 2)),
+                             Inst(f"v_permlane32_swap_b32_e32 v{w + 1}, v{w + 3}", PERM, rd=vr(w + 1) + vr(w + 3), wr=vr(w + 1) + vr(w + 3))]
+                stage[4].append(Inst(f"buffer_store_dwordx4 v[{w}:{w + 3}], v{V_OOFF[j]}, s[{S_OD}:{S_OD + 3}], 0 offen offset:{64 * dt + 16 * u}",
+                                     VSTORE, rd=vr(w, 4) + vr(V_OOFF[j]) + sr(S_OD, 4)))
+            for k in range(5):
+                ins += stage[k]
         return ins
 
     # ------------------------------------------------------------------ whole kernel

@@ -1081,8 +1081,14 @@ static void run_bwd(const BwdParams& p, hipStream_t stream) {
   auto dq = [&](hipStream_t st) {
     dim3 grid(p.s.b * p.s.h * ((p.s.seqlen_q + DqTile<D>::BM - 1) / DqTile<D>::BM));
     prof_begin(kTimeBwdDq, st);
-    if (D == 128 && !DROPOUT && !masked && dq_asm_applicable(p))   // the assembly dQ kernel (fa_bwd_asm.cpp)
-      launch_bwd_dq_asm(p, BF16, st);
+    if (D == 128 && !DROPOUT && !masked && dq_asm_applicable(p)) {   // the assembly dQ kernel (fa_bwd_asm.cpp)
+      BwdParams pa = p;   // (persistent: heads grouped per XCD as in the forward, knob 7)
+      if (p.s.cu_seqlens_q == nullptr)
+        pa.dq_head_group = xcd_head_group((long long)p.s.b * p.s.h, (p.s.seqlen_q + 255) / 256,
+                                        4ll * p.s.b * p.s.seqlen_k * p.s.hk * p.s.d, p.s.causal,
+                                        knob(kKnobAsmXcdGroupMinMiB));
+      launch_bwd_dq_asm(pa, BF16, st);
+    }
     else if (masked)
       hipLaunchKernelGGL((bwd_dq_kernel<BF16, D, CAUSAL, DROPOUT, true>), grid, dim3(DqTile<D>::NW * 64), 0, st, p);
     else

@@ -434,8 +434,9 @@ __device__ inline void xcd_order_grouped(int L, int nbh, int nblk, int hp, int& 
 // +14% dQ).  causal = false: every block costs the same, one head per group.
 // The threshold is the FLASH_ATTN_MI355X_XCD_GROUP_MIN_MIB knob (default 256), and
 // FLASH_ATTN_MI355X_NO_XCD_GROUP=1 forces head-fastest order (fa_params.h Knob: read once).
-inline int xcd_head_group(long long nbh, long long nblk, long long stream_bytes, bool causal) {
-  if (knob(kKnobNoXcdGroup) == 1 || stream_bytes <= ((long long)knob(kKnobXcdGroupMinMiB) << 20)) return 0;
+inline int xcd_head_group(long long nbh, long long nblk, long long stream_bytes, bool causal, int min_mib = -1) {
+  if (min_mib < 0) min_mib = knob(kKnobXcdGroupMinMiB);
+  if (knob(kKnobNoXcdGroup) == 1 || stream_bytes <= ((long long)min_mib << 20)) return 0;
   if (nbh % 8 != 0 || nbh <= 0 || nblk <= 0) return 0;
   if (!causal) return 1;
   const long long h8 = nbh / 8;

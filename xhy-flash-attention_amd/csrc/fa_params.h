@@ -173,7 +173,9 @@ enum Knob { kKnobNoSplitKv = 0 /* FLASH_ATTN_MI355X_NO_SPLITKV: 1 = never split 
                                    workgroup per item, 1 = one persistent workgroup per CU */,
             kKnobBwdPersist = 6 /* FLASH_ATTN_MI355X_BWD_PERSIST: the same for the assembly dK/dV and
                                    dQ kernels */,
-            kNumKnobs = 7 };
+            kKnobAsmXcdGroupMinMiB = 7 /* FLASH_ATTN_MI355X_ASM_XCD_GROUP_MIN_MIB: knob 2's threshold
+                                          for the persistent assembly forward / dQ (default 0) */,
+            kNumKnobs = 8 };
 int knob(int id);
 void set_knob(int id, int value);
 
