@@ -159,6 +159,7 @@ OPT_ALIGN = int(os.environ.get("FA_GEN_ALIGN", "0"))          # .p2align N befor
 OPT_MFZERO = os.environ.get("FA_GEN_MFZERO") == "1"          # zero O with 2 NP MFMAs (zero operands)
 OPT_EPI2 = os.environ.get("FA_GEN_EPI2") == "1"              # epilogue: groups interleaved stage by stage
 OPT_LAST2 = os.environ.get("FA_GEN_LAST2") == "1"            # last step: PV(a) under softmax(b), then PV(b)
+OPT_NOGUARD = os.environ.get("FA_GEN_NOGUARD") == "1"        # ablation (wrong on a refit): no guard branch
 V_ZERO = 228      # 228..231: zeros (MFMA operands of the O zeroing)
 OPT_STAMP = os.environ.get("FA_GEN_STAMP") in ("1", "2")
 # FA_GEN_STAMP=2 also sums, per wave, the cycles of each step's compute, its vmcnt/lgkmcnt wait and
@@ -297,6 +298,10 @@ class K:
     def guard_ops(self, j, refit_label, key, deadline=None):
         """partial sum <= 2^8 on every lane (and not NaN), else refit; then l += partial.  The branch
         and its return label are one instruction so that nothing is scheduled between them."""
+        add = Inst(f"v_add_f32_e32 v{V_L[j]}, v{V_L[j]}, v{V_PS[j]}", VALU, rd=vr(V_L[j]) + vr(V_PS[j]),
+                   wr=vr(V_L[j]), key=key, deadline=deadline)
+        if OPT_NOGUARD:
+            return [Inst(f"{refit_label}_back:", LABEL, key=key), add]
         cmp = Inst(f"v_cmp_nge_f32_e32 vcc, 0x43800000, v{V_PS[j]}", VALU, rd=vr(V_PS[j]), wr=[("vcc", 0)],
                    key=key, deadline=deadline)
         sc = Inst("s_cmp_lg_u64 vcc, 0", SALU, rd=[("vcc", 0)], wr=[("scc", 0)], key=key, deadline=deadline)

@@ -641,7 +641,7 @@ static void run_fwd(const FwdParams& p, hipStream_t stream) {
   if constexpr (!DROPOUT && (D == 128 || D == 64)) {   // hand-scheduled assembly kernels (fa_fwd_asm.cpp)
     // the persistent assembly forward groups heads per XCD below the Infinity-Cache threshold too
     // (knob 7): a head's K/V is then streamed by many CUs of one XCD at once and served from its L2
-    // (C3: forward -0.5 to -0.9 %, profiles/r04/ab_xcd_group_r04d.txt)
+    // (C3: forward -0.5 to -0.9 %, profiles/r04/ab_asm_xcd_group_c3_r04e.txt)
     FwdParams pa = p;
     if (pa.n_split == 0 && pa.pack_g == 1 && p.s.cu_seqlens_q == nullptr)   // (varlen: device-built list)
       pa.head_group = xcd_head_group((long long)p.s.b * p.s.h, p.num_m_blocks, 4ll * p.s.b * p.s.seqlen_k * p.s.hk * p.s.d,
