@@ -160,6 +160,7 @@ OPT_MFZERO = os.environ.get("FA_GEN_MFZERO") == "1"          # zero O with 2 NP 
 OPT_EPI2 = os.environ.get("FA_GEN_EPI2") == "1"              # epilogue: groups interleaved stage by stage
 OPT_LAST2 = os.environ.get("FA_GEN_LAST2") == "1"            # last step: PV(a) under softmax(b), then PV(b)
 OPT_NOGUARD = os.environ.get("FA_GEN_NOGUARD") == "1"        # ablation (wrong on a refit): no guard branch
+OPT_T0OV = os.environ.get("FA_GEN_T0OV") == "1"              # tile 0: QK(a), then QK(b) || max / softmax(a)
 V_ZERO = 228      # 228..231: zeros (MFMA operands of the O zeroing)
 OPT_STAMP = os.environ.get("FA_GEN_STAMP") in ("1", "2")
 # FA_GEN_STAMP=2 also sums, per wave, the cycles of each step's compute, its vmcnt/lgkmcnt wait and
@@ -1096,11 +1097,14 @@ class K:
         for f in range(2 * KS):
             reads.append(self.kread(f, f % 8, key=f, earliest=max(2 * (f - 3), 2 * (f - 8) + 3) if f >= 3 else None,
                                     deadline=2 * f - 1 if f >= 3 else 0))
-        body = schedule(mfm, reads)
-        ins += body
-        ins.append(nop(15))
+        if OPT_T0OV:
+            ins += self.tile0_overlapped()
+        else:
+            body = schedule(mfm, reads)
+            ins += body
+            ins.append(nop(15))
         ins += self.dump("pro_qk")
-        for j, sreg in ((0, SA), (1, SB(0))):
+        for j, sreg in ((((1, SB(0)),) if OPT_T0OV else ((0, SA), (1, SB(0))))):
             ins += self.mask_ops(j, sreg, (S_N0, 0), V_LM)
             mx = V_T + 2
             ins.append(Inst(f"v_max3_f32 v{mx}, v{sreg}, v{sreg + 1}, v{sreg + 2}", VALU, rd=vr(sreg, 3), wr=vr(mx)))
@@ -1116,9 +1120,10 @@ class K:
                     Inst(f"v_cmp_eq_f32_e32 vcc, v{V_NINF}, v{mx}", VALU, rd=vr(V_NINF) + vr(mx), wr=[("vcc", 0)]),
                     Inst(f"v_cndmask_b32_e64 v{V_NEGMC[j]}, v{V_NEGMC[j]}, 0, vcc", VALU,
                          rd=vr(V_NEGMC[j]) + [("vcc", 0)], wr=vr(V_NEGMC[j]))]
-        sm, _ = self.softmax_ops(0, SA, PA(0), False, None, key0=0)
-        ins += sm
-        ins += [Inst(f"v_mov_b32_e32 v{V_L[0]}, v{V_PS[0]}", VALU, rd=vr(V_PS[0]), wr=vr(V_L[0]))]
+        if not OPT_T0OV:
+            sm, _ = self.softmax_ops(0, SA, PA(0), False, None, key0=0)
+            ins += sm
+            ins += [Inst(f"v_mov_b32_e32 v{V_L[0]}, v{V_PS[0]}", VALU, rd=vr(V_PS[0]), wr=vr(V_L[0]))]
         ins += self.dump("pro_end")
         ins += self.stamp_point(6)
         # V reads tile 0 (slot S_KOFF); S_KOFF -> tile 1 (the LAST step's refit takes S_KOFF - TILE)
@@ -1139,6 +1144,50 @@ class K:
                 I(f"s_cbranch_scc1 {l_entry_fast}", BRANCH),
                 I(f"s_branch {l_entry_masked}", BRANCH)]
         return ins
+
+    def tile0_maxops(self, j, sreg, key):
+        """mask, explicit row max and -m c of q-block j's first tile (tile 0)"""
+        ops = self.mask_ops(j, sreg, (S_N0, 0), V_LM, key0=key)
+        mx = V_T + 2
+        ops.append(Inst(f"v_max3_f32 v{mx}, v{sreg}, v{sreg + 1}, v{sreg + 2}", VALU, rd=vr(sreg, 3), wr=vr(mx), key=key + 200))
+        for e in range(3, 32, 2):
+            if e + 1 < 32:
+                ops.append(Inst(f"v_max3_f32 v{mx}, v{mx}, v{sreg + e}, v{sreg + e + 1}", VALU, rd=vr(mx) + vr(sreg + e, 2),
+                                wr=vr(mx), key=key + 200))
+            else:
+                ops.append(Inst(f"v_max_f32_e32 v{mx}, v{mx}, v{sreg + e}", VALU, rd=vr(mx) + vr(sreg + e), wr=vr(mx), key=key + 200))
+        for op in self.half_max(mx, V_T + 3):
+            op.key = key + 200
+            ops.append(op)
+        ops += [Inst(f"v_mul_f32_e32 v{V_T + 4}, s{S_C}, v{mx}", VALU, rd=sr(S_C) + vr(mx), wr=vr(V_T + 4), key=key + 200),
+                Inst(f"v_sub_f32_e32 v{V_NEGMC[j]}, 0, v{V_T + 4}", VALU, rd=vr(V_T + 4), wr=vr(V_NEGMC[j]), key=key + 200),
+                Inst(f"v_cmp_eq_f32_e32 vcc, v{V_NINF}, v{mx}", VALU, rd=vr(V_NINF) + vr(mx), wr=[("vcc", 0)], key=key + 200),
+                Inst(f"v_cndmask_b32_e64 v{V_NEGMC[j]}, v{V_NEGMC[j]}, 0, vcc", VALU,
+                     rd=vr(V_NEGMC[j]) + [("vcc", 0)], wr=vr(V_NEGMC[j]), key=key + 200)]
+        return ops
+
+    def tile0_overlapped(self):
+        """tile 0's QK with q-block a's MFMAs first: a's mask, max and softmax run in the gaps of b's
+        MFMAs (K fragments re-read for b at d = 128, where the 8-slot ring cannot hold all 16)"""
+        mfm = []
+        for j in range(2):
+            for st in range(2):
+                for ks in range(KS):
+                    f = st * KS + ks
+                    sreg = (SA if j == 0 else SB(0)) + 16 * st
+                    mfm.append(self.mfma_s(sreg, f % 8, j, ks, ks == 0))
+        n2 = 2 * KS
+        fill = []
+        for f in range(n2):
+            fill.append(self.kread(f, f % 8, key=-100 + f, earliest=(f - 8) if f >= 8 else None, deadline=max(f - 2, 0)))
+        if n2 > 8:
+            for f in range(n2):
+                fill.append(self.kread(f, f % 8, key=-60 + f, earliest=f + 8, deadline=n2 + f - 2))
+        fill += self.tile0_maxops(0, SA, key=0)
+        sm, _ = self.softmax_ops(0, SA, PA(0), False, None, key0=400)
+        fill += sm
+        fill += [Inst(f"v_mov_b32_e32 v{V_L[0]}, v{V_PS[0]}", VALU, rd=vr(V_PS[0]), wr=vr(V_L[0]), key=700)]
+        return schedule(mfm, fill) + [nop(15)]
 
     # ------------------------------------------------------------------ epilogue
     def epilogue(self):
