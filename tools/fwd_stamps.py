@@ -36,6 +36,7 @@ def main():
     ap.add_argument("--workload", default="c3")
     ap.add_argument("--warm-s", type=float, default=2.0)
     ap.add_argument("--samples", type=int, default=3)
+    ap.add_argument("--epi", action="store_true", help="library built with FA_GEN_STAMP=3 (epilogue parts)")
     args = ap.parse_args()
     lib = load(args.lib)
     lib.flash_attn_debug_fwd_stamps.argtypes = [ctypes.c_void_p]
@@ -92,7 +93,9 @@ def main():
                 row[f"{nm}_per_step_med"] = float(np.median(a[:, i] / np.maximum(steps, 1)))
             row["steps_med"] = float(np.median(steps))
             items = np.maximum(a[:, 9], 1)
-            for i, nm in ((20, "tile0"), (21, "last_step"), (22, "epilogue"), (23, "item_start")):
+            names = (("epi_lse", "last_step", "epi_o_b", "epi_o_a") if args.epi else
+                     ("tile0", "last_step", "epilogue", "item_start"))
+            for i, nm in zip((20, 21, 22, 23), names):
                 row[f"{nm}_per_item_med"] = float(np.median(a[:, i] / items))
         rows.append(row)
         print(" ".join(f"{k}={v:.4g}" if isinstance(v, float) else f"{k}={v}" for k, v in row.items()), flush=True)

@@ -162,10 +162,13 @@ OPT_LAST2 = os.environ.get("FA_GEN_LAST2") == "1"            # last step: PV(a) 
 OPT_NOGUARD = os.environ.get("FA_GEN_NOGUARD") == "1"        # ablation (wrong on a refit): no guard branch
 OPT_T0OV = os.environ.get("FA_GEN_T0OV") == "1"              # tile 0: QK(a), then QK(b) || max / softmax(a)
 V_ZERO = 228      # 228..231: zeros (MFMA operands of the O zeroing)
-OPT_STAMP = os.environ.get("FA_GEN_STAMP") in ("1", "2")
+OPT_STAMP = os.environ.get("FA_GEN_STAMP") in ("1", "2", "3")
 # FA_GEN_STAMP=2 also sums, per wave, the cycles of each step's compute, its vmcnt/lgkmcnt wait and
 # its barrier wait (s_memtime around the step-end wait and barrier; perturbs the schedule a little)
-OPT_STEPSTAMP = os.environ.get("FA_GEN_STAMP") == "2"
+OPT_STEPSTAMP = os.environ.get("FA_GEN_STAMP") in ("2", "3")
+# FA_GEN_STAMP=3: the tile-0 / item-start accumulators time the epilogue's parts instead (LSE of both
+# q-blocks -> tile 0's slot, O of q-block a -> item start's slot, O of q-block b -> the epilogue's)
+OPT_EPISTAMP = os.environ.get("FA_GEN_STAMP") == "3"
 V_SSUM = 240      # 240..244: compute, wait, barrier sums, step count, last stamp;
                   # 246..249: item phases: tile 0, last step, epilogue, item start (geometry .. tile 0's barrier)
 # latency-aware gap scheduling (isa.schedule lat=): "valu,trans,lds,mfma" result latencies in cycles
@@ -1083,7 +1086,7 @@ class K:
         row max, P(0, a); then into the step loop"""
         I = Inst
         ins = [I(f"s_waitcnt vmcnt({2 * NP})", WAIT), I("s_barrier", BARRIER)]
-        ins += self.stamp_point(9)
+        ins += [] if OPT_EPISTAMP else self.stamp_point(9)
         ins += self.dump("pro_lds")
         ins += [I(f"v_add_u32_e32 v{V_KB0}, s{S_KOFF}, v{V_RB0}", VALU, rd=sr(S_KOFF) + vr(V_RB0), wr=vr(V_KB0)),
                 I(f"v_add_u32_e32 v{V_KB1}, s{S_KOFF}, v{V_RB1}", VALU, rd=sr(S_KOFF) + vr(V_RB1), wr=vr(V_KB1))]
@@ -1125,7 +1128,7 @@ class K:
             ins += sm
             ins += [Inst(f"v_mov_b32_e32 v{V_L[0]}, v{V_PS[0]}", VALU, rd=vr(V_PS[0]), wr=vr(V_L[0]))]
         ins += self.dump("pro_end")
-        ins += self.stamp_point(6)
+        ins += [] if OPT_EPISTAMP else self.stamp_point(6)
         # V reads tile 0 (slot S_KOFF); S_KOFF -> tile 1 (the LAST step's refit takes S_KOFF - TILE)
         ins += [I(f"s_add_u32 s{S_VOFF}, s{S_KOFF}, {VBASE}", SALU),
                 I(f"s_add_u32 s{S_KOFF}, s{S_KOFF}, {TILE}", SALU),
@@ -1211,6 +1214,8 @@ class K:
                     Inst(f"v_cndmask_b32_e32 v{lse}, v{t + 3}, v{lse}, vcc", VALU, rd=vr(lse) + vr(t + 3) + [("vcc", 0)], wr=vr(lse)),
                     Inst(f"buffer_store_dword v{lse}, v{V_LSEOFF[j]}, s[{S_LD}:{S_LD + 3}], 0 offen", VSTORE,
                          rd=vr(lse) + vr(V_LSEOFF[j]) + sr(S_LD, 4))]
+            if OPT_EPISTAMP:
+                ins += self.stamp_point(6)
             for dt in range(NP):
                 for u in (0, 2):
                     w = t + 4 + 4 * ((dt * 2 + u // 2) % 4)
@@ -1224,6 +1229,8 @@ class K:
                             Inst(f"v_permlane32_swap_b32_e32 v{w + 1}, v{w + 3}", PERM, rd=vr(w + 1) + vr(w + 3), wr=vr(w + 1) + vr(w + 3))]
                     ins.append(Inst(f"buffer_store_dwordx4 v[{w}:{w + 3}], v{V_OOFF[j]}, s[{S_OD}:{S_OD + 3}], 0 offen offset:{64 * dt + 16 * u}",
                                     VSTORE, rd=vr(w, 4) + vr(V_OOFF[j]) + sr(S_OD, 4)))
+            if OPT_EPISTAMP and j == 0:
+                ins += self.stamp_point(9)
         return ins
 
     def epilogue2(self):
