@@ -291,6 +291,10 @@ class Emu:
             if w.scc:
                 w.pc = self.labels[a[0]]
             return
+        if op in ("s_cbranch_vccnz", "s_cbranch_vccz"):
+            if w.vcc.any() == (op == "s_cbranch_vccnz"):
+                w.pc = self.labels[a[0]]
+            return
         if op.startswith("s_load_dword"):
             n = {"s_load_dword": 1, "s_load_dwordx2": 2, "s_load_dwordx4": 4, "s_load_dwordx8": 8,
                  "s_load_dwordx16": 16}[op]

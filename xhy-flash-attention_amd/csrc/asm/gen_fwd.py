@@ -151,6 +151,7 @@ OPT_NOZERO = os.environ.get("FA_GEN_NOZERO") == "1"          # never zero K/V re
 OPT_NODIAG = os.environ.get("FA_GEN_NODIAG") == "1"          # causal diagonal: generic masked steps only
 OPT_PLAIN_SNAKE = os.environ.get("FA_GEN_PLAIN_SNAKE") == "1"  # snake reversal over single workgroups
 OPT_BUDGET = int(os.environ.get("FA_GEN_BUDGET", "24"))        # filler issue cycles per MFMA gap
+OPT_BUDGET64 = int(os.environ.get("FA_GEN_BUDGET64", str(OPT_BUDGET)))  # ... at head dim 64
 OPT_ZERO_NOP = int(os.environ.get("FA_GEN_ZERO_NOP", "0"))    # s_nop 15 x N before zeroing them
 OPT_SHIFT = int(os.environ.get("FA_GEN_SHIFT", "0"))          # s_nop 0 x N at the kernel entry (code placement)
 OPT_ALIGN = int(os.environ.get("FA_GEN_ALIGN", "0"))          # .p2align N before each step body (code placement)
@@ -161,6 +162,9 @@ OPT_EPI2 = os.environ.get("FA_GEN_EPI2") == "1"              # epilogue: groups 
 OPT_LAST2 = os.environ.get("FA_GEN_LAST2") == "1"            # last step: PV(a) under softmax(b), then PV(b)
 OPT_NOGUARD = os.environ.get("FA_GEN_NOGUARD") == "1"        # ablation (wrong on a refit): no guard branch
 OPT_T0OV = os.environ.get("FA_GEN_T0OV") == "1"              # tile 0: QK(a), then QK(b) || max / softmax(a)
+# guard: compare as soon as the partial sum is complete, branch on vcc later (round 4 default: the
+# compare + s_cmp + branch in one place stalled the wave, 1.3 % at C3; FA_GEN_GUARD1=1 restores it)
+OPT_GUARD2 = os.environ.get("FA_GEN_GUARD1") != "1"
 V_ZERO = 228      # 228..231: zeros (MFMA operands of the O zeroing)
 OPT_STAMP = os.environ.get("FA_GEN_STAMP") in ("1", "2", "3")
 # FA_GEN_STAMP=2 also sums, per wave, the cycles of each step's compute, its vmcnt/lgkmcnt wait and
@@ -314,6 +318,19 @@ class K:
                    wr=vr(V_L[j]), key=key, deadline=deadline)
         return [cmp, sc, br, add]
 
+    def guard_cmp(self, j, key):
+        """(FA_GEN_GUARD2) the guard's compare alone: vcc = partial sum > 2^8 or NaN.  Scheduled as
+        soon as the sum is complete; the branch reads vcc later, so the wave does not stall on it."""
+        return Inst(f"v_cmp_nge_f32_e32 vcc, 0x43800000, v{V_PS[j]}", VALU, rd=vr(V_PS[j]), wr=[("vcc", 0)], key=key)
+
+    def guard_br(self, j, refit_label, key, deadline=None, eg=None):
+        """(FA_GEN_GUARD2) branch to the refit on vcc (all lanes are active), then l += partial"""
+        br = Inst(f"s_cbranch_vccnz {refit_label}\n{refit_label}_back:", BRANCH, rd=[("vcc", 0)], key=key,
+                  deadline=deadline, earliest=eg)
+        add = Inst(f"v_add_f32_e32 v{V_L[j]}, v{V_L[j]}, v{V_PS[j]}", VALU, rd=vr(V_L[j]) + vr(V_PS[j]),
+                   wr=vr(V_L[j]), key=key, deadline=deadline, earliest=eg)
+        return [br, add]
+
     # ------------------------------------------------------------------ the item's last step (no QK)
     def step_last2(self, p, tag):
         """the last step (tile n = the item's last, no QK(n+1)): phase X runs PV(n) of q-block a --
@@ -335,7 +352,7 @@ class K:
         rl_b = self.lab(f"{tag}_refit_b")
         refits.append(self.refit(1, SB(p), PB, rl_b, tile_add=0, phase="Y"))
         fx += self.guard_ops(1, rl_b, key=600)
-        xs = schedule(mx, fx, budget=OPT_BUDGET)
+        xs = schedule(mx, fx, budget=(OPT_BUDGET64 if D == 64 else OPT_BUDGET))
         order = list(range(8, nv)) + list(range(min(8, nv)))
         my = [self.mfma_o(1, f // 4, f % 8, PB + 4 * (f % 4)) for f in order]
         fy = []
@@ -353,7 +370,7 @@ class K:
                Inst(f"s_sub_u32 s{t + 2}, s{S_VOFF}, {NSLOT * TILE}", SALU, rd=sr(S_VOFF), wr=sr(t + 2) + [("scc", 0)], key=801),
                Inst(f"s_cmp_ge_u32 s{S_VOFF}, {VBASE + NSLOT * TILE}", SALU, rd=sr(S_VOFF), wr=[("scc", 0)], key=802),
                Inst(f"s_cselect_b32 s{S_VOFF}, s{t + 2}, s{S_VOFF}", SALU, rd=sr(t + 2) + sr(S_VOFF) + [("scc", 0)], wr=sr(S_VOFF), key=803)]
-        ys = schedule(my, fy, budget=OPT_BUDGET)
+        ys = schedule(my, fy, budget=(OPT_BUDGET64 if D == 64 else OPT_BUDGET))
         return xs + ys, refits
 
     # ------------------------------------------------------------------ one pipelined step
@@ -404,11 +421,13 @@ class K:
         # softmax (n, b)
         sm_b, sum_b = self.softmax_ops(1, SB(p), PB, masked, (S_N0, 0), key0=0)
         fx += sm_b
+        if OPT_GUARD2:
+            fx.append(self.guard_cmp(1, key=1))
         # V fragments of d-tiles 0 and 1 (8 frags) for phase Y
         for f in range(8):
             for h in range(2):
                 fx.append(self.vread(f, f % 8, h, key=-80 + 2 * f + h, earliest=max(0, NX - 18 + 2 * f) if not last else None))
-        xs = schedule(mx, fx, budget=OPT_BUDGET, lat=OPT_LAT) if mx else schedule([], fx)
+        xs = schedule(mx, fx, budget=(OPT_BUDGET64 if D == 64 else OPT_BUDGET), lat=OPT_LAT) if mx else schedule([], fx)
         # ---------------- phase Y
         my = []
         for i in range(NY):
@@ -420,7 +439,10 @@ class K:
         fy = []
         rl_b = self.lab(f"{tag}_refit_b")
         refits.append(self.refit(1, SB(p), PB, rl_b, tile_add=0, phase="Y"))
-        fy += self.guard_ops(1, rl_b, key=-200, deadline=4)
+        if OPT_GUARD2:
+            fy += self.guard_br(1, rl_b, key=-200, deadline=4)
+        else:
+            fy += self.guard_ops(1, rl_b, key=-200, deadline=4)
         # V fragments of d-tiles 2, 3
         for f in range(8, 4 * NP):
             dt, kk = f // 4, f % 4
@@ -465,10 +487,13 @@ class K:
             refits.append(self.refit(0, SA, PA(p ^ 1), rl_a, tile_add=64, phase="end"))
             # after the phase's LAST MFMA: refit_a borrows the V fragment ring as scratch and rescales
             # O_a, so no PV MFMA may still be pending (placed earlier, it corrupted the d-tile 3 MFMAs)
-            ga = self.guard_ops(0, rl_a, key=700)
-            for op in ga:
-                op.eg = NY - 1
-            fy += ga
+            if OPT_GUARD2:
+                fy += [self.guard_cmp(0, key=700)] + self.guard_br(0, rl_a, key=700, eg=NY - 1)
+            else:
+                ga = self.guard_ops(0, rl_a, key=700)
+                for op in ga:
+                    op.eg = NY - 1
+                fy += ga
         if last:
             # Q of the next item (persistent loop): the Q registers are idle from here on (no QK MFMA
             # in the last step; the refit of q-block b, which reads them, returns before MFMA 4)
@@ -481,7 +506,7 @@ class K:
                Inst(f"s_sub_u32 s{t + 2}, s{S_VOFF}, {NSLOT * TILE}", SALU, rd=sr(S_VOFF), wr=sr(t + 2) + [("scc", 0)], key=801),
                Inst(f"s_cmp_ge_u32 s{S_VOFF}, {VBASE + NSLOT * TILE}", SALU, rd=sr(S_VOFF), wr=[("scc", 0)], key=802),
                Inst(f"s_cselect_b32 s{S_VOFF}, s{t + 2}, s{S_VOFF}", SALU, rd=sr(t + 2) + sr(S_VOFF) + [("scc", 0)], wr=sr(S_VOFF), key=803)]
-        ys = schedule(my, fy, budget=OPT_BUDGET, lat=OPT_LAT)
+        ys = schedule(my, fy, budget=(OPT_BUDGET64 if D == 64 else OPT_BUDGET), lat=OPT_LAT)
         body = xs + ys
         if not last and OPT_STEPSTAMP:
             A, B, t0 = S_TMP, S_TMP + 2, V_T
