@@ -15,8 +15,8 @@ sys.path.insert(0, ROOT)
 
 import torch  # noqa: E402
 
-from bench import KernelTimer, flops_fwd  # noqa: E402
-from flash_attn import flash_attn_func  # noqa: E402
+from bench import KernelTimer, c4_seqlens, flops_fwd, varlen_flops_fwd  # noqa: E402
+from flash_attn import flash_attn_func, flash_attn_varlen_qkvpacked_func  # noqa: E402
 from knobs import knob  # noqa: E402
 
 
@@ -31,6 +31,7 @@ def main():
     ap.add_argument("--d", type=int, default=128)
     ap.add_argument("--causal", type=int, default=1)
     ap.add_argument("--bwd", action="store_true")
+    ap.add_argument("--c4", action="store_true", help="the C4 varlen qkvpacked workload (--h / --d apply)")
     ap.add_argument("--rounds", type=int, default=4)
     ap.add_argument("--iters", type=int, default=10)
     a = ap.parse_args()
@@ -43,8 +44,19 @@ def main():
     dout = torch.randn(a.b, a.s, a.h, a.d, device="cuda", dtype=torch.bfloat16, generator=g)
     timer = KernelTimer()
     res = {x: {} for x in values}
+    if a.c4:
+        lens = c4_seqlens()
+        cu = torch.tensor([0] + torch.tensor(lens).cumsum(0).tolist(), dtype=torch.int32, device="cuda")
+        qkv = torch.randn(sum(lens), 3, a.h, a.d, device="cuda", dtype=torch.bfloat16, generator=g).requires_grad_()
+        dout = torch.randn(sum(lens), a.h, a.d, device="cuda", dtype=torch.bfloat16, generator=g)
 
     def step():
+        if a.c4:
+            with torch.set_grad_enabled(a.bwd):
+                out = flash_attn_varlen_qkvpacked_func(qkv, cu, max(lens), causal=bool(a.causal))
+                if a.bwd:
+                    torch.autograd.grad(out, (qkv,), dout)
+            return
         if a.bwd:
             out = flash_attn_func(q, k, v, causal=bool(a.causal))
             torch.autograd.grad(out, (q, k, v), dout)
@@ -64,7 +76,7 @@ def main():
                 torch.cuda.synchronize()
                 for name, r in timer.stop().items():
                     res[x].setdefault(name, []).append(r["avg_ms"])
-    f = flops_fwd(a.b, a.s, a.h, a.d, bool(a.causal))
+    f = varlen_flops_fwd(lens, a.h, a.d, bool(a.causal)) if a.c4 else flops_fwd(a.b, a.s, a.h, a.d, bool(a.causal))
     fac = {"fwd_kernel": 1.0, "bwd_dkdv_kernel": 2.0, "bwd_dq_kernel": 1.5}
     for x in values:
         parts = []

@@ -165,6 +165,23 @@ OPT_T0OV = os.environ.get("FA_GEN_T0OV") == "1"              # tile 0: QK(a), th
 # guard: compare as soon as the partial sum is complete, branch on vcc later (round 4 default: the
 # compare + s_cmp + branch in one place stalled the wave, 1.3 % at C3; FA_GEN_GUARD1=1 restores it)
 OPT_GUARD2 = os.environ.get("FA_GEN_GUARD1") != "1"
+# epilogue ablations (wrong results; with FA_GEN_STAMP=3 they split its cost): no O stores / only them
+OPT_EPI_ABL = os.environ.get("FA_GEN_EPI_ABL", "")
+# deferred epilogue stores: the epilogue leaves O (packed) and the LSE in registers that the next
+# item's tile 0 does not touch, and its O / LSE stores issue in the gaps of that tile 0's MFMAs --
+# after its s_waitcnt (vmcnt counts stores: stores queued ahead of the wait were waited for) and
+# spread one per gap (a store of 32 rows x 32 bytes holds the wave's issue for ~76 cycles)
+OPT_DEFER = os.environ.get("FA_GEN_DEFER") == "1"
+V_LSEV = (191, 195)                   # LSE values of the finished item (deferred stores)
+V_SAVE = (228, 229, 230, 231, 238, 239)   # its O / LSE descriptor words 0..2 across the warm start
+S_ODD, S_LDD = 88, 36                 # ... restored here for tile 0 (geometry temps, free by then)
+
+
+def PKR(j, dt, u):
+    """(deferred stores) packed O of q-block j, d-tile dt, column half u: v64..95 and v112..143 (S(1)
+    / P(1) / P(b): idle in tile 0)"""
+    i = 32 * j + 4 * (2 * dt + u // 2)
+    return 64 + i if i < 32 else 112 + (i - 32)
 V_ZERO = 228      # 228..231: zeros (MFMA operands of the O zeroing)
 OPT_STAMP = os.environ.get("FA_GEN_STAMP") in ("1", "2", "3")
 # FA_GEN_STAMP=2 also sums, per wave, the cycles of each step's compute, its vmcnt/lgkmcnt wait and
@@ -208,8 +225,9 @@ class K:
         if not OPT_STEPSTAMP:
             return []
         t0 = V_T
-        return [Inst(f"s_memtime s[{S_TMP}:{S_TMP + 1}]", SMEM), Inst("s_waitcnt lgkmcnt(0)", WAIT),
-                Inst(f"v_mov_b32_e32 v{t0}, s{S_TMP}", VALU),
+        # (s[100:101]: dead at every stamp point; S_TMP may hold the deferred LSE descriptor)
+        return [Inst(f"s_memtime s[{S_SWT}:{S_SWT + 1}]", SMEM), Inst("s_waitcnt lgkmcnt(0)", WAIT),
+                Inst(f"v_mov_b32_e32 v{t0}, s{S_SWT}", VALU),
                 Inst(f"v_sub_u32_e32 v{t0 + 1}, v{t0}, v{V_SSUM + 4}", VALU),
                 Inst(f"v_add_u32_e32 v{V_SSUM + acc}, v{V_SSUM + acc}, v{t0 + 1}", VALU),
                 Inst(f"v_mov_b32_e32 v{V_SSUM + 4}, v{t0}", VALU)]
@@ -1052,7 +1070,10 @@ class K:
         I = Inst
         ins = []
         # ---- cold
-        ins += [label(l_cold_wait), Inst("s_waitcnt vmcnt(0) lgkmcnt(0)", WAIT), Inst("s_barrier", BARRIER),
+        ins += [label(l_cold_wait)]
+        if OPT_DEFER:
+            ins += self.defer_stores(S_OD, S_LD)
+        ins += [Inst("s_waitcnt vmcnt(0) lgkmcnt(0)", WAIT), Inst("s_barrier", BARRIER),
                 label(l_cold)]
         ins += self.item_pos(S_SWT, 0)
         ins += [I(f"s_cmp_ge_u32 s{S_SWT}, s{S_NITEMS}", SALU), I(f"s_cbranch_scc1 {l_end}", BRANCH)]
@@ -1083,12 +1104,29 @@ class K:
         ins += [label(l_warm)]
         ins += self.item_pos(S_SWT, 0)
         ins += [I(f"s_mov_b32 s{S_QD + i}, s{S_QD2 + i}", SALU) for i in range(4)]
-        ins += self.item_geom("warm", l_skip)
+        restore = []
+        l_skip_w = l_skip
+        if OPT_DEFER:
+            assert not OPT_MFZERO
+            ins += [I(f"v_mov_b32_e32 v{V_SAVE[i]}, s{S_OD + i}", VALU, rd=sr(S_OD + i), wr=vr(V_SAVE[i])) for i in range(3)]
+            ins += [I(f"v_mov_b32_e32 v{V_SAVE[3 + i]}, s{S_LD + i}", VALU, rd=sr(S_LD + i), wr=vr(V_SAVE[3 + i])) for i in range(3)]
+            restore = []
+            for i in range(6):
+                sd = S_ODD + i if i < 3 else S_LDD + i - 3
+                restore += [nop(0), I(f"v_readfirstlane_b32 s{sd}, v{V_SAVE[i]}", RFL, rd=vr(V_SAVE[i]), wr=sr(sd))]
+            restore += [I(f"s_mov_b32 s{S_ODD + 3}, 0x20000", SALU, wr=sr(S_ODD + 3)),
+                        I(f"s_mov_b32 s{S_LDD + 3}, 0x20000", SALU, wr=sr(S_LDD + 3))]
+            l_skip_w = self.lab("skipw")
+        ins += self.item_geom("warm", l_skip_w)
         ins += self.item_geom("next", None)
         ins += [I(f"s_mov_b32 s{S_WARM}, 0", SALU),
                 I(f"s_sub_u32 s{S_KOFF}, s{S_VOFF}, {VBASE}", SALU)]
         ins += self.item_zero()
+        ins += restore
         ins += self.dma_tile_ops("w3")
+        if OPT_DEFER:
+            ins += [nop(5), I(f"s_branch {self.l_tile0w}", BRANCH),
+                    label(l_skip_w)] + restore + [nop(5)] + self.defer_stores(S_ODD, S_LDD) + [I(f"s_branch {l_skip}", BRANCH)]
         return ins
 
     def item_zero(self):
@@ -1106,7 +1144,7 @@ class K:
                 I(f"v_mov_b32_e32 v{V_NEGMC[1]}, 0", VALU, wr=vr(V_NEGMC[1]))]
         return ins
 
-    def tile0(self, l_entry_last, l_entry_fast, l_entry_masked):
+    def tile0(self, l_entry_last, l_entry_fast, l_entry_masked, stores=False):
         """Q + tiles 0, 1, 2 landed (tile 3 in flight); tile 0: S(0, a), S(0, b) -> masked, explicit
         row max, P(0, a); then into the step loop"""
         I = Inst
@@ -1125,7 +1163,10 @@ class K:
         for f in range(2 * KS):
             reads.append(self.kread(f, f % 8, key=f, earliest=max(2 * (f - 3), 2 * (f - 8) + 3) if f >= 3 else None,
                                     deadline=2 * f - 1 if f >= 3 else 0))
+        if stores:
+            reads += self.defer_stores(S_ODD, S_LDD, spread=NX)
         if OPT_T0OV:
+            assert not stores
             ins += self.tile0_overlapped()
         else:
             body = schedule(mfm, reads)
@@ -1218,6 +1259,24 @@ class K:
         return schedule(mfm, fill) + [nop(15)]
 
     # ------------------------------------------------------------------ epilogue
+    def defer_stores(self, od, ld, spread=0):
+        """(FA_GEN_DEFER) the finished item's LSE and O stores from V_LSEV / PKR with descriptors
+        s[od:od+3], s[ld:ld+3]; spread > 0: store i not before MFMA gap i * spread / count"""
+        out = []
+        for j in range(2):
+            out.append(Inst(f"buffer_store_dword v{V_LSEV[j]}, v{V_LSEOFF[j]}, s[{ld}:{ld + 3}], 0 offen", VSTORE,
+                            rd=vr(V_LSEV[j]) + vr(V_LSEOFF[j]) + sr(ld, 4)))
+            for dt in range(NP):
+                for u in (0, 2):
+                    w = PKR(j, dt, u)
+                    out.append(Inst(f"buffer_store_dwordx4 v[{w}:{w + 3}], v{V_OOFF[j]}, s[{od}:{od + 3}], 0 offen offset:{64 * dt + 16 * u}",
+                                    VSTORE, rd=vr(w, 4) + vr(V_OOFF[j]) + sr(od, 4)))
+        for i, op in enumerate(out):
+            op.key = 300 + i
+            if spread:
+                op.eg = i * spread // len(out)
+        return out
+
     def epilogue(self):
         if OPT_EPI2:
             return self.epilogue2()
@@ -1236,24 +1295,29 @@ class K:
                     Inst(f"s_and_b64 vcc, vcc, s[{S_TMP}:{S_TMP + 1}]", SALU, rd=sr(S_TMP, 2) + [("vcc", 0)], wr=[("vcc", 0)]),
                     Inst(f"v_cndmask_b32_e64 v{inv}, 1.0, v{inv}, vcc", VALU, rd=vr(inv) + [("vcc", 0)], wr=vr(inv)),
                     Inst(f"v_mov_b32_e32 v{t + 3}, 0x7f800000", VALU, wr=vr(t + 3)),
-                    Inst(f"v_cndmask_b32_e32 v{lse}, v{t + 3}, v{lse}, vcc", VALU, rd=vr(lse) + vr(t + 3) + [("vcc", 0)], wr=vr(lse)),
-                    Inst(f"buffer_store_dword v{lse}, v{V_LSEOFF[j]}, s[{S_LD}:{S_LD + 3}], 0 offen", VSTORE,
-                         rd=vr(lse) + vr(V_LSEOFF[j]) + sr(S_LD, 4))]
+                    Inst(f"v_cndmask_b32_e32 v{lse}, v{t + 3}, v{lse}, vcc", VALU, rd=vr(lse) + vr(t + 3) + [("vcc", 0)], wr=vr(lse))]
+            if OPT_DEFER:
+                ins.append(Inst(f"v_mov_b32_e32 v{V_LSEV[j]}, v{lse}", VALU, rd=vr(lse), wr=vr(V_LSEV[j])))
+            else:
+                ins.append(Inst(f"buffer_store_dword v{lse}, v{V_LSEOFF[j]}, s[{S_LD}:{S_LD + 3}], 0 offen", VSTORE,
+                                rd=vr(lse) + vr(V_LSEOFF[j]) + sr(S_LD, 4)))
             if OPT_EPISTAMP:
                 ins += self.stamp_point(6)
             for dt in range(NP):
                 for u in (0, 2):
-                    w = t + 4 + 4 * ((dt * 2 + u // 2) % 4)
+                    w = PKR(j, dt, u) if OPT_DEFER else t + 4 + 4 * ((dt * 2 + u // 2) % 4)
                     o = O_(j, dt) + 4 * u
                     x = t + 20
-                    ins += [Inst(f"v_accvgpr_read_b32 v{x + k}, a{o + k}", ACCR, rd=ar(o + k), wr=vr(x + k)) for k in range(8)]
-                    ins += [Inst(f"v_mul_f32_e32 v{x + k}, v{x + k}, v{inv}", VALU, rd=vr(x + k) + vr(inv), wr=vr(x + k)) for k in range(8)]
-                    ins += [self.cvt(w + 0, x + 0, x + 1), self.cvt(w + 1, x + 2, x + 3),
-                            self.cvt(w + 2, x + 4, x + 5), self.cvt(w + 3, x + 6, x + 7)]
-                    ins += [Inst(f"v_permlane32_swap_b32_e32 v{w}, v{w + 2}", PERM, rd=vr(w) + vr(w + 2), wr=vr(w) + vr(w + 2)),
-                            Inst(f"v_permlane32_swap_b32_e32 v{w + 1}, v{w + 3}", PERM, rd=vr(w + 1) + vr(w + 3), wr=vr(w + 1) + vr(w + 3))]
-                    ins.append(Inst(f"buffer_store_dwordx4 v[{w}:{w + 3}], v{V_OOFF[j]}, s[{S_OD}:{S_OD + 3}], 0 offen offset:{64 * dt + 16 * u}",
-                                    VSTORE, rd=vr(w, 4) + vr(V_OOFF[j]) + sr(S_OD, 4)))
+                    if OPT_EPI_ABL != "storeonly":
+                        ins += [Inst(f"v_accvgpr_read_b32 v{x + k}, a{o + k}", ACCR, rd=ar(o + k), wr=vr(x + k)) for k in range(8)]
+                        ins += [Inst(f"v_mul_f32_e32 v{x + k}, v{x + k}, v{inv}", VALU, rd=vr(x + k) + vr(inv), wr=vr(x + k)) for k in range(8)]
+                        ins += [self.cvt(w + 0, x + 0, x + 1), self.cvt(w + 1, x + 2, x + 3),
+                                self.cvt(w + 2, x + 4, x + 5), self.cvt(w + 3, x + 6, x + 7)]
+                        ins += [Inst(f"v_permlane32_swap_b32_e32 v{w}, v{w + 2}", PERM, rd=vr(w) + vr(w + 2), wr=vr(w) + vr(w + 2)),
+                                Inst(f"v_permlane32_swap_b32_e32 v{w + 1}, v{w + 3}", PERM, rd=vr(w + 1) + vr(w + 3), wr=vr(w + 1) + vr(w + 3))]
+                    if OPT_EPI_ABL != "nostore" and not OPT_DEFER:
+                        ins.append(Inst(f"buffer_store_dwordx4 v[{w}:{w + 3}], v{V_OOFF[j]}, s[{S_OD}:{S_OD + 3}], 0 offen offset:{64 * dt + 16 * u}",
+                                        VSTORE, rd=vr(w, 4) + vr(V_OOFF[j]) + sr(S_OD, 4)))
             if OPT_EPISTAMP and j == 0:
                 ins += self.stamp_point(9)
         return ins
@@ -1304,6 +1368,7 @@ class K:
     def build(self):
         self.switches = []
         l_end = self.lab("end")
+        self.l_tile0w = self.lab("tile0w")
         self.lab_end = l_end
         l_epi = self.lab("epi")
         L = {k: self.lab(k) for k in ("fast0", "fast1", "sel0", "sel1", "masked0", "masked1", "last0", "last1",
@@ -1320,6 +1385,9 @@ class K:
         code += [nop(0) for _ in range(OPT_SHIFT)]
         emit_block(self.entry())
         emit_block(self.item_start(L["cold"], L["coldw"], L["warm"], L["skip"], L["tile0"], l_epi, l_end), pre=tailpad)
+        if OPT_DEFER:
+            code.append(label(self.l_tile0w))
+            emit_block(self.tile0(L["last0"], L["fast0"], L["sel0"], stores=True), pre=tailpad)
         code.append(label(L["tile0"]))
         emit_block(self.tile0(L["last0"], L["fast0"], L["sel0"]), pre=tailpad)
         refits = []
