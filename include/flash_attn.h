@@ -423,7 +423,7 @@ void flash_attn_timing_read(int kernel_id, double * total_ms, long * count);
  * default 256), 3 / 4 assembly dK/dV / dQ kernels (FLASH_ATTN_MI355X_BWD_ASM / _DQ_ASM, default 1),
  * 5 persistent assembly forward, one workgroup per CU walking the item list
  * (FLASH_ATTN_MI355X_FWD_PERSIST, default 1; 0 = one workgroup per item), 6 the same for the
- * assembly dK/dV and dQ kernels (FLASH_ATTN_MI355X_BWD_PERSIST, default 1), 7 knob 2's threshold
+ * assembly dK/dV and dQ kernels, fixed-length launches (FLASH_ATTN_MI355X_BWD_PERSIST, default 1), 7 knob 2's threshold
  * for the persistent assembly forward and dQ (FLASH_ATTN_MI355X_ASM_XCD_GROUP_MIN_MIB, default 0:
  * heads grouped per XCD whenever the shape allows).  Each is read from its environment variable
  * once, at first use. */

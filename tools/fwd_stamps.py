@@ -37,6 +37,7 @@ def main():
     ap.add_argument("--warm-s", type=float, default=2.0)
     ap.add_argument("--samples", type=int, default=3)
     ap.add_argument("--epi", action="store_true", help="library built with FA_GEN_STAMP=3 (epilogue parts)")
+    ap.add_argument("--t0", action="store_true", help="library built with FA_GEN_STAMP=4 (item-start parts)")
     args = ap.parse_args()
     lib = load(args.lib)
     lib.flash_attn_debug_fwd_stamps.argtypes = [ctypes.c_void_p]
@@ -94,9 +95,12 @@ def main():
             row["steps_med"] = float(np.median(steps))
             items = np.maximum(a[:, 9], 1)
             names = (("epi_lse", "last_step", "epi_o_b", "epi_o_a") if args.epi else
+                     ("t0_vmwait", "last_step", "epilogue", "geometry") if args.t0 else
                      ("tile0", "last_step", "epilogue", "item_start"))
             for i, nm in zip((20, 21, 22, 23), names):
                 row[f"{nm}_per_item_med"] = float(np.median(a[:, i] / items))
+            if args.t0:
+                row["t0_barrier_per_item_med"] = float(np.median(a[:, 24] / items))
         rows.append(row)
         print(" ".join(f"{k}={v:.4g}" if isinstance(v, float) else f"{k}={v}" for k, v in row.items()), flush=True)
 

@@ -172,6 +172,9 @@ OPT_EPI_ABL = os.environ.get("FA_GEN_EPI_ABL", "")
 # after its s_waitcnt (vmcnt counts stores: stores queued ahead of the wait were waited for) and
 # spread one per gap (a store of 32 rows x 32 bytes holds the wave's issue for ~76 cycles)
 OPT_DEFER = os.environ.get("FA_GEN_DEFER") == "1"
+# O zeroed by v_accvgpr_write in the gaps of tile 0's MFMAs instead of ahead of them (an empty item,
+# which runs no tile 0, zeroes it on its own branch)
+OPT_T0ZERO = os.environ.get("FA_GEN_T0ZERO") == "1"
 V_LSEV = (191, 195)                   # LSE values of the finished item (deferred stores)
 V_SAVE = (228, 229, 230, 231, 238, 239)   # its O / LSE descriptor words 0..2 across the warm start
 S_ODD, S_LDD = 88, 36                 # ... restored here for tile 0 (geometry temps, free by then)
@@ -183,13 +186,16 @@ def PKR(j, dt, u):
     i = 32 * j + 4 * (2 * dt + u // 2)
     return 64 + i if i < 32 else 112 + (i - 32)
 V_ZERO = 228      # 228..231: zeros (MFMA operands of the O zeroing)
-OPT_STAMP = os.environ.get("FA_GEN_STAMP") in ("1", "2", "3")
+OPT_STAMP = os.environ.get("FA_GEN_STAMP") in ("1", "2", "3", "4")
 # FA_GEN_STAMP=2 also sums, per wave, the cycles of each step's compute, its vmcnt/lgkmcnt wait and
 # its barrier wait (s_memtime around the step-end wait and barrier; perturbs the schedule a little)
-OPT_STEPSTAMP = os.environ.get("FA_GEN_STAMP") in ("2", "3")
+OPT_STEPSTAMP = os.environ.get("FA_GEN_STAMP") in ("2", "3", "4")
 # FA_GEN_STAMP=3: the tile-0 / item-start accumulators time the epilogue's parts instead (LSE of both
 # q-blocks -> tile 0's slot, O of q-block a -> item start's slot, O of q-block b -> the epilogue's)
 OPT_EPISTAMP = os.environ.get("FA_GEN_STAMP") == "3"
+# FA_GEN_STAMP=4: the item start split -- geometry (epilogue end -> tile 0's wait) in the item-start
+# slot, tile 0's vmcnt wait in the tile-0 slot, its barrier wait in V_SSUM + 5 (record offset 96)
+OPT_T0STAMP = os.environ.get("FA_GEN_STAMP") == "4"
 V_SSUM = 240      # 240..244: compute, wait, barrier sums, step count, last stamp;
                   # 246..249: item phases: tile 0, last step, epilogue, item start (geometry .. tile 0's barrier)
 # latency-aware gap scheduling (isa.schedule lat=): "valu,trans,lds,mfma" result latencies in cycles
@@ -774,7 +780,7 @@ class K:
             ins += [I(f"v_mov_b32_e32 v{V_STAMP + i}, s{T0 + i}", VALU, rd=sr(T0 + i), wr=vr(V_STAMP + i)) for i in range(4)]
             ins += [I(f"v_mov_b32_e32 v{V_STAMP + 4}, 0", VALU, wr=vr(V_STAMP + 4)),
                     I(f"v_mov_b32_e32 v{V_STAMP + 5}, 0", VALU, wr=vr(V_STAMP + 5))]
-            ins += [I(f"v_mov_b32_e32 v{V_SSUM + i}, 0", VALU) for i in (0, 1, 2, 3, 6, 7, 8, 9)]
+            ins += [I(f"v_mov_b32_e32 v{V_SSUM + i}, 0", VALU) for i in (0, 1, 2, 3, 5, 6, 7, 8, 9)]
             ins += [I(f"v_mov_b32_e32 v{V_SSUM + 4}, s{T0}", VALU)]
         # rng_state (block 0, wave 0): {seed, offset}; lanes >= 1 fall outside the 16-byte record
         l_norng = self.lab("norng")
@@ -1091,15 +1097,17 @@ class K:
         ins += [I(f"s_mov_b32 s{S_WARM}, 0", SALU),
                 I(f"s_mov_b32 s{S_KOFF}, 0", SALU),
                 I(f"s_lshl_b32 s{S_DOFF}, s{S_WAVE}, 10", SALU)]
-        ins += self.item_zero()
+        ins += self.item_zero(o=False)
         # no tiles at all: epilogue (O = 0, LSE = +inf)
         ins += [I(f"s_cmp_eq_u32 s{S_NBLK}, 0", SALU, rd=sr(S_NBLK), wr=[("scc", 0)]),
                 I("s_waitcnt vmcnt(0)", WAIT),
-                I(f"s_cbranch_scc1 {l_epi}", BRANCH)]
+                I(f"s_cbranch_scc1 {self.l_empty if OPT_T0ZERO else l_epi}", BRANCH)]
         for tile in range(4):
             ins += self.dma_tile_ops(f"c{tile}")
         ins += [I(f"s_branch {l_tile0}", BRANCH)]
         ins += [label(l_skip), I(f"s_add_u32 s{S_ROUND}, s{S_ROUND}, 1", SALU), I(f"s_branch {l_cold}", BRANCH)]
+        if OPT_T0ZERO:   # an item with no tiles: O = 0 for its epilogue (no tile 0 zeroes it)
+            ins += [label(self.l_empty)] + self.o_zero_ops() + [I(f"s_branch {l_epi}", BRANCH)]
         # ---- warm
         ins += [label(l_warm)]
         ins += self.item_pos(S_SWT, 0)
@@ -1121,7 +1129,7 @@ class K:
         ins += self.item_geom("next", None)
         ins += [I(f"s_mov_b32 s{S_WARM}, 0", SALU),
                 I(f"s_sub_u32 s{S_KOFF}, s{S_VOFF}, {VBASE}", SALU)]
-        ins += self.item_zero()
+        ins += self.item_zero(o=False)
         ins += restore
         ins += self.dma_tile_ops("w3")
         if OPT_DEFER:
@@ -1129,11 +1137,16 @@ class K:
                     label(l_skip_w)] + restore + [nop(5)] + self.defer_stores(S_ODD, S_LDD) + [I(f"s_branch {l_skip}", BRANCH)]
         return ins
 
-    def item_zero(self):
+    def o_zero_ops(self, key=0):
+        return [Inst(f"v_accvgpr_write_b32 a{i}, 0", ACCW, wr=ar(i), key=key + i) for i in range(2 * NP * 16)]
+
+    def item_zero(self, o=True):
         I = Inst
         ins = [I(f"s_mov_b32 s{S_N}, 0", SALU, wr=sr(S_N)),
                I(f"s_mov_b32 s{S_N0}, 0", SALU, wr=sr(S_N0))]
-        if OPT_MFZERO:   # O = 0 x 0 + 0: one MFMA per 16 accumulators instead of 16 v_accvgpr_write
+        if OPT_T0ZERO and not o:
+            pass
+        elif OPT_MFZERO:   # O = 0 x 0 + 0: one MFMA per 16 accumulators instead of 16 v_accvgpr_write
             ins += [I(f"v_mfma_f32_32x32x16_{self.ty} {rtxt('a', 16 * i, 16)}, {rtxt('v', V_ZERO, 4)}, {rtxt('v', V_ZERO, 4)}, 0",
                       MFMA, rd=vr(V_ZERO, 4), wr=ar(16 * i, 16)) for i in range(2 * NP)]
         else:
@@ -1148,8 +1161,12 @@ class K:
         """Q + tiles 0, 1, 2 landed (tile 3 in flight); tile 0: S(0, a), S(0, b) -> masked, explicit
         row max, P(0, a); then into the step loop"""
         I = Inst
-        ins = [I(f"s_waitcnt vmcnt({2 * NP})", WAIT), I("s_barrier", BARRIER)]
-        ins += [] if OPT_EPISTAMP else self.stamp_point(9)
+        if OPT_T0STAMP:
+            ins = (self.stamp_point(9) + [I(f"s_waitcnt vmcnt({2 * NP})", WAIT)] + self.stamp_point(6) +
+                   [I("s_barrier", BARRIER)] + self.stamp_point(5))
+        else:
+            ins = [I(f"s_waitcnt vmcnt({2 * NP})", WAIT), I("s_barrier", BARRIER)]
+            ins += [] if OPT_EPISTAMP else self.stamp_point(9)
         ins += self.dump("pro_lds")
         ins += [I(f"v_add_u32_e32 v{V_KB0}, s{S_KOFF}, v{V_RB0}", VALU, rd=sr(S_KOFF) + vr(V_RB0), wr=vr(V_KB0)),
                 I(f"v_add_u32_e32 v{V_KB1}, s{S_KOFF}, v{V_RB1}", VALU, rd=sr(S_KOFF) + vr(V_RB1), wr=vr(V_KB1))]
@@ -1165,6 +1182,8 @@ class K:
                                     deadline=2 * f - 1 if f >= 3 else 0))
         if stores:
             reads += self.defer_stores(S_ODD, S_LDD, spread=NX)
+        if OPT_T0ZERO:
+            reads += self.o_zero_ops(key=100)
         if OPT_T0OV:
             assert not stores
             ins += self.tile0_overlapped()
@@ -1194,7 +1213,7 @@ class K:
             ins += sm
             ins += [Inst(f"v_mov_b32_e32 v{V_L[0]}, v{V_PS[0]}", VALU, rd=vr(V_PS[0]), wr=vr(V_L[0]))]
         ins += self.dump("pro_end")
-        ins += [] if OPT_EPISTAMP else self.stamp_point(6)
+        ins += [] if (OPT_EPISTAMP or OPT_T0STAMP) else self.stamp_point(6)
         # V reads tile 0 (slot S_KOFF); S_KOFF -> tile 1 (the LAST step's refit takes S_KOFF - TILE)
         ins += [I(f"s_add_u32 s{S_VOFF}, s{S_KOFF}, {VBASE}", SALU),
                 I(f"s_add_u32 s{S_KOFF}, s{S_KOFF}, {TILE}", SALU),
@@ -1369,6 +1388,7 @@ class K:
         self.switches = []
         l_end = self.lab("end")
         self.l_tile0w = self.lab("tile0w")
+        self.l_empty = self.lab("empty")
         self.lab_end = l_end
         l_epi = self.lab("epi")
         L = {k: self.lab(k) for k in ("fast0", "fast1", "sel0", "sel1", "masked0", "masked1", "last0", "last1",
@@ -1475,6 +1495,7 @@ class K:
                    I("buffer_store_dwordx4 v[4:7], v8, s[52:55], s46 offen offset:48", VSTORE),
                    I(f"buffer_store_dwordx4 v[{V_SSUM}:{V_SSUM + 3}], v8, s[52:55], s46 offen offset:64", VSTORE),
                    I(f"buffer_store_dwordx4 v[{V_SSUM + 6}:{V_SSUM + 9}], v8, s[52:55], s46 offen offset:80", VSTORE),
+                   I(f"buffer_store_dword v{V_SSUM + 5}, v8, s[52:55], s46 offen offset:96", VSTORE),
                    I("s_waitcnt vmcnt(0)", WAIT)]
             code.extend(st)
         code.append(I("s_endpgm", SOPP))

@@ -147,8 +147,12 @@ void launch_bwd_dkdv_asm(const BwdParams& p, bool is_bf16, hipStream_t stream) {
     cus = m.cus;
   }
   // persistent grid (knob 6, default on): one workgroup per CU (151 KiB of LDS allows one) walking the
-  // heaviest-first item list in snake order -- no workgroup dispatch between items
-  const long long grid = (knob(kKnobBwdPersist) != 0 && cus > 0 && nwg > cus) ? cus : nwg;
+  // heaviest-first item list in snake order -- no workgroup dispatch between items.  Fixed length
+  // only: varlen items range from empty to a full sweep, and the static snake assignment then
+  // leaves CUs idle where the dispatcher's dynamic one does not (C4: dK/dV 3.48 vs 3.16 ms, dQ
+  // 2.25 vs 2.07, profiles/r04/ab_bwd_persist_c4_r04l.txt)
+  const bool persist = knob(kKnobBwdPersist) != 0 && s.cu_seqlens_q == nullptr && s.cu_seqlens_k == nullptr;
+  const long long grid = (persist && cus > 0 && nwg > cus) ? cus : nwg;
   BwdAsmArgs a;
   std::memset(&a, 0, sizeof(a));
   a.q = p.q; a.k = p.k; a.v = p.v; a.dout = p.dout; a.dk = p.dk; a.dv = p.dv;
@@ -205,8 +209,10 @@ void launch_bwd_dq_asm(const BwdParams& p, bool is_bf16, hipStream_t stream) {
     fn = m.fn_dq[(is_bf16 ? 0 : 2) + (s.causal ? 0 : 1)];
     cus = m.cus;
   }
-  // persistent grid (knob 6): one workgroup per CU walking the item list in snake order
-  const long long grid = (knob(kKnobBwdPersist) != 0 && cus > 0 && nwg > cus) ? cus : nwg;
+  // persistent grid (knob 6): one workgroup per CU walking the item list in snake order (fixed
+  // length only, as dK/dV)
+  const bool persist = knob(kKnobBwdPersist) != 0 && s.cu_seqlens_q == nullptr && s.cu_seqlens_k == nullptr;
+  const long long grid = (persist && cus > 0 && nwg > cus) ? cus : nwg;
   DqAsmArgs a;
   std::memset(&a, 0, sizeof(a));
   a.q = p.q; a.k = p.k; a.v = p.v; a.dout = p.dout; a.dq = p.dq;
