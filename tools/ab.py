@@ -22,7 +22,7 @@ sys.path.insert(0, ROOT)
 import torch  # noqa: E402
 
 import flash_attn_2_cuda as m  # noqa: E402
-from bench import KERNELS, WORKLOADS, flops_fwd  # noqa: E402
+from bench import KERNELS, WORKLOADS, c4_seqlens, flops_fwd, varlen_flops_fwd  # noqa: E402
 
 
 def load(path):
@@ -53,7 +53,7 @@ def read_times(lib):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("libs", nargs="+")
-    ap.add_argument("--workload", default="c3", choices=[w for w in sorted(WORKLOADS) if WORKLOADS[w][0]])
+    ap.add_argument("--workload", default="c3", choices=sorted(WORKLOADS))
     ap.add_argument("--rounds", type=int, default=5)
     ap.add_argument("--iters", type=int, default=10)
     ap.add_argument("--bwd", action="store_true")
@@ -64,11 +64,31 @@ def main():
     b, s, h, hk, d, dt, causal, _kind = WORKLOADS[args.workload]
     dtype = torch.bfloat16 if dt == "bf16" else torch.float16
     g = torch.Generator(device="cuda").manual_seed(1234)
-    q = torch.randn(b, s, h, d, device="cuda", dtype=dtype, generator=g)
-    k = torch.randn(b, s, hk, d, device="cuda", dtype=dtype, generator=g)
-    v = torch.randn(b, s, hk, d, device="cuda", dtype=dtype, generator=g)
-    dout = torch.randn(b, s, h, d, device="cuda", dtype=dtype, generator=g)
+    varlen = b is None       # c4: varlen, the packed qkv's views, SURVEY 8(d) sequence lengths
+    if varlen:
+        lens = c4_seqlens(total=s)
+        cu = torch.tensor([0] + torch.tensor(lens).cumsum(0).tolist(), dtype=torch.int32, device="cuda")
+        qkv = torch.randn(s, 3, h, d, device="cuda", dtype=dtype, generator=g)
+        q, k, v = qkv.unbind(1)
+        dout = torch.randn(s, h, d, device="cuda", dtype=dtype, generator=g)
+        ms_ = max(lens)
+    else:
+        q = torch.randn(b, s, h, d, device="cuda", dtype=dtype, generator=g)
+        k = torch.randn(b, s, hk, d, device="cuda", dtype=dtype, generator=g)
+        v = torch.randn(b, s, hk, d, device="cuda", dtype=dtype, generator=g)
+        dout = torch.randn(b, s, h, d, device="cuda", dtype=dtype, generator=g)
     scale = d ** -0.5
+
+    def fwd(gen):
+        if varlen:
+            return m.varlen_fwd(q, k, v, None, cu, cu, ms_, ms_, pd, scale, False, causal, False, gen)
+        return m.fwd(q, k, v, None, pd, scale, causal, False, gen)
+
+    def bwd(res):
+        if varlen:
+            return m.varlen_bwd(dout, q, k, v, res[0], res[5], None, None, None, cu, cu, ms_, ms_, pd, scale, False,
+                                causal, None, res[7])
+        return m.bwd(dout, q, k, v, res[0], res[5], None, None, None, pd, scale, causal, None, res[7])
     libs = [load(p) for p in args.libs]
     names = [os.path.basename(p) for p in args.libs]
     times = {n: {} for n in names}
@@ -77,11 +97,11 @@ def main():
         for lib, name in zip(libs, names):
             m._lib = lib
             gen = torch.Generator(device="cuda").manual_seed(7) if pd > 0 else None
-            res = m.fwd(q, k, v, None, pd, scale, causal, False, gen)
+            res = fwd(gen)
             out, lse = res[0], res[5]
             grads = None
             if args.bwd:
-                grads = m.bwd(dout, q, k, v, out, lse, None, None, None, pd, scale, causal, None, res[7])[:3]
+                grads = bwd(res)[:3]
             torch.cuda.synchronize()
             if rnd == 0:
                 cur = [out, lse] + (list(grads) if grads else [])
@@ -93,15 +113,15 @@ def main():
                           + ", ".join(f"{x:.3e}" for x in diffs), flush=True)
             lib.flash_attn_timing_enable(1)
             for _ in range(args.iters):
-                r2 = m.fwd(q, k, v, None, pd, scale, causal, False, None)
+                r2 = fwd(None)
                 if args.bwd:
-                    m.bwd(dout, q, k, v, r2[0], r2[5], None, None, None, pd, scale, causal, None, r2[7])
+                    bwd(r2)
             torch.cuda.synchronize()
             t = read_times(lib)
             lib.flash_attn_timing_enable(0)
             for kname, ms in t.items():
                 times[name].setdefault(kname, []).append(ms)
-    f = flops_fwd(b, s, h, d, causal)
+    f = varlen_flops_fwd(lens, h, d, causal) if varlen else flops_fwd(b, s, h, d, causal)
     alg = {"fwd_kernel": f, "bwd_dkdv_kernel": 2 * f, "bwd_dq_kernel": 1.5 * f, "bwd_pre_kernel": 0}
     for name in names:
         parts = []

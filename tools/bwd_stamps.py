@@ -22,27 +22,59 @@ import flash_attn_2_cuda as m  # noqa: E402
 from ab import load  # noqa: E402
 
 
-def main(path, b=4, s=8192, h=16):
+def main(path, b=4, s=8192, h=16, c4=False):
+    """c4: the C4 varlen workload (bench.c4_seqlens, 32 heads; one workgroup per item)"""
     lib = load(path)
     lib.flash_attn_debug_bwd_stamps.argtypes = [ctypes.c_void_p]
     m._lib = lib
-    nwg = b * h * (s // 128)
-    buf = torch.zeros(nwg * 16, dtype=torch.int32, device="cuda")
-    q, k, v, do = (torch.randn(b, s, h, 128, device="cuda", dtype=torch.bfloat16) for _ in range(4))
     scale = 128 ** -0.5
-    res = m.fwd(q, k, v, None, 0.0, scale, True, False, None)
+    if c4:
+        from bench import c4_seqlens
+        lens = c4_seqlens()
+        h, b, s = 32, len(lens), max(lens)
+        cu_t = torch.tensor([0] + torch.tensor(lens).cumsum(0).tolist(), dtype=torch.int32, device="cuda")
+        q, k, v, do = (torch.randn(sum(lens), h, 128, device="cuda", dtype=torch.bfloat16) for _ in range(4))
+        res = m.varlen_fwd(q, k, v, None, cu_t, cu_t, s, s, 0.0, scale, False, True, False, None)
+    else:
+        q, k, v, do = (torch.randn(b, s, h, 128, device="cuda", dtype=torch.bfloat16) for _ in range(4))
+        res = m.fwd(q, k, v, None, 0.0, scale, True, False, None)
+    nwg = b * h * ((s + 127) // 128)
+    steps = "--steps" in sys.argv[2:]
+    buf = torch.zeros(nwg * 16 * (4 if steps else 1), dtype=torch.int32, device="cuda")
     for it in range(3):
         lib.flash_attn_debug_bwd_stamps(ctypes.c_void_p(buf.data_ptr() if it == 2 else 0))
-        m.bwd(do, q, k, v, res[0], res[5], None, None, None, 0.0, scale, True, None, res[7])
+        if c4:
+            m.varlen_bwd(do, q, k, v, res[0], res[5], None, None, None, cu_t, cu_t, s, s, 0.0, scale, False, True,
+                         None, res[7])
+        else:
+            m.bwd(do, q, k, v, res[0], res[5], None, None, None, 0.0, scale, True, None, res[7])
         torch.cuda.synchronize()
     lib.flash_attn_debug_bwd_stamps(ctypes.c_void_p(0))
-    a = buf.cpu().numpy().view(np.uint32).reshape(nwg, 16)
+    if steps:   # FA_GBW_STAMP=2: per wave {compute, wait, barrier, steps, -, prologue, epilogue, items}
+        a = buf.cpu().numpy().view(np.uint32).reshape(nwg * 4, 16)[:, :8].astype(np.int64)
+        a = a[a[:, 7] > 0]
+        st = np.maximum(a[:, 3], 1)
+        it = np.maximum(a[:, 7], 1)
+        tot = a[:, 0] + a[:, 1] + a[:, 2] + a[:, 5] + a[:, 6]
+        print(f"waves {len(a)}, items per wave med {np.median(a[:, 7]):.0f}, steps per wave med {np.median(a[:, 3]):.0f}")
+        for i, nm in ((0, "compute"), (1, "vmwait"), (2, "barrier")):
+            print(f"  {nm}: per step med {np.median(a[:, i] / st):.0f} cycles, share {np.median(a[:, i] / tot):.3f}")
+        for i, nm in ((5, "prologue"), (6, "tail+epilogue")):
+            print(f"  {nm}: per item med {np.median(a[:, i] / it):.0f} cycles, share {np.median(a[:, i] / tot):.3f}")
+        print(f"  total per wave med {np.median(tot):.0f} cycles; ideal MFMA cycles per step 2048 (64 MFMAs)")
+        return
     start = a[:, 0].astype(np.int64) | (a[:, 1].astype(np.int64) << 32)
     end = a[:, 5].astype(np.int64) | (a[:, 6].astype(np.int64) << 32)
     hwid, xcc = a[:, 2], a[:, 3]
     cu = (xcc.astype(np.int64) << 16) | ((hwid >> 8) & 0xFF)
+    ran = end > 0                       # (a persistent grid leaves the records of unrun items at 0)
+    start, end, hwid, xcc, cu, a = start[ran], end[ran], hwid[ran], xcc[ran], cu[ran], a[ran]
+    nwg = int(ran.sum())
+    # s_memtime runs per XCD: spans and heads / tails are taken within each XCD
+    t0x = {x: start[xcc == x].min() for x in np.unique(xcc)}
+    t1x = {x: end[xcc == x].max() for x in np.unique(xcc)}
     t0 = start.min()
-    span = end.max() - t0
+    span = float(np.median([t1x[x] - t0x[x] for x in t0x]))
     print(f"{nwg} workgroups, span {span} ticks (s_memtime), mean WG duration {np.mean(end - start):.0f}")
     gaps, busy, tails, heads = [], [], [], []
     for c in np.unique(cu):
@@ -50,9 +82,10 @@ def main(path, b=4, s=8192, h=16):
         o = idx[np.argsort(start[idx])]
         st, en = start[o], end[o]
         gaps += list(st[1:] - en[:-1])
-        busy.append((en - st).sum() / span)
-        heads.append(st[0] - t0)
-        tails.append(end.max() - en[-1])
+        x = xcc[o[0]]
+        busy.append((en - st).sum() / (t1x[x] - t0x[x]))
+        heads.append(st[0] - t0x[x])
+        tails.append(t1x[x] - en[-1])
     gaps = np.array(gaps)
     print(f"CUs {len(busy)}; WGs per CU {nwg / len(busy):.1f}; busy share mean {np.mean(busy):.3f} min {np.min(busy):.3f}")
     print(f"gap between consecutive WGs on a CU: median {np.median(gaps):.0f} mean {gaps.mean():.0f} p90 {np.percentile(gaps, 90):.0f}"
@@ -72,4 +105,4 @@ def main(path, b=4, s=8192, h=16):
 
 
 if __name__ == "__main__":
-    main(sys.argv[1])
+    main(sys.argv[1], c4="--c4" in sys.argv[2:])

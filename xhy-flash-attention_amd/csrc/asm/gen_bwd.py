@@ -140,6 +140,12 @@ OPT_LEAD = int(os.environ.get("FA_GBW_LEAD", "2"))    # ... and at least LEAD MF
 # dev timeline: every workgroup stores {start, end} s_memtime, HW_ID, XCC_ID, id at the `stamps`
 # kernarg address + 32 id (tools/bwd_stamps.py)
 OPT_STAMP = os.environ.get("FA_GBW_STAMP") == "1"
+# FA_GBW_STAMP=2: per wave, over all its items, the cycles of the steps' compute, their end-of-step
+# vmcnt wait and barrier, the prologues (item start .. phase -1's barrier) and the tails + epilogues;
+# record (workgroup * 4 + wave) * 64 bytes at the `stamps` kernarg (tools/bwd_stamps.py --steps)
+OPT_STEPSTAMP = os.environ.get("FA_GBW_STAMP") == "2"
+V_SS = 186             # 186..193: compute, wait, barrier, steps, last stamp, prologue, epilogue, items
+                       # (194, 195: temporaries)
 V_ROUND = 184          # round r of the persistent item loop (uniform)
 S_ITEM = 28            # the item index, until the sweep geometry takes the register (S_QF)
 V_STAMP = 164          # 164..177: start lo / hi, HW_ID, XCC_ID, wg, end lo / hi, wave, -, -, loop start lo / hi,
@@ -391,10 +397,29 @@ class K:
         self.ool.extend(blk)
         return check
 
+    def stamp(self, acc, count=None):
+        """(FA_GBW_STAMP=2) v[acc] += now - last; last = now (acc None: only last = now); v[count] += 1"""
+        if not OPT_STEPSTAMP:
+            return []
+        t = S_TMP + 1
+        ins = [Inst(f"s_memtime s[{t}:{t + 1}]", SMEM), Inst("s_waitcnt lgkmcnt(0)", WAIT),
+               Inst(f"v_mov_b32_e32 v{V_SS + 8}, s{t}", VALU)]
+        if acc is not None:
+            ins += [Inst(f"v_sub_u32_e32 v{V_SS + 9}, v{V_SS + 8}, v{V_SS + 4}", VALU),
+                    Inst(f"v_add_u32_e32 v{acc}, v{acc}, v{V_SS + 9}", VALU)]
+        ins += [Inst(f"v_mov_b32_e32 v{V_SS + 4}, v{V_SS + 8}", VALU)]
+        if count is not None:
+            ins += [Inst(f"v_add_u32_e32 v{count}, 1, v{count}", VALU)]
+        return ins
+
     def step_end(self):
         """after a step: head wraps of the DMA cursors, wait for the subtiles the next step reads, barrier"""
         ins = self.wrap_check("d") + self.wrap_check("l")
-        ins += [Inst(f"s_waitcnt vmcnt({VMCNT_STEP}) lgkmcnt(0)", WAIT), Inst("s_barrier", BARRIER)]
+        ins += self.stamp(V_SS + 0, count=V_SS + 3)
+        ins += [Inst(f"s_waitcnt vmcnt({VMCNT_STEP}) lgkmcnt(0)", WAIT)]
+        ins += self.stamp(V_SS + 1)
+        ins += [Inst("s_barrier", BARRIER)]
+        ins += self.stamp(V_SS + 2)
         return ins
 
     def tail(self):
@@ -685,7 +710,7 @@ class K:
             return I(f"{op} s{d}, s{a}, s{b}", SALU, rd=sr(a) + sr(b) + list(extra_rd), wr=sr(d) + [("scc", 0)])
 
         # the last steps' DMA (zero records past the sweep) must have landed before the workgroup's LDS
-        # is released
+        # is released (moving this wait after the stores measured ±0 at C3 / C5, +0.3..1.8 % at C4)
         ins += [I("s_waitcnt vmcnt(0)", WAIT)]
         ins += [rf(KW0v, T4), rf(HDv, T5), rf(SKv, T6)]
         for dst, ptr, off, rowv, headv, acc, scale in ((S_QD, PDV, DVO, RDV, HDV, DV, False),
@@ -747,7 +772,8 @@ class K:
         emit([Inst("v_lshrrev_b32_e32 v1, 6, v0", VALU, rd=vr(0), wr=vr(1)),
               Inst(f"v_readfirstlane_b32 s{S_WAVE}, v1", RFL, rd=vr(1), wr=sr(S_WAVE)),
               Inst(f"v_and_b32_e32 v{V_LANE}, 63, v0", VALU, rd=vr(0), wr=vr(V_LANE)),
-              Inst(f"v_mov_b32_e32 v{V_ROUND}, 0", VALU, wr=vr(V_ROUND))])
+              Inst(f"v_mov_b32_e32 v{V_ROUND}, 0", VALU, wr=vr(V_ROUND))] +
+             ([Inst(f"v_mov_b32_e32 v{V_SS + i}, 0", VALU) for i in range(8)] + self.stamp(None) if OPT_STEPSTAMP else []))
         # persistent item loop (fa_bwd_asm.cpp, knob 6): workgroup w runs items r G + (r odd ? rev(w) :
         # w); G = n_items runs one item per workgroup.  The barrier keeps every wave's LDS reads of
         # the previous item ahead of the DMA of this one.
@@ -800,6 +826,7 @@ class K:
         sch = schedule([x[0] for x in mf], ph + fill)
         # step 0 reads Q / dO <= 3 and LSE / D <= 3: the same wait as at every step's end
         sch += [Inst(f"s_waitcnt vmcnt({VMCNT_STEP}) lgkmcnt(0)", WAIT), Inst("s_barrier", BARRIER)]
+        sch += self.stamp(V_SS + 5)
         emit(sch, pre=[nop(15)])
         L = {}
         variants = [(f, l, m) for f in (True, False) for l in (True, False) for m in ((True, False) if self.causal else (False,))
@@ -835,10 +862,21 @@ class K:
             stamp_epi = [Inst(f"s_memtime s[{S_TMP + 1}:{S_TMP + 2}]", SMEM), Inst("s_waitcnt lgkmcnt(0)", WAIT),
                          Inst(f"v_mov_b32_e32 v{V_STAMP + 12}, s{S_TMP + 1}", VALU),
                          Inst(f"v_mov_b32_e32 v{V_STAMP + 13}, s{S_TMP + 2}", VALU)]
-        emit([nop(15)] + stamp_epi + self.epilogue(), pre=pad)
+        emit([nop(15)] + stamp_epi + self.epilogue() + self.stamp(V_SS + 6, count=V_SS + 7), pre=pad)
         code.append(label(self.lab_next))
         code += [Inst(f"v_add_u32_e32 v{V_ROUND}, 1, v{V_ROUND}", VALU), Inst(f"s_branch {l_item}", BRANCH)]
         code.append(label(self.lab_end))
+        if OPT_STEPSTAMP:
+            I = Inst
+            code.extend([I("s_waitcnt vmcnt(0)", WAIT), I("s_load_dwordx2 s[52:53], s[0:1], 0xd8", SMEM),
+                         I("s_waitcnt lgkmcnt(0)", WAIT),
+                         I("s_cmp_eq_u64 s[52:53], 0", SALU), I("s_cselect_b32 s54, 0, 0x7fffffff", SALU),
+                         I("s_mov_b32 s55, 0x20000", SALU), I("s_and_b32 s53, s53, 0xffff", SALU),
+                         I("s_lshl_b32 s50, s2, 2", SALU), I(f"s_add_u32 s50, s50, s{S_WAVE}", SALU),
+                         I("s_lshl_b32 s50, s50, 6", SALU), I(f"v_mov_b32_e32 v{V_SS + 8}, 0", VALU), nop(4),
+                         I(f"buffer_store_dwordx4 v[{V_SS}:{V_SS + 3}], v{V_SS + 8}, s[52:55], s50 offen", VSTORE),
+                         I(f"buffer_store_dwordx4 v[{V_SS + 4}:{V_SS + 7}], v{V_SS + 8}, s[52:55], s50 offen offset:16", VSTORE),
+                         I("s_waitcnt vmcnt(0)", WAIT)])
         if OPT_STAMP:
             I = Inst
             st = [I("s_waitcnt vmcnt(0)", WAIT),
