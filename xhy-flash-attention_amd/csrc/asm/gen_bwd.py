@@ -144,6 +144,10 @@ OPT_STAMP = os.environ.get("FA_GBW_STAMP") == "1"
 # vmcnt wait and barrier, the prologues (item start .. phase -1's barrier) and the tails + epilogues;
 # record (workgroup * 4 + wave) * 64 bytes at the `stamps` kernarg (tools/bwd_stamps.py --steps)
 OPT_STEPSTAMP = os.environ.get("FA_GBW_STAMP") == "2"
+# dV^T / dK^T zeroed after the first subtiles' DMAs are issued (under their latency) instead of ahead
+OPT_ZLATE = os.environ.get("FA_GBW_ZEARLY") != "1"
+# ablations (wrong results; which resource bounds the steady state): novalu / nofrag / nodma
+OPT_ABL = os.environ.get("FA_GBW_ABL", "")
 V_SS = 186             # 186..193: compute, wait, barrier, steps, last stamp, prologue, epilogue, items
                        # (194, 195: temporaries)
 V_ROUND = 184          # round r of the persistent item loop (uniform)
@@ -326,11 +330,14 @@ class K:
                 continue
             fill += self.frag_reads(m, t, i, key=-100 + m, earliest=max(m - OPT_WIN, -1) if m >= OPT_WIN else None,
                                     deadline=max(m - OPT_LEAD, 0))
+        if OPT_ABL == "nofrag":
+            fill = []
         if valu:
-            fill += self.valu_ops(par, masked, q0_add)
+            fill += [] if OPT_ABL == "novalu" else self.valu_ops(par, masked, q0_add)
             fill += self.init_reads(par)
         if dma:
-            fill += self.dma_subtile(True, key=-40, eg=2)
+            d = self.dma_subtile(True, key=-40, eg=2)
+            fill += [x for x in d if x.kind != DMA] if OPT_ABL == "nodma" else d
         # slots and bases of the next phase: rows of p+2, transposed of p, chain starts of p+3
         nxt = []
         nxt += self.slot_advance(S_SROW, key=400) + self.slot_advance(S_STR, key=400) + self.lslot_advance(S_LRD, key=400)
@@ -667,8 +674,13 @@ class K:
                 I(f"s_mov_b32 s{S_NLAST}, s{T2}", SALU, rd=sr(T2), wr=sr(S_NLAST)),
                 I(f"s_mov_b32 s{S_N}, 0", SALU, wr=sr(S_N))]
         # zero dV^T, dK^T
-        for i in range(128):
-            ins.append(I(f"v_accvgpr_write_b32 a{i}, 0", ACCW, wr=ar(i)))
+        zero = [I(f"v_accvgpr_write_b32 a{i}, 0", ACCW, wr=ar(i)) for i in range(128)]
+        if OPT_ZLATE:   # (build() zeroes after the first DMAs; an empty item zeroes out of line)
+            l_empty = self.lab("empty")
+            self.ool.extend([label(l_empty), nop(15)] + zero + [I(f"s_branch {l_epi}", BRANCH)])
+            l_epi = l_empty
+        else:
+            ins += zero
         # nothing to sweep: epilogue (zeros)
         ins += [I(f"s_cmp_lt_i32 s{S_NLAST}, 0", SALU, rd=sr(S_NLAST), wr=[("scc", 0)]),
                 I(f"s_cbranch_scc1 {l_epi}", BRANCH)]
@@ -678,9 +690,11 @@ class K:
         """LSE / D of subtiles 0, 1, then three virtual steps (Q / dO of 0..5, LSE / D of 2..7), with
         the cursors' head wraps, in the steady state's issue order"""
         ins = self.dma_l_only() + self.dma_l_only() + self.wrap_check("l")
-        for _ in range(3):
+        for vs in range(3):
             ins += self.dma_subtile(True) + self.dma_subtile(True)
             ins += self.wrap_check("d") + self.wrap_check("l")
+            if vs == 0 and OPT_ZLATE:
+                ins += [Inst(f"v_accvgpr_write_b32 a{i}, 0", ACCW, wr=ar(i)) for i in range(128)]
         return ins
 
     def dma_l_only(self):
