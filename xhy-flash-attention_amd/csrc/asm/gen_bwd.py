@@ -578,6 +578,12 @@ class K:
                 I(f"v_lshlrev_b32_e32 v{x + 3}, 4, v{x + 3}", VALU, rd=vr(x + 3), wr=vr(x + 3)),
                 I(f"s_lshl_b32 s{T0}, s{S_WAVE}, 6", SALU, rd=sr(S_WAVE), wr=sr(T0)),
                 I(f"v_add_u32_e32 v{x + 3}, s{T0}, v{x + 3}", VALU, rd=sr(T0) + vr(x + 3), wr=vr(x + 3))]
+        if OPT_ABL == "dmarows":   # timing ablation (wrong data): each DMA covers 4 whole rows
+            ins += [I(f"v_lshrrev_b32_e32 v{x + 2}, 4, v{V_LANE}", VALU, rd=vr(V_LANE), wr=vr(x + 2)),
+                    I(f"s_lshl_b32 s{T0}, s{S_WAVE}, 2", SALU, rd=sr(S_WAVE), wr=sr(T0)),
+                    I(f"v_add_u32_e32 v{x + 2}, s{T0}, v{x + 2}", VALU, rd=sr(T0) + vr(x + 2), wr=vr(x + 2)),
+                    I(f"v_and_b32_e32 v{x + 3}, 15, v{V_LANE}", VALU, rd=vr(V_LANE), wr=vr(x + 3)),
+                    I(f"v_lshlrev_b32_e32 v{x + 3}, 4, v{x + 3}", VALU, rd=vr(x + 3), wr=vr(x + 3))]
         for vq, rs in ((V_QV0, Rq), (V_OV0, Rdo)):
             ins += [I(f"v_mul_lo_u32 v{vq}, v{x + 2}, s{rs}", VALU, rd=vr(x + 2) + sr(rs), wr=vr(vq)),
                     I(f"v_add_u32_e32 v{vq}, v{vq}, v{x + 3}", VALU, rd=vr(vq) + vr(x + 3), wr=vr(vq)),

@@ -175,6 +175,8 @@ OPT_DEFER = os.environ.get("FA_GEN_DEFER") == "1"
 # O zeroed by v_accvgpr_write in the gaps of tile 0's MFMAs instead of ahead of them (an empty item,
 # which runs no tile 0, zeroes it on its own branch)
 OPT_T0ZERO = os.environ.get("FA_GEN_T0ZERO") == "1"
+# cache-policy modifiers of the epilogue's O stores (dev A/B), e.g. "nt"
+OPT_OPOL = (" " + os.environ["FA_GEN_OPOL"]) if os.environ.get("FA_GEN_OPOL") else ""
 V_LSEV = (191, 195)                   # LSE values of the finished item (deferred stores)
 V_SAVE = (228, 229, 230, 231, 238, 239)   # its O / LSE descriptor words 0..2 across the warm start
 S_ODD, S_LDD = 88, 36                 # ... restored here for tile 0 (geometry temps, free by then)
@@ -1335,7 +1337,7 @@ class K:
                         ins += [Inst(f"v_permlane32_swap_b32_e32 v{w}, v{w + 2}", PERM, rd=vr(w) + vr(w + 2), wr=vr(w) + vr(w + 2)),
                                 Inst(f"v_permlane32_swap_b32_e32 v{w + 1}, v{w + 3}", PERM, rd=vr(w + 1) + vr(w + 3), wr=vr(w + 1) + vr(w + 3))]
                     if OPT_EPI_ABL != "nostore" and not OPT_DEFER:
-                        ins.append(Inst(f"buffer_store_dwordx4 v[{w}:{w + 3}], v{V_OOFF[j]}, s[{S_OD}:{S_OD + 3}], 0 offen offset:{64 * dt + 16 * u}",
+                        ins.append(Inst(f"buffer_store_dwordx4 v[{w}:{w + 3}], v{V_OOFF[j]}, s[{S_OD}:{S_OD + 3}], 0 offen offset:{64 * dt + 16 * u}{OPT_OPOL}",
                                         VSTORE, rd=vr(w, 4) + vr(V_OOFF[j]) + sr(S_OD, 4)))
             if OPT_EPISTAMP and j == 0:
                 ins += self.stamp_point(9)
