@@ -318,6 +318,13 @@ class Emu:
                 d = lds[addr[lane]:addr[lane] + 16].view(np.uint32)
                 w.r[ri:ri + 4, lane] = d
             return
+        if op in ("ds_write_b64", "ds_write_b128"):
+            addr = self.vsrc(w, a[0]).astype(np.int64) + mods.get("offset", 0)
+            ri, n = self.regs(w, a[1])
+            nb = 8 if op == "ds_write_b64" else 16
+            for lane in range(64):
+                lds[addr[lane]:addr[lane] + nb] = w.r[ri:ri + nb // 4, lane].astype(np.uint32).view(np.uint8)
+            return
         if op == "ds_read_b64_tr_b16":
             addr = self.vsrc(w, a[1]).astype(np.int64) + mods.get("offset", 0)
             ri, n = self.regs(w, a[0])
@@ -383,6 +390,12 @@ class Emu:
                 return U(a[1]) - U(a[2])
             if base == "v_subrev_u32":
                 return U(a[2]) - U(a[1])
+            if base == "v_mul_u32_u24":
+                return (U(a[1]) & 0xFFFFFF) * (U(a[2]) & 0xFFFFFF)
+            if base == "v_or_b32":
+                return U(a[1]) | U(a[2])
+            if base == "v_lshl_or_b32":
+                return (U(a[1]) << (U(a[2]) & 31)) | U(a[3])
             if base == "v_mul_lo_u32":
                 return (U(a[1]).astype(np.uint64) * U(a[2]).astype(np.uint64)).astype(np.uint32)
             if base == "v_min_i32":

@@ -177,6 +177,9 @@ OPT_DEFER = os.environ.get("FA_GEN_DEFER") == "1"
 OPT_T0ZERO = os.environ.get("FA_GEN_T0ZERO") == "1"
 # cache-policy modifiers of the epilogue's O stores (dev A/B), e.g. "nt"
 OPT_OPOL = (" " + os.environ["FA_GEN_OPOL"]) if os.environ.get("FA_GEN_OPOL") else ""
+# O staged through LDS (the K/V slot of the item's last tile, free after the last step): each store
+# then writes whole rows (4 rows of 256 B at d = 128) instead of 32 rows x 32 B
+OPT_OSTAGE = os.environ.get("FA_GEN_OSTAGE") == "1"
 V_LSEV = (191, 195)                   # LSE values of the finished item (deferred stores)
 V_SAVE = (228, 229, 230, 231, 238, 239)   # its O / LSE descriptor words 0..2 across the warm start
 S_ODD, S_LDD = 88, 36                 # ... restored here for tile 0 (geometry temps, free by then)
@@ -1298,9 +1301,124 @@ class K:
                 op.eg = i * spread // len(out)
         return out
 
+    def lse_ops(self, j, inv, lse, t2, t3):
+        """1 / l -> v[inv], LSE -> v[lse] of q-block j (bad l: inv = 1, LSE = +inf)"""
+        l = V_L[j]
+        ins = self.half_sum(l, t2)
+        ins += [Inst(f"v_rcp_f32_e32 v{inv}, v{l}", TRANS, rd=vr(l), wr=vr(inv)),
+                Inst(f"v_log_f32_e32 v{lse}, v{l}", TRANS, rd=vr(l), wr=vr(lse)),
+                Inst(f"v_sub_f32_e32 v{lse}, v{lse}, v{V_NEGMC[j]}", VALU, rd=vr(lse) + vr(V_NEGMC[j]), wr=vr(lse)),
+                Inst(f"v_mul_f32_e32 v{lse}, 0x3f317218, v{lse}", VALU, rd=vr(lse), wr=vr(lse)),
+                Inst(f"v_cmp_neq_f32_e32 vcc, 0, v{l}", VALU, rd=vr(l), wr=[("vcc", 0)]),
+                Inst(f"v_cmp_eq_f32_e64 s[{S_TMP}:{S_TMP + 1}], v{l}, v{l}", VALU, rd=vr(l), wr=sr(S_TMP, 2)),
+                Inst(f"s_and_b64 vcc, vcc, s[{S_TMP}:{S_TMP + 1}]", SALU, rd=sr(S_TMP, 2) + [("vcc", 0)], wr=[("vcc", 0)]),
+                Inst(f"v_cndmask_b32_e64 v{inv}, 1.0, v{inv}, vcc", VALU, rd=vr(inv) + [("vcc", 0)], wr=vr(inv)),
+                Inst(f"v_mov_b32_e32 v{t3}, 0x7f800000", VALU, wr=vr(t3)),
+                Inst(f"v_cndmask_b32_e32 v{lse}, v{t3}, v{lse}, vcc", VALU, rd=vr(lse) + vr(t3) + [("vcc", 0)], wr=vr(lse))]
+        return ins
+
+    def epilogue_staged(self):
+        """(FA_GEN_OSTAGE) O normalised, packed and written to LDS in row-major order (XOR-swizzled
+        16-byte chunks), read back 16 bytes per lane with lpr lanes per row and stored as whole rows.
+        The staging area is the K/V slot of the item's last tile: its K part was last read in the
+        previous step (before that step's barrier), its V part in the last step -- hence the barrier
+        first (a refit of the last step re-reads the K part too).  Wave w stages one q-block at a time
+        in 32 rows x 2D bytes: waves 0, 1 in the K part, 2, 3 in the V part."""
+        I = Inst
+        Ro = self.kargs()["Ro"]
+        RB = 2 * D                      # bytes per staged row
+        NCH = RB // 16                  # 16-byte chunks per row
+        lpr = NCH                       # lanes per row when reading back
+        rpi = 64 // lpr                 # rows per read / store instruction
+        nrd = 32 // rpi
+        sh = 0 if D == 128 else 1       # swizzle key = (row >> sh) & (NCH - 1): conflict-free writes
+        R = S_M0R                       # region base (SGPR)
+        T = S_TMP + 2
+        ins = [I("s_barrier", BARRIER)]
+        # region: K slot of the last tile = S_VOFF - VBASE - TILE (mod the ring), + wave part
+        ins += [I(f"s_sub_i32 s{R}, s{S_VOFF}, {VBASE + TILE}", SALU, rd=sr(S_VOFF), wr=sr(R)),
+                I(f"s_add_u32 s{T}, s{R}, {NSLOT * TILE}", SALU, rd=sr(R), wr=sr(T)),
+                I(f"s_cmp_lt_i32 s{R}, 0", SALU, rd=sr(R), wr=[("scc", 0)]),
+                I(f"s_cselect_b32 s{R}, s{T}, s{R}", SALU, rd=sr(T) + sr(R) + [("scc", 0)], wr=sr(R)),
+                I(f"s_and_b32 s{T}, s{S_WAVE}, 1", SALU, rd=sr(S_WAVE), wr=sr(T)),
+                I(f"s_mul_i32 s{T}, s{T}, {32 * RB}", SALU, rd=sr(T), wr=sr(T)),
+                I(f"s_add_u32 s{R}, s{R}, s{T}", SALU, rd=sr(R) + sr(T), wr=sr(R)),
+                I(f"s_cmp_ge_u32 s{S_WAVE}, 2", SALU, rd=sr(S_WAVE), wr=[("scc", 0)]),
+                I(f"s_cselect_b32 s{T}, {VBASE}, 0", SALU, rd=[("scc", 0)], wr=sr(T)),
+                I(f"s_add_u32 s{R}, s{R}, s{T}", SALU, rd=sr(R) + sr(T), wr=sr(R))]
+        # per-lane constants (v4..): q = lane & 31, hh = lane >> 5
+        VQ, VH, VB, VK, VBR, VLR = 4, 5, 6, 7, 80, 88
+        VA = 8                          # write addresses of the NCH chunks: v8 ..
+        ins += [I(f"v_and_b32_e32 v{VQ}, 31, v{V_LANE}", VALU, rd=vr(V_LANE), wr=vr(VQ)),
+                I(f"v_lshrrev_b32_e32 v{VH}, 5, v{V_LANE}", VALU, rd=vr(V_LANE), wr=vr(VH)),
+                I(f"v_lshrrev_b32_e32 v{VK}, {sh}, v{VQ}", VALU, rd=vr(VQ), wr=vr(VK)),
+                I(f"v_and_b32_e32 v{VK}, {NCH - 1}, v{VK}", VALU, rd=vr(VK), wr=vr(VK)),
+                I(f"v_lshlrev_b32_e32 v{VK}, 4, v{VK}", VALU, rd=vr(VK), wr=vr(VK)),
+                I(f"v_mul_u32_u24_e32 v{VB}, {RB}, v{VQ}", VALU, rd=vr(VQ), wr=vr(VB)),
+                I(f"v_add_u32_e32 v{VB}, s{R}, v{VB}", VALU, rd=sr(R) + vr(VB), wr=vr(VB)),
+                I(f"v_or_b32_e32 v{VB}, v{VB}, v{VK}", VALU, rd=vr(VB) + vr(VK), wr=vr(VB)),
+                I(f"v_lshl_or_b32 v{VB}, v{VH}, 3, v{VB}", VALU, rd=vr(VH) + vr(VB), wr=vr(VB))]
+        for c in range(NCH):
+            ins.append(I(f"v_xor_b32_e32 v{VA + c}, {16 * c}, v{VB}", VALU, rd=vr(VB), wr=vr(VA + c)))
+        # read-back: lane row lr = lane / lpr, chunk cc = lane % lpr; physical chunk = cc ^ key(row)
+        # key(rpi i + lr) = key_i ^ (lr >> sh)  (disjoint bits), key_i = ((rpi i) >> sh) & (NCH - 1)
+        lg = lpr.bit_length() - 1
+        ins += [I(f"v_lshrrev_b32_e32 v{VLR}, {lg}, v{V_LANE}", VALU, rd=vr(V_LANE), wr=vr(VLR)),            # lr
+                I(f"v_and_b32_e32 v{VLR + 1}, {lpr - 1}, v{V_LANE}", VALU, rd=vr(V_LANE), wr=vr(VLR + 1)),   # cc
+                I(f"v_lshrrev_b32_e32 v{VLR + 2}, {sh}, v{VLR}", VALU, rd=vr(VLR), wr=vr(VLR + 2)),
+                I(f"v_xor_b32_e32 v{VLR + 2}, v{VLR + 2}, v{VLR + 1}", VALU, rd=vr(VLR + 1, 2), wr=vr(VLR + 2)),
+                I(f"v_mul_u32_u24_e32 v{VLR + 3}, {RB}, v{VLR}", VALU, rd=vr(VLR), wr=vr(VLR + 3)),
+                I(f"v_add_u32_e32 v{VLR + 3}, s{R}, v{VLR + 3}", VALU, rd=sr(R) + vr(VLR + 3), wr=vr(VLR + 3)),
+                I(f"v_lshl_or_b32 v{VLR + 3}, v{VLR + 2}, 4, v{VLR + 3}", VALU, rd=vr(VLR + 2, 2), wr=vr(VLR + 3))]
+        keys = sorted({((rpi * i) >> sh) & (NCH - 1) for i in range(nrd)})
+        kreg = {}
+        for n, k in enumerate(keys):
+            kreg[k] = VBR + n
+            ins.append(I(f"v_xor_b32_e32 v{VBR + n}, {16 * k}, v{VLR + 3}", VALU, rd=vr(VLR + 3), wr=vr(VBR + n)))
+        # global row offsets of the read-back rows: (64 wave + 32 j + lr) Ro + 16 cc
+        VS = (VLR + 4, VLR + 5)
+        ins += [I(f"v_lshlrev_b32_e32 v{VLR + 6}, 4, v{VLR + 1}", VALU, rd=vr(VLR + 1), wr=vr(VLR + 6))]
+        for j in range(2):
+            ins += [I(f"s_lshl_b32 s{T}, s{S_WAVE}, 6", SALU, rd=sr(S_WAVE), wr=sr(T)),
+                    I(f"s_add_u32 s{T}, s{T}, {32 * j}", SALU, rd=sr(T), wr=sr(T)),
+                    I(f"v_add_u32_e32 v{VS[j]}, s{T}, v{VLR}", VALU, rd=sr(T) + vr(VLR), wr=vr(VS[j])),
+                    I(f"v_mul_lo_u32 v{VS[j]}, v{VS[j]}, s{Ro}", VALU, rd=vr(VS[j]) + sr(Ro), wr=vr(VS[j])),
+                    I(f"v_add_u32_e32 v{VS[j]}, v{VS[j]}, v{VLR + 6}", VALU, rd=vr(VS[j]) + vr(VLR + 6), wr=vr(VS[j]))]
+        RD = 48                          # read-back data v48 .. v79
+        XT, PKT = 24, 40                 # 4 sets of 4 temps, 4 pairs
+        for j in range(2):
+            inv, lse = 0, 1
+            ins += self.lse_ops(j, inv, lse, 2, 3)
+            ins.append(I(f"buffer_store_dword v{lse}, v{V_LSEOFF[j]}, s[{S_LD}:{S_LD + 3}], 0 offen", VSTORE,
+                         rd=vr(lse) + vr(V_LSEOFF[j]) + sr(S_LD, 4)))
+            n = 0
+            for dt in range(NP):
+                for k4 in range(4):
+                    x, pk = XT + 4 * (n % 4), PKT + 2 * (n % 4)
+                    o = O_(j, dt) + 4 * k4
+                    ins += [I(f"v_accvgpr_read_b32 v{x + k}, a{o + k}", ACCR, rd=ar(o + k), wr=vr(x + k)) for k in range(4)]
+                    ins += [I(f"v_mul_f32_e32 v{x + k}, v{x + k}, v{inv}", VALU, rd=vr(x + k) + vr(inv), wr=vr(x + k)) for k in range(4)]
+                    ins += [self.cvt(pk, x, x + 1), self.cvt(pk + 1, x + 2, x + 3)]
+                    c = 4 * dt + k4
+                    ins.append(I(f"ds_write_b64 v{VA + c}, v[{pk}:{pk + 1}]", LDS, rd=vr(VA + c) + vr(pk, 2)))
+                    n += 1
+            ins.append(I("s_waitcnt lgkmcnt(0)", WAIT))
+            for i in range(nrd):
+                k = ((rpi * i) >> sh) & (NCH - 1)
+                ins.append(I(f"ds_read_b128 v[{RD + 4 * i}:{RD + 4 * i + 3}], v{kreg[k]} offset:{rpi * i * RB}", LDS,
+                             rd=vr(kreg[k]), wr=vr(RD + 4 * i, 4)))
+            ins.append(I("s_waitcnt lgkmcnt(0)", WAIT))
+            for i in range(nrd):
+                ins += [I(f"s_mul_i32 s{T}, s{Ro}, {rpi * i}", SALU, rd=sr(Ro), wr=sr(T)),
+                        I(f"buffer_store_dwordx4 v[{RD + 4 * i}:{RD + 4 * i + 3}], v{VS[j]}, s[{S_OD}:{S_OD + 3}], s{T} offen",
+                          VSTORE, rd=vr(RD + 4 * i, 4) + vr(VS[j]) + sr(S_OD, 4) + sr(T))]
+        return ins
+
     def epilogue(self):
         if OPT_EPI2:
             return self.epilogue2()
+        if OPT_OSTAGE:
+            return self.epilogue_staged()
         ins = []
         t = 0   # the score registers are free after the last step
         for j in range(2):
@@ -1336,7 +1454,21 @@ class K:
                                 self.cvt(w + 2, x + 4, x + 5), self.cvt(w + 3, x + 6, x + 7)]
                         ins += [Inst(f"v_permlane32_swap_b32_e32 v{w}, v{w + 2}", PERM, rd=vr(w) + vr(w + 2), wr=vr(w) + vr(w + 2)),
                                 Inst(f"v_permlane32_swap_b32_e32 v{w + 1}, v{w + 3}", PERM, rd=vr(w + 1) + vr(w + 3), wr=vr(w + 1) + vr(w + 3))]
-                    if OPT_EPI_ABL != "nostore" and not OPT_DEFER:
+                    if OPT_EPI_ABL == "orows":   # timing ablation (wrong placement): 4 whole rows per store
+                        Ro = self.kargs()["Ro"]
+                        i = 2 * dt + u // 2
+                        if i == 0:
+                            ins += [Inst(f"v_and_b32_e32 v28, 0xffffffe0, v{V_ROW[j]}", VALU, rd=vr(V_ROW[j]), wr=vr(28)),
+                                    Inst(f"v_lshrrev_b32_e32 v29, 4, v{V_LANE}", VALU, rd=vr(V_LANE), wr=vr(29)),
+                                    Inst("v_add_u32_e32 v28, v28, v29", VALU, rd=vr(28) + vr(29), wr=vr(28)),
+                                    Inst(f"v_mul_lo_u32 v28, v28, s{Ro}", VALU, rd=vr(28) + sr(Ro), wr=vr(28)),
+                                    Inst(f"v_and_b32_e32 v29, 15, v{V_LANE}", VALU, rd=vr(V_LANE), wr=vr(29)),
+                                    Inst("v_lshl_add_u32 v28, v29, 4, v28", VALU, rd=vr(28) + vr(29), wr=vr(28))]
+                        ins += [Inst(f"s_mul_i32 s{S_TMP + 2}, s{Ro}, {4 * i}", SALU, rd=sr(Ro), wr=sr(S_TMP + 2)),
+                                Inst(f"v_add_u32_e32 v30, s{S_TMP + 2}, v28", VALU, rd=sr(S_TMP + 2) + vr(28), wr=vr(30)),
+                                Inst(f"buffer_store_dwordx4 v[{w}:{w + 3}], v30, s[{S_OD}:{S_OD + 3}], 0 offen",
+                                     VSTORE, rd=vr(w, 4) + vr(30) + sr(S_OD, 4))]
+                    elif OPT_EPI_ABL != "nostore" and not OPT_DEFER:
                         ins.append(Inst(f"buffer_store_dwordx4 v[{w}:{w + 3}], v{V_OOFF[j]}, s[{S_OD}:{S_OD + 3}], 0 offen offset:{64 * dt + 16 * u}{OPT_OPOL}",
                                         VSTORE, rd=vr(w, 4) + vr(V_OOFF[j]) + sr(S_OD, 4)))
             if OPT_EPISTAMP and j == 0:
