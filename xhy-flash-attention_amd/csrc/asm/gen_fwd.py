@@ -178,8 +178,9 @@ OPT_T0ZERO = os.environ.get("FA_GEN_T0ZERO") == "1"
 # cache-policy modifiers of the epilogue's O stores (dev A/B), e.g. "nt"
 OPT_OPOL = (" " + os.environ["FA_GEN_OPOL"]) if os.environ.get("FA_GEN_OPOL") else ""
 # O staged through LDS (the K/V slot of the item's last tile, free after the last step): each store
-# then writes whole rows (4 rows of 256 B at d = 128) instead of 32 rows x 32 B
-OPT_OSTAGE = os.environ.get("FA_GEN_OSTAGE") == "1"
+# then writes whole rows (4 rows of 256 B at d = 128) instead of 32 rows x 32 B (round 4 default:
+# C3 -0.3 %, C4 -0.4 %, C2 ±0, bitwise identical; FA_GEN_OSTAGE=0 restores the direct stores)
+OPT_OSTAGE = os.environ.get("FA_GEN_OSTAGE", "1") == "1"
 V_LSEV = (191, 195)                   # LSE values of the finished item (deferred stores)
 V_SAVE = (228, 229, 230, 231, 238, 239)   # its O / LSE descriptor words 0..2 across the warm start
 S_ODD, S_LDD = 88, 36                 # ... restored here for tile 0 (geometry temps, free by then)
