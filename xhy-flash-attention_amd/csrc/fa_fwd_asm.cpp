@@ -44,7 +44,8 @@ struct FwdAsmArgs {
   float c;
   int32_t flags;    // bit 0: varlen_padded_input
   int32_t n_items;  // entries of the work table
-  int32_t grid;     // workgroups: workgroup w runs items r G + (r odd ? G - 1 - w : w), r = 0, 1, ...
+  int32_t grid;     // workgroups: workgroup w runs items r G + (r odd ? rev(w) : w), r = 0, 1, ...; rev
+                    // reverses groups of 8 workgroups when G % 8 == 0 (w keeps its XCD), else G - 1 - w
   int32_t pad;
   ItemDecode dec;   // the work order, computed in the kernel from the item index (flags bit 1 clear)
 };
