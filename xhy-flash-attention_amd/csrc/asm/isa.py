@@ -11,6 +11,7 @@ was read stale on hardware, which misplaced every LDS-DMA piece (tools/probe_gen
 inserts `s_waitcnt lgkmcnt(N)` / `vmcnt(N)` before the first reader of a register that a still
 outstanding LDS or VMEM load writes, counted (only the loads that have to land are waited for).
 """
+import os
 
 # instruction kinds
 MFMA, VALU, TRANS, PERM, ACCR, ACCW, SALU, SMEM, LDS, DMA, VLOAD, VSTORE, WAIT, NOP, BRANCH, LABEL, \
@@ -20,6 +21,10 @@ VALU_LIKE = (VALU, TRANS, PERM, ACCR, ACCW, RFL)
 # issue cost in cycles (one wave alone on its SIMD; MI355X_MICROARCH.md per-instruction constants)
 COST = {MFMA: 8, VALU: 4, TRANS: 8, PERM: 4, ACCR: 4, ACCW: 4, SALU: 2, SMEM: 2, LDS: 2, DMA: 8,
         VLOAD: 4, VSTORE: 4, WAIT: 1, NOP: 4, BRANCH: 2, LABEL: 0, BARRIER: 4, SOPP: 2, RFL: 4}
+# dev A/B: scheduling weights, e.g. FA_ISA_COST="TRANS=7,LDS=3" (tools/asm_variant.sh)
+for _kv in filter(None, os.environ.get("FA_ISA_COST", "").split(",")):
+    _k, _v = _kv.split("=")
+    COST[{"TRANS": TRANS, "VALU": VALU, "LDS": LDS, "SALU": SALU, "DMA": DMA, "PERM": PERM}[_k]] = int(_v)
 
 
 def vr(i, n=1):
