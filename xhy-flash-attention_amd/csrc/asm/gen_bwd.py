@@ -44,6 +44,13 @@ from isa import (ACCR, ACCW, BARRIER, BRANCH, DMA, LABEL, LDS, MFMA, PERM, RFL, 
                  TRANS, VALU, VLOAD, VSTORE, WAIT, Inst, add_waits, ar, fix_hazards, item_decode_ops, item_pos_ops, label, nop, rtxt,
                  schedule, sr, vr)
 
+import isa as _isa  # noqa: E402
+
+# scheduling weights (round 4 A/B, profiles/r04/ab_sched_weights_r04.txt): an LDS read weighs 5 issue
+# cycles in the gap budget (2 before), spreading the reads over more MFMA gaps
+_isa.apply_costs("LDS=5")
+_isa.apply_costs(os.environ.get("FA_ISA_COST", ""))
+_isa.apply_costs(os.environ.get("FA_GBW_COST", ""))
 D = 128
 KS = D // 16            # k-steps of S / dP
 NP = D // 32            # d-tiles of dV^T / dK^T

@@ -43,6 +43,13 @@ from isa import (ACCR, ACCW, BARRIER, BRANCH, DMA, LABEL, LDS, MFMA, NOP, PERM, 
                  TRANS, VALU, VLOAD, VSTORE, WAIT, Counters, Inst, add_waits, ar, fix_hazards, label, nop,
                  item_decode_ops, rtxt, schedule, sr, vr)
 
+import isa as _isa  # noqa: E402
+
+# scheduling weights (round 4 A/B, profiles/r04/ab_sched_weights_r04.txt): an LDS read weighs 4 issue
+# cycles in the gap budget (2 before), spreading the reads over more MFMA gaps
+_isa.apply_costs("LDS=4")
+_isa.apply_costs(os.environ.get("FA_ISA_COST", ""))
+_isa.apply_costs(os.environ.get("FA_GEN_COST", ""))
 BN = 64               # keys per K/V tile
 BM = 256              # query rows per workgroup
 NSLOT = 5

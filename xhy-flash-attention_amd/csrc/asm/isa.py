@@ -21,10 +21,20 @@ VALU_LIKE = (VALU, TRANS, PERM, ACCR, ACCW, RFL)
 # issue cost in cycles (one wave alone on its SIMD; MI355X_MICROARCH.md per-instruction constants)
 COST = {MFMA: 8, VALU: 4, TRANS: 8, PERM: 4, ACCR: 4, ACCW: 4, SALU: 2, SMEM: 2, LDS: 2, DMA: 8,
         VLOAD: 4, VSTORE: 4, WAIT: 1, NOP: 4, BRANCH: 2, LABEL: 0, BARRIER: 4, SOPP: 2, RFL: 4}
-# dev A/B: scheduling weights, e.g. FA_ISA_COST="TRANS=7,LDS=3" (tools/asm_variant.sh)
-for _kv in filter(None, os.environ.get("FA_ISA_COST", "").split(",")):
-    _k, _v = _kv.split("=")
-    COST[{"TRANS": TRANS, "VALU": VALU, "LDS": LDS, "SALU": SALU, "DMA": DMA, "PERM": PERM}[_k]] = int(_v)
+COST_LDS128 = None      # (LDS128=n) a separate weight for ds_read_b128
+
+
+def apply_costs(spec):
+    """scheduling weights, e.g. "LDS=5,SALU=3": each generator applies its defaults, then
+    FA_ISA_COST and its own FA_G*_COST (dev A/B, tools/asm_variant.sh).  The gap scheduler fills a
+    gap while the weights fit the budget, so a heavier LDS weight spreads the reads over more gaps."""
+    global COST_LDS128
+    for kv in filter(None, spec.split(",")):
+        k, v = kv.split("=")
+        if k == "LDS128":
+            COST_LDS128 = int(v)
+            continue
+        COST[{"TRANS": TRANS, "VALU": VALU, "LDS": LDS, "SALU": SALU, "DMA": DMA, "PERM": PERM}[k]] = int(v)
 
 
 def vr(i, n=1):
@@ -57,6 +67,8 @@ class Inst:
         self.dl = deadline            # must be emitted before MFMA number dl of its phase
         self.eg = earliest            # may not be emitted before gap eg (after MFMA eg)
         self.cost = COST[kind]
+        if COST_LDS128 is not None and kind == LDS and text.startswith("ds_read_b128"):
+            self.cost = COST_LDS128
         self.deps = list(deps)        # filler ops that must precede this one
         self.name = name
 
