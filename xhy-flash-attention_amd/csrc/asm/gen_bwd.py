@@ -46,9 +46,9 @@ from isa import (ACCR, ACCW, BARRIER, BRANCH, DMA, LABEL, LDS, MFMA, PERM, RFL, 
 
 import isa as _isa  # noqa: E402
 
-# scheduling weights (round 4 A/B, profiles/r04/ab_sched_weights_r04.txt): an LDS read weighs 5 issue
+# scheduling weights (round 4 A/B, profiles/r04/ab_sched_weights_r04.txt): an LDS read weighs 5 (a SALU op 3) issue
 # cycles in the gap budget (2 before), spreading the reads over more MFMA gaps
-_isa.apply_costs("LDS=5")
+_isa.apply_costs("LDS=5,SALU=3")
 _isa.apply_costs(os.environ.get("FA_ISA_COST", ""))
 _isa.apply_costs(os.environ.get("FA_GBW_COST", ""))
 D = 128
