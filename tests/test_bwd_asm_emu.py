@@ -110,6 +110,19 @@ def test_asm_dq_persistent_loop(dq_text, b, sq, sk, h, hk, causal, grid):
     assert e <= 1e-2, e
 
 
+@pytest.mark.timeout(900)
+@pytest.mark.parametrize("b,sq,sk,h,hk,causal,bf16", [
+    (1, 330, 200, 2, 1, True, True),            # GQA, ragged last group (rows past seqlen_q: zero scratch)
+    (1, 96, 300, 3, 1, True, False),            # fp16 (v_dot2_f32_f16)
+])
+def test_asm_dq_fused_pre_in_emulator(dq_text, b, sq, sk, h, hk, causal, bf16):
+    """flags bit 1 (knob 8): the dQ kernel computes D = rowsum(dO o O) itself (bwd_pre_kernel's work):
+    the softmax_d input is NaN, the outputs softmax_d and the dK/dV scratch are checked too"""
+    import emu_dq
+    e, *_ = emu_dq.run(b, sq, sk, h, hk, causal, bf16, seed=2, text=dq_text, verbose=False, fused=True)
+    assert e <= (1e-2 if bf16 else 2e-3), e
+
+
 def test_generated_dq_kernels_assemble_shape():
     text = subprocess.run([sys.executable, os.path.join(ROOT, "xhy-flash-attention_amd", "csrc", "asm", "gen_dq.py")],
                           check=True, capture_output=True, text=True).stdout

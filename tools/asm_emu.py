@@ -287,8 +287,8 @@ class Emu:
         if op == "s_branch":
             w.pc = self.labels[a[0]]
             return
-        if op == "s_cbranch_scc1":
-            if w.scc:
+        if op in ("s_cbranch_scc1", "s_cbranch_scc0"):
+            if bool(w.scc) == (op == "s_cbranch_scc1"):
                 w.pc = self.labels[a[0]]
             return
         if op in ("s_cbranch_vccnz", "s_cbranch_vccz"):
@@ -404,6 +404,12 @@ class Emu:
                 return (U(a[1]) >> U(a[2])) & ((np.uint32(1) << U(a[3])) - 1)
             if base == "v_cvt_f32_u32":
                 return f2u(U(a[1]).astype(np.float32))
+            if base in ("v_dot2_f32_bf16", "v_dot2_f32_f16"):
+                cv = bf16_to_f32 if base.endswith("bf16") else f16_to_f32
+                x, y = U(a[1]), U(a[2])
+                lo = cv((x & 0xFFFF).astype(np.uint16)).astype(np.float64) * cv((y & 0xFFFF).astype(np.uint16))
+                hi = cv((x >> 16).astype(np.uint16)).astype(np.float64) * cv((y >> 16).astype(np.uint16))
+                return f2u(np.float32(lo + hi + F(a[3])))
             if base == "v_fma_f32":
                 return f2u(np.float32(F(a[1]).astype(np.float64) * F(a[2]) + F(a[3])))
             if base == "v_exp_f32":
@@ -439,7 +445,7 @@ class Emu:
             x, y = self.vsrc(w, a[1]), self.vsrc(w, a[2])
         with np.errstate(all="ignore"):
             r = {"gt": x > y, "lt": x < y, "ge": x >= y, "le": x <= y, "eq": x == y,
-                 "neq": ~(x == y), "nge": ~(x >= y), "lg": (x < y) | (x > y)}[kind]
+                 "neq": ~(x == y), "nge": ~(x >= y), "lg": (x < y) | (x > y), "ne": x != y}[kind]
         if a[0] == "vcc":
             w.vcc = r
         else:

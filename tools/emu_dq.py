@@ -38,15 +38,21 @@ def pack_args(**kw):
     out += struct.pack("<ff", kw["c"], kw["scale"])
     out += struct.pack("<10I", *kw["dec"])
     out += struct.pack("<ii", kw["n_items"], kw["grid"])
-    assert len(out) == 232, len(out)
+    # fused bwd_pre (flags bit 1): o, o_batch, o_row, o_head, lsed, lsed_ng, -1 / scale
+    out += struct.pack("<Qqii", kw.get("o", 0), kw.get("o_batch", 0), kw.get("o_row", 0), kw.get("o_head", 0))
+    out += struct.pack("<Qif", kw.get("lsed", 0), kw.get("lsed_ng", 0), kw.get("nrscale", 0.0))
+    assert len(out) == 272, len(out)
     return out
 
 
-def reference_dq(q, k, v, do, causal, scale):
+def reference_dq(q, k, v, do, causal, scale, o=None):
+    """o: D = rowsum(dO o O) from this O instead of the forward's (the fused-D test)"""
     b, sq, h, d = q.shape
     sk, hk = k.shape[1], k.shape[2]
     g = h // hk
     lse, dsum, _, _ = bwd_reference(q, k, v, do, causal, scale)
+    if o is not None:
+        dsum = np.einsum("bshd,bshd->bhs", do, o)
     dq = np.zeros_like(q)
     for bi in range(b):
         for hi in range(h):
@@ -61,9 +67,12 @@ def reference_dq(q, k, v, do, causal, scale):
     return lse, dsum, dq
 
 
-def run(b=1, sq=300, sk=300, h=2, hk=1, causal=True, bf16=True, seed=0, text=None, verbose=True, hp=0, grid=None):
+def run(b=1, sq=300, sk=300, h=2, hk=1, causal=True, bf16=True, seed=0, text=None, verbose=True, hp=0, grid=None,
+        fused=False, wgs=None):
     """hp: heads per XCD group of the work order (0: head-fastest); grid: workgroups of the
-    persistent item loop (default: one per item)"""
+    persistent item loop (default: one per item); fused: the kernel computes D = rowsum(dO o O) itself
+    (flags bit 1, bwd_pre fused): the D input is garbage, softmax_d and the dK/dV scratch
+    [-LSE / scale | -D] are checked against float64 (the error returned is the max of the three)"""
     rng = np.random.default_rng(seed)
     q = rng.standard_normal((b, sq, h, D)).astype(np.float32)
     k = rng.standard_normal((b, sk, hk, D)).astype(np.float32)
@@ -73,11 +82,17 @@ def run(b=1, sq=300, sk=300, h=2, hk=1, causal=True, bf16=True, seed=0, text=Non
     q16, k16, v16, do16 = (enc(x).astype(np.uint16) for x in (q, k, v, do))
     qf, kf, vf, dof = (dec(x).astype(np.float64) for x in (q16, k16, v16, do16))
     scale = D ** -0.5
-    lse, dsum, dq_ref = reference_dq(qf, kf, vf, dof, causal, scale)
+    of = None
+    if fused:
+        o16 = enc(rng.standard_normal((b, sq, h, D)).astype(np.float32)).astype(np.uint16)
+        of = dec(o16).astype(np.float64)
+    lse, dsum, dq_ref = reference_dq(qf, kf, vf, dof, causal, scale, o=of)
+    if fused:
+        dsum = np.einsum("bshd,bshd->bhs", dof, of)
     sqr = (sq + 127) // 128 * 128
     lse32 = lse.astype(np.float32)
     ds32 = np.zeros((b, h, sqr), np.float32)
-    ds32[:, :, :sq] = dsum
+    ds32[:, :, :sq] = np.nan if fused else dsum
     heap = Heap(64 << 20)
     aq, ak, av, ado = heap.put(q16), heap.put(k16), heap.put(v16), heap.put(do16)
     adq = heap.alloc(b * sq * h * D * 2)
@@ -92,14 +107,39 @@ def run(b=1, sq=300, sk=300, h=2, hk=1, causal=True, bf16=True, seed=0, text=Non
               q_head=D * 2, k_head=D * 2, v_head=D * 2, do_head=D * 2, dq_head=D * 2,
               sq=sq, sk=sk, lse_pitch=sq, dsum_pitch=sqr, h=h, hk=hk, flags=0,
               c=float(np.float32(scale * 1.4426950408889634)), scale=float(np.float32(scale)))
+    ng = (sq + 31) // 32
+    if fused:
+        ao = heap.put(o16)
+        alsed = heap.alloc(b * h * ng * 256)
+        heap.get(alsed, b * h * ng * 256).view(np.float32)[:] = np.nan
+        kw.update(o=ao, o_batch=sq * h * D * 2, o_row=h * D * 2, o_head=D * 2, lsed=alsed, lsed_ng=ng,
+                  nrscale=float(np.float32(-1.0 / scale)), flags=2)
     akarg = heap.put(np.frombuffer(pack_args(**kw), dtype=np.uint8))
     text = text or asm_text()
     name = f"fa_bwd_dq_asm_d128_{'bf16' if bf16 else 'f16'}_{'causal' if causal else 'full'}"
     emu = Emu(text, name, heap)
-    for L in range(grid or n_items):
+    for L in range(grid or n_items) if wgs is None else wgs:
         emu.run_wg(L, akarg)
     dq = dec(heap.get(adq, b * sq * h * D * 2).view(np.uint16)).reshape(b, sq, h, D).astype(np.float64)
     e = np.abs(dq - dq_ref).max() / max(np.abs(dq_ref).max(), 1e-9)
+    if fused:
+        got = heap.get(ads, b * h * sqr * 4).view(np.float32).reshape(b, h, sqr)[:, :, :sq]
+        if wgs is not None:     # a subset of the items: the rows they wrote
+            ok = np.isfinite(got)
+            ed = np.abs(got[ok] - dsum[ok]).max() / max(np.abs(dsum).max(), 1e-9)
+            print(f"softmax_d: {ok.sum()} rows written, rel max err {ed:.3e}")
+            return ed, got, dsum
+        e = max(e, np.abs(got - dsum).max() / max(np.abs(dsum).max(), 1e-9))
+        sc = heap.get(alsed, b * h * ng * 256).view(np.float32).reshape(b, h, ng, 2, 32)
+        want = np.zeros((b, h, ng * 32, 2))
+        with np.errstate(all="ignore"):
+            want[:, :, :sq, 0] = -lse / scale
+        want[:, :, :sq, 1] = -dsum
+        want = want.reshape(b, h, ng, 32, 2).transpose(0, 1, 2, 4, 3)
+        fin = np.isfinite(want)
+        assert np.array_equal(fin, np.isfinite(sc)), "scratch: non-finite entries differ"
+        assert np.array_equal(want[~fin], sc[~fin].astype(np.float64)), "scratch: infinite entries differ"
+        e = max(e, np.abs(sc[fin] - want[fin]).max() / max(np.abs(want[fin]).max(), 1e-9))
     if verbose:
         print(f"b={b} sq={sq} sk={sk} h={h} hk={hk} causal={causal} bf16={bf16}: rel max|ddQ| {e:.3e} "
               f"({emu.count} instructions, {emu.mfma_count} MFMAs)")
@@ -116,5 +156,6 @@ if __name__ == "__main__":
     ap.add_argument("--full", action="store_true")
     ap.add_argument("--fp16", action="store_true")
     ap.add_argument("--seed", type=int, default=0)
+    ap.add_argument("--fused", action="store_true", help="the kernel computes D (bwd_pre fused)")
     a = ap.parse_args()
-    run(a.b, a.sq, a.sk, a.h, a.hk, not a.full, not a.fp16, a.seed)
+    run(a.b, a.sq, a.sk, a.h, a.hk, not a.full, not a.fp16, a.seed, fused=a.fused)

@@ -18,6 +18,8 @@ gfx950 rules below (wait states = issued instructions in between, `s_nop N` coun
     transcendental (v_exp / v_log / v_rcp / ...) -> VALU reads its result        1
     VALU writes a VGPR -> v_permlane*_swap reads it                              2
     VALU writes a VGPR -> v_readfirstlane / v_readlane reads it                  1
+    v_dot* writes a VGPR -> another VALU reads it (except the same v_dot
+        opcode reading it as the accumulator, src2)                            3
 
     python tools/hazard_check.py [LIB.so]
 """
@@ -36,7 +38,7 @@ TRANS_OPS = ("v_exp_", "v_log_", "v_rcp_", "v_rsq_", "v_sqrt_", "v_sin_", "v_cos
 
 RULES = {   # name: wait states
     "valu->mfma": 2, "mfma->access": 12, "mfma->mfma": 12, "valu_sgpr->vmem": 5, "m0->lds_dma": 1,
-    "trans->valu": 1, "valu->permlane": 2, "valu->readlane": 1,
+    "trans->valu": 1, "valu->permlane": 2, "valu->readlane": 1, "dot->valu": 3,
 }
 MAXWS = max(RULES.values())
 
@@ -208,6 +210,11 @@ def need(p, c):
             found.append("valu->readlane")
         if p.kind == "trans" and c.kind in ("valu", "trans", "permlane", "readlane") and vw & c.rd:
             found.append("trans->valu")
+        if p.op.startswith("v_dot") and c.kind in ("valu", "trans", "permlane", "readlane") and vw & c.rd:
+            co = c.ops
+            acc_only = (c.op == p.op and len(co) > 3 and not (vw & (regs(co[1]) | regs(co[2]))))
+            if not acc_only:
+                found.append("dot->valu")
     if p.kind == "salu" and ("m0",) in p.wr and c.kind == "lds_dma":
         found.append("m0->lds_dma")
     if not found:

@@ -59,6 +59,7 @@ VMCNT_STEP = 8
 
 OPT_WIN = int(os.environ.get("FA_GDQ_WIN", "16"))
 OPT_LEAD = int(os.environ.get("FA_GDQ_LEAD", "2"))
+OPT_OWAIT = int(os.environ.get("FA_GDQ_OWAIT", "23"))
 
 # ---- AGPRs ----
 def DQ(j, dt):
@@ -123,7 +124,8 @@ S_ROUND = 100                  # round r of the persistent item loop
 S_ITEM = 101                   # the item index
 NSGPR = 102
 
-KARG_SIZE = 232
+KARG_SIZE = 272
+FUSE_OFF = 232   # DqAsmArgs: o, o_batch, o_row, o_head, lsed, lsed_ng, nrscale (flags bit 1: fused D)
 DEC_OFF = 184    # fa_params.h ItemDecode (40 bytes) after DqAsmArgs' 184
 NITEMS_OFF = 224  # n_items, grid (persistent item loop)
 
@@ -304,7 +306,7 @@ class K:
         return schedule(mf, fill)
 
     # ------------------------------------------------------------------ prologue
-    def prologue(self, l_epi):
+    def prologue(self):
         I = Inst
         ins = []
         # kernargs (DqAsmArgs, fa_bwd_asm.cpp) -> s56..s99
@@ -471,6 +473,61 @@ class K:
         # dQ descriptor (S_QD is still read by the loads above: the epilogue builds it in S_OD... kept
         # in SGPRs nothing rewrites: 92..95)
         ins += desc(92, Pdq, DQOFF, HEAD, Hdq, M0R, Rdq, [I(f"s_mul_i32 s94, s{NROW}, s{Rdq}", SALU, rd=sr(NROW) + sr(Rdq), wr=sr(94))])
+        # (flags bit 1, knob 8: bwd_pre fused) O fragments for D = rowsum(dO o O).  O descriptor in
+        # s[16:19] (the dO loads are issued); the dK/dV scratch descriptor in s[12:15] (the Q loads are
+        # issued); kernargs o, o_batch, o_row, o_head, lsed in s[40:47] (the row offsets are consumed),
+        # lsed_ng, -1 / scale in s[48:49] (the LSE descriptor's loads are issued; s49 lives to fused_d)
+        l_nof = self.lab("nofuse")
+        Po, Bo, Ro, Ho, Plsed, NG = 40, 42, 44, 45, 46, 48
+        OOFF = (18, 19)
+        ins += [I(f"s_bitcmp1_b32 s{FLG}, 1", SALU, rd=sr(FLG), wr=[("scc", 0)]),
+                I(f"s_cbranch_scc0 {l_nof}", BRANCH),
+                I(f"s_load_dwordx8 s[40:47], s[0:1], {FUSE_OFF}", SMEM, rd=sr(0, 2), wr=sr(40, 8)),
+                I(f"s_load_dwordx2 s[48:49], s[0:1], {FUSE_OFF + 32}", SMEM, rd=sr(0, 2), wr=sr(48, 2)),
+                I("s_waitcnt lgkmcnt(0)", WAIT)]
+        lf, ld = self.lab("ofixed"), self.lab("odone")
+        ins += [I(f"s_cmp_eq_u64 s[{Pcq}:{Pcq + 1}], 0", SALU, rd=sr(Pcq, 2), wr=[("scc", 0)]),
+                I(f"s_cbranch_scc1 {lf}", BRANCH),
+                I(f"s_bitcmp1_b32 s{FLG}, 0", SALU, rd=sr(FLG), wr=[("scc", 0)]),
+                I(f"s_cbranch_scc1 {lf}", BRANCH),
+                I(f"s_lshl_b32 s{T[2]}, s{BIDB}, 2", SALU, rd=sr(BIDB), wr=sr(T[2])),
+                I(f"s_load_dword s{T[2]}, s[{Pcq}:{Pcq + 1}], s{T[2]}", SMEM, rd=sr(Pcq, 2) + sr(T[2]), wr=sr(T[2])),
+                I("s_waitcnt lgkmcnt(0)", WAIT)]
+        ins += mul64(OOFF, T[2], Ro)
+        ins += [I(f"s_branch {ld}", BRANCH), label(lf)]
+        ins += mul64_i64(OOFF, BIDB, Bo)
+        ins += [label(ld)]
+        ins += desc(16, Po, OOFF, HEAD, Ho, M0R, Ro, [I(f"s_mul_i32 s18, s{NROW}, s{Ro}", SALU, rd=sr(NROW) + sr(Ro), wr=sr(18))])
+        # lsed + ((bidb h + head) ng) 256 + m0 8 (the item's first group), records ng 256 - m0 8
+        ins += [I(f"s_mul_i32 s{T[0]}, s{BIDB}, s{NH}", SALU, rd=sr(BIDB) + sr(NH), wr=sr(T[0])),
+                I(f"s_add_u32 s{T[0]}, s{T[0]}, s{HEAD}", SALU, rd=sr(T[0]) + sr(HEAD), wr=sr(T[0])),
+                I(f"s_mul_i32 s{T[0]}, s{T[0]}, s{NG}", SALU, rd=sr(T[0]) + sr(NG), wr=sr(T[0])),
+                I(f"s_lshr_b32 s{T[1]}, s{T[0]}, 24", SALU, rd=sr(T[0]), wr=sr(T[1])),
+                I(f"s_lshl_b32 s{T[0]}, s{T[0]}, 8", SALU, rd=sr(T[0]), wr=sr(T[0])),
+                I(f"s_add_u32 s12, s{Plsed}, s{T[0]}", SALU, rd=sr(Plsed) + sr(T[0]), wr=sr(12) + [("scc", 0)]),
+                I(f"s_addc_u32 s13, s{Plsed + 1}, s{T[1]}", SALU, rd=sr(Plsed + 1) + sr(T[1]) + [("scc", 0)], wr=sr(13) + [("scc", 0)]),
+                I(f"s_lshl_b32 s{T[0]}, s{M0R}, 3", SALU, rd=sr(M0R), wr=sr(T[0])),
+                I(f"s_add_u32 s12, s12, s{T[0]}", SALU, rd=sr(12) + sr(T[0]), wr=sr(12) + [("scc", 0)]),
+                I("s_addc_u32 s13, s13, 0", SALU, rd=sr(13) + [("scc", 0)], wr=sr(13)),
+                I("s_and_b32 s13, s13, 0xffff", SALU, rd=sr(13), wr=sr(13)),
+                I(f"s_lshl_b32 s14, s{NG}, 8", SALU, rd=sr(NG), wr=sr(14)),
+                I(f"s_sub_u32 s14, s14, s{T[0]}", SALU, rd=sr(14) + sr(T[0]), wr=sr(14)),
+                I("s_mov_b32 s15, 0x20000", SALU, wr=sr(15))]
+        # O fragments into v[64 + 32 j + 4 ks ..] (the dP^T tiles, free until phase -1); lane rows as
+        # the Q / dO loads', with o_row
+        for j in range(2):
+            ins += [I(f"v_lshl_add_u32 v{x}, v1, 6, v{r_}", VALU, rd=vr(1) + vr(r_), wr=vr(x)),
+                    I(f"v_add_u32_e32 v{x}, {32 * j}, v{x}", VALU, rd=vr(x), wr=vr(x)),
+                    I(f"v_mul_lo_u32 v{x + 1 + j}, v{x}, s{Ro}", VALU, rd=vr(x) + sr(Ro), wr=vr(x + 1 + j)),
+                    I(f"v_lshl_add_u32 v{x + 1 + j}, v{hh}, 4, v{x + 1 + j}", VALU, rd=vr(hh) + vr(x + 1 + j), wr=vr(x + 1 + j))]
+        # the vector memory counter holds 63: LSE / D (4), Q (16), dO (16) are in flight, the O loads (16)
+        # and the first 6 K / V subtiles (24) follow -- at most 23 of the first 36 may be outstanding
+        ins.append(I(f"s_waitcnt vmcnt({OPT_OWAIT})", WAIT))
+        for j in range(2):
+            for ks in range(KS):
+                ins.append(I(f"buffer_load_dwordx4 {rtxt('v', 64 + 32 * j + 4 * ks, 4)}, v{x + 1 + j}, s[16:19], 0 offen offset:{32 * ks}",
+                             VLOAD, rd=vr(x + 1 + j) + sr(16, 4), wr=vr(64 + 32 * j + 4 * ks, 4)))
+        ins += [label(l_nof)]
         # LDS lane bases (as gen_fwd.py)
         ins += [I(f"v_bfe_u32 v{x}, v{r_}, 2, 2", VALU, rd=vr(r_), wr=vr(x)),
                 I(f"v_xor_b32_e32 v{x + 1}, v{hh}, v{x}", VALU, rd=vr(hh) + vr(x), wr=vr(x + 1)),
@@ -516,9 +573,58 @@ class K:
                 I(f"s_mov_b32 s{S_N}, 0", SALU, wr=sr(S_N))]
         for i in range(128):
             ins.append(I(f"v_accvgpr_write_b32 a{i}, 0", ACCW, wr=ar(i)))
-        # no keys: epilogue (dQ = 0)
-        ins += [I(f"s_cmp_lt_i32 s{S_NLAST}, 0", SALU, rd=sr(S_NLAST), wr=[("scc", 0)]),
-                I(f"s_cbranch_scc1 {l_epi}", BRANCH)]
+        return ins
+
+    def fused_d(self):
+        """(flags bit 1) D = rowsum(dO o O) per row -- bwd_pre_kernel's work (fa_bwd.hip) for the item's
+        rows -- from the O fragments (v[64:127], landed with the prologue's wait) and a VGPR copy of the
+        dO fragments (v[0:63]); then V_D = D and bwd_pre_kernel's stores: softmax_d (dsum, descriptor
+        s[52:55] of the D load: row 4) and the dK/dV scratch [-LSE / scale | -D] of each 32-row group
+        (s[12:15] at the item's first group: (2 w + j) 256 + lane 4).  Rows past seqlen_q read zero O,
+        dO and LSE: their scratch entries are zero, their softmax_d stores fall outside the records."""
+        I = Inst
+        l_nof = self.lab("nofused")
+        r_, hh, x = V_TMP, V_TMP + 1, V_TMP + 2
+        dot = f"v_dot2_f32_{self.ty}"
+        ins = [I("s_bitcmp1_b32 s99, 1", SALU, rd=sr(99), wr=[("scc", 0)]), I(f"s_cbranch_scc0 {l_nof}", BRANCH)]
+        if os.environ.get("FA_GDQ_FWAIT"):
+            ins.append(I("s_waitcnt vmcnt(0)", WAIT))
+        for j in range(2):
+            for ks in range(KS):
+                for k in range(4):
+                    ins.append(I(f"v_accvgpr_read_b32 v{32 * j + 4 * ks + k}, a{OF(j, ks) + k}", ACCR,
+                                 rd=ar(OF(j, ks) + k), wr=vr(32 * j + 4 * ks + k)))
+        ins += [I(f"v_and_b32_e32 v{r_}, 31, v{V_LANE}", VALU, rd=vr(V_LANE), wr=vr(r_)),
+                I(f"v_lshrrev_b32_e32 v{hh}, 5, v{V_LANE}", VALU, rd=vr(V_LANE), wr=vr(hh)),
+                I(f"v_cmp_ne_u32_e32 vcc, 0, v{hh}", VALU, rd=vr(hh), wr=[("vcc", 0)])]
+        for j in range(2):
+            acc = V_D[j]
+            ins.append(I(f"v_mov_b32_e32 v{acc}, 0", VALU, wr=vr(acc)))
+            for i in range(32):
+                ins.append(I(f"{dot} v{acc}, v{64 + 32 * j + i}, v{32 * j + i}, v{acc}", VALU,
+                             rd=vr(64 + 32 * j + i) + vr(32 * j + i) + vr(acc), wr=vr(acc)))
+            # the other lane half holds the row's other 64 columns (a v_dot result read by another
+            # VALU op: 3 wait states -- tools/hazard_check.py "dot->valu")
+            ins += [nop(2),
+                    I(f"v_mov_b32_e32 v{x}, v{acc}", VALU, rd=vr(acc), wr=vr(x)),
+                    I(f"v_permlane32_swap_b32_e32 v{acc}, v{x}", PERM, rd=vr(acc) + vr(x), wr=vr(acc) + vr(x)),
+                    I(f"v_add_f32_e32 v{acc}, v{acc}, v{x}", VALU, rd=vr(acc) + vr(x), wr=vr(acc))]
+            # softmax_d[m0 + 64 w + 32 j + r]
+            ins += [I(f"s_lshl_b32 s{S_TMP}, s{S_WAVE}, 6", SALU, rd=sr(S_WAVE), wr=sr(S_TMP)),
+                    I(f"v_add_u32_e32 v{x + 1}, s{S_TMP}, v{r_}", VALU, rd=sr(S_TMP) + vr(r_), wr=vr(x + 1)),
+                    I(f"v_add_u32_e32 v{x + 1}, {32 * j}, v{x + 1}", VALU, rd=vr(x + 1), wr=vr(x + 1)),
+                    I(f"v_lshlrev_b32_e32 v{x + 1}, 2, v{x + 1}", VALU, rd=vr(x + 1), wr=vr(x + 1)),
+                    I(f"buffer_store_dword v{acc}, v{x + 1}, s[52:55], 0 offen", VSTORE, rd=vr(acc) + vr(x + 1) + sr(52, 4)),
+                    # scratch group 2 w + j, lane: hh ? -D : -LSE / scale (V_NLC holds the raw LSE here)
+                    I(f"v_mul_f32_e32 v{x + 2}, s49, v{V_NLC[j]}", VALU, rd=sr(49) + vr(V_NLC[j]), wr=vr(x + 2)),
+                    I(f"v_sub_f32_e32 v{x + 3}, 0, v{acc}", VALU, rd=vr(acc), wr=vr(x + 3)),
+                    I(f"v_cndmask_b32_e32 v{x + 2}, v{x + 2}, v{x + 3}, vcc", VALU, rd=vr(x + 2, 2) + [("vcc", 0)], wr=vr(x + 2)),
+                    I(f"s_lshl_b32 s{S_TMP + 1}, s{S_WAVE}, 9", SALU, rd=sr(S_WAVE), wr=sr(S_TMP + 1)),
+                    I(f"v_lshlrev_b32_e32 v{x + 4}, 2, v{V_LANE}", VALU, rd=vr(V_LANE), wr=vr(x + 4)),
+                    I(f"v_add_u32_e32 v{x + 4}, s{S_TMP + 1}, v{x + 4}", VALU, rd=sr(S_TMP + 1) + vr(x + 4), wr=vr(x + 4)),
+                    I(f"buffer_store_dword v{x + 2}, v{x + 4}, s[12:15], 0 offen offset:{256 * j}", VSTORE,
+                      rd=vr(x + 2) + vr(x + 4) + sr(12, 4))]
+        ins += [label(l_nof)]
         return ins
 
     def epilogue(self):
@@ -571,11 +677,15 @@ class K:
                 Inst("s_waitcnt lgkmcnt(0)", WAIT)]
         head += item_pos_ops(S_ITEM, S_ROUND, 2, T0 + 2, T0, T0 + 3)
         head += [Inst(f"s_cmp_ge_u32 s{S_ITEM}, s{T0 + 1}", SALU), Inst(f"s_cbranch_scc1 {self.lab_end}", BRANCH)]
-        pro = head + self.prologue(l_epi)
+        pro = head + self.prologue()
         for _ in range(KQ):
             pro += self.dma_subtile()
         # K / V(0) and (1) landed (phase -1 reads 0, its tail prefetches 1): 16 younger DMAs
         pro += [Inst("s_waitcnt vmcnt(16)", WAIT), Inst("s_barrier", BARRIER)]
+        pro += self.fused_d()
+        # no keys: epilogue (dQ = 0), after the fused D (softmax_d and the scratch are still written)
+        pro += [Inst(f"s_cmp_lt_i32 s{S_NLAST}, 0", SALU, rd=sr(S_NLAST), wr=[("scc", 0)]),
+                Inst(f"s_cbranch_scc1 {l_epi}", BRANCH)]
         emit(pro, pre=[nop(15)])
         # phase -1: S^T / dP^T(0) -> buffers 0
         # -LSE log2 e (LSE = +inf -> -inf: P = 0); the loads landed with the prologue's wait

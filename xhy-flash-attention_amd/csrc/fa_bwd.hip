@@ -1121,7 +1121,11 @@ static void run_bwd(const BwdParams& p, hipStream_t stream) {
     side = ss->s[mode - 1];
   }
   prof_begin(kTimeBwdBoth, stream);
-  if (side == nullptr) {
+  if (p.fuse_pre) {   // dQ writes D and the dK/dV scratch (no bwd_pre_kernel): dQ first, serially
+    lk.unlock();
+    dq(stream);
+    dkdv(stream);
+  } else if (side == nullptr) {
     lk.unlock();
     dkdv(stream);
     dq(stream);
@@ -1165,7 +1169,7 @@ void bwd_block_size(int d, int* block_m, int* block_n) {
 template <bool BF16>
 static void launch_bwd_t(const BwdParams& p, hipStream_t stream) {
   if (p.lse_s == nullptr) throw std::runtime_error("flash_attn_bwd: no scratch for the scaled LSE");
-  {
+  if (!p.fuse_pre) {
     // (assembly dK / dV: also the zero rows up to the last 32-row group)
     const int rows = p.lsed != nullptr ? 32 * p.lsed_ng : p.s.seqlen_q;
     dim3 grid(p.s.b * p.s.h, (rows + 63) / 64);   // 64 rows per block (bwd_pre_kernel kPreRows)
@@ -1218,6 +1222,9 @@ void launch_bwd(const BwdParams& p_in, bool is_bf16, hipStream_t stream) {
       p.lse_s = static_cast<float*>(ws.p);
     }
   }
+  // knob 8: the assembly dQ kernel computes D itself and writes softmax_d and the dK/dV scratch
+  p.fuse_pre = asm_dkdv && knob(kKnobFusePre) != 0 && p.s.d == 128 && !p.s.dropout && p.s.mask == nullptr &&
+               p.s.fm_lts == nullptr && dq_asm_applicable(p);
   if (is_bf16) launch_bwd_t<true>(p, stream); else launch_bwd_t<false>(p, stream);
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) throw std::runtime_error(std::string("flash_attn_bwd launch: ") + hipGetErrorString(e));

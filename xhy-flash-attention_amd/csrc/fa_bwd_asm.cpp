@@ -68,8 +68,14 @@ struct DqAsmArgs {
   ItemDecode dec;   // the work order, computed in the kernel from the item index
   int32_t n_items;  // items (batch x heads x query blocks)
   int32_t grid;     // workgroups (persistent item loop, as BwdAsmArgs)
+  // flags bit 1 (BwdParams::fuse_pre): D = rowsum(dO o O) in the kernel, written to dsum and with
+  // -LSE / scale to the dK/dV scratch lsed (bwd_pre_kernel's outputs)
+  const void* o; int64_t o_batch;                                   // bytes
+  int32_t o_row, o_head;                                            // bytes
+  float* lsed; int32_t lsed_ng; float nrscale;                      // -1 / scale
 };
-static_assert(sizeof(DqAsmArgs) == 232 && offsetof(DqAsmArgs, dec) == 184, "DqAsmArgs layout");
+static_assert(sizeof(DqAsmArgs) == 272 && offsetof(DqAsmArgs, dec) == 184 && offsetof(DqAsmArgs, o) == 232,
+              "DqAsmArgs layout");
 
 constexpr int kMaxDev = 64;
 constexpr int kBkn = 128;   // keys per workgroup
@@ -185,7 +191,8 @@ bool dq_asm_applicable(const BwdParams& p) {
   if (p.k_row != p.v_row || p.k_batch != p.v_batch) return false;   // K / V share the DMA offsets
   const int nmb = (s.seqlen_q + 255) / 256;
   if (nmb > 65535 || (long long)s.b * s.h * nmb > 0x7fffffffll) return false;
-  for (int64_t x : {p.q_row, p.k_row, p.do_row, p.dq_row, p.q_head, p.k_head, p.v_head, p.do_head, p.dq_head})
+  for (int64_t x : {p.q_row, p.k_row, p.do_row, p.dq_row, p.q_head, p.k_head, p.v_head, p.do_head, p.dq_head,
+                    p.o_row, p.o_head})
     if (!fits32(2 * x)) return false;
   const int64_t sq = s.seqlen_q + 256, sk = s.seqlen_k + 64;
   for (int64_t x : {256 * 2 * p.q_row, 256 * 2 * p.do_row, 256 * 2 * p.dq_row, sk * 2 * p.k_row})
@@ -224,8 +231,10 @@ void launch_bwd_dq_asm(const BwdParams& p, bool is_bf16, hipStream_t stream) {
   a.do_head = (int32_t)(2 * p.do_head); a.dq_head = (int32_t)(2 * p.dq_head);
   a.sq = s.seqlen_q; a.sk = s.seqlen_k; a.lse_pitch = s.lse_pitch; a.dsum_pitch = p.seqlen_q_rounded;
   a.h = s.h; a.hk = s.hk;
-  a.flags = s.varlen_padded_input ? 1 : 0;
+  a.flags = (s.varlen_padded_input ? 1 : 0) | (p.fuse_pre ? 2 : 0);
   a.c = s.scale_log2; a.scale = s.scale;
+  a.o = p.o; a.o_batch = 2 * p.o_batch; a.o_row = (int32_t)(2 * p.o_row); a.o_head = (int32_t)(2 * p.o_head);
+  a.lsed = p.lsed; a.lsed_ng = p.lsed_ng; a.nrscale = -1.0f / s.scale;
   a.dec = fwd_item_decode(s.b * s.h, s.h, s.h / s.hk, nmb, p.dq_head_group);
   a.n_items = (int32_t)nwg;
   a.grid = (int32_t)grid;

@@ -108,6 +108,7 @@ struct BwdParams {
   // [-LSE / scale x 32 | -D x 32] written by bwd_pre_kernel instead of lse_s; nullptr: HIP path
   float* lsed;
   int lsed_ng;
+  bool fuse_pre;          // (knob 8) the assembly dQ kernel writes D, softmax_d and lsed; dQ before dK/dV
 };
 
 // calc_reduced_attn_scores (fa_reduced.hip; reference reduced_scores::Params,
@@ -175,7 +176,9 @@ enum Knob { kKnobNoSplitKv = 0 /* FLASH_ATTN_MI355X_NO_SPLITKV: 1 = never split 
                                    dQ kernels */,
             kKnobAsmXcdGroupMinMiB = 7 /* FLASH_ATTN_MI355X_ASM_XCD_GROUP_MIN_MIB: knob 2's threshold
                                           for the persistent assembly forward / dQ (default 0) */,
-            kNumKnobs = 8 };
+            kKnobFusePre = 8 /* FLASH_ATTN_MI355X_FUSE_PRE: 1 = the assembly dQ kernel computes D and
+                                writes the dK/dV scratch itself (no bwd_pre_kernel); dQ runs first */,
+            kNumKnobs = 9 };
 int knob(int id);
 void set_knob(int id, int value);
 
