@@ -425,8 +425,10 @@ void flash_attn_timing_read(int kernel_id, double * total_ms, long * count);
  * (FLASH_ATTN_MI355X_FWD_PERSIST, default 1; 0 = one workgroup per item), 6 the same for the
  * assembly dK/dV and dQ kernels, fixed-length launches (FLASH_ATTN_MI355X_BWD_PERSIST, default 1), 7 knob 2's threshold
  * for the persistent assembly forward and dQ (FLASH_ATTN_MI355X_ASM_XCD_GROUP_MIN_MIB, default 0:
- * heads grouped per XCD whenever the shape allows).  Each is read from its environment variable
- * once, at first use. */
+ * heads grouped per XCD whenever the shape allows), 8 the backward preprocessing fused into the
+ * assembly dQ kernel (FLASH_ATTN_MI355X_FUSE_PRE, default 1: D = rowsum(dO o O), softmax_d and the
+ * dK/dV kernel's scratch are written by dQ, which then runs before dK/dV; 0 launches the separate
+ * preprocessing kernel).  Each is read from its environment variable once, at first use. */
 void flash_attn_set_knob(int id, int value);
 int flash_attn_get_knob(int id);
 /* 0 routes every forward to the HIP kernel, 1 (default) lets head dim 128 and 64 take the assembly

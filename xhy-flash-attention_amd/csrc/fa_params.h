@@ -176,8 +176,9 @@ enum Knob { kKnobNoSplitKv = 0 /* FLASH_ATTN_MI355X_NO_SPLITKV: 1 = never split 
                                    dQ kernels */,
             kKnobAsmXcdGroupMinMiB = 7 /* FLASH_ATTN_MI355X_ASM_XCD_GROUP_MIN_MIB: knob 2's threshold
                                           for the persistent assembly forward / dQ (default 0) */,
-            kKnobFusePre = 8 /* FLASH_ATTN_MI355X_FUSE_PRE: 1 = the assembly dQ kernel computes D and
-                                writes the dK/dV scratch itself (no bwd_pre_kernel); dQ runs first */,
+            kKnobFusePre = 8 /* FLASH_ATTN_MI355X_FUSE_PRE: 1 (default) = the assembly dQ kernel computes
+                                D and writes softmax_d and the dK/dV scratch itself (no bwd_pre_kernel);
+                                dQ runs first.  0 = bwd_pre_kernel, then dK/dV and dQ */,
             kNumKnobs = 9 };
 int knob(int id);
 void set_knob(int id, int value);
