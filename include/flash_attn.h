@@ -436,7 +436,8 @@ int flash_attn_get_knob(int id);
 void flash_attn_fwd_use_asm(int on);
 /* Backward dQ / dK-dV stream overlap: 0 (default) serial on the caller's stream, 1 dQ on a second
  * stream, 2 dQ on a lowest-priority stream, 3 dK/dV on a highest-priority stream
- * (FLASH_ATTN_MI355X_BWD_OVERLAP). */
+ * (FLASH_ATTN_MI355X_BWD_OVERLAP).  Launches whose dQ kernel computes D itself (knob 8) run dQ then
+ * dK/dV on the caller's stream whatever the mode: dK/dV reads what dQ writes. */
 void flash_attn_bwd_overlap(int mode);
 
 #ifdef __cplusplus
