@@ -12,6 +12,8 @@ Contents
                                   ``reorder_ops`` (scale k instead of q) for the PyTorch-error bound.
   * ``attention_lse_ref``      -- logsumexp of the scaled, masked scores (the ``softmax_lse``
                                   output, flash_fwd_kernel.h:509-518: +inf for an empty row).
+  * ``attention_lse_pt`` / ``check_lse_within_bound`` -- the LSE of the PyTorch-precision path and
+                                  the 2x rule applied to ``softmax_lse``.
   * ``flash_fwd_np`` / ``flash_bwd_np`` -- float64 numpy restatement of the kernel algebra:
         O = softmax(s QK^T) V, LSE = max*s + ln(sum)                (flash_fwd_kernel.h:509-518)
         P = exp(s QK^T - LSE)                                        (flash_bwd_kernel.h:847)
@@ -36,7 +38,7 @@ import numpy as np
 import torch
 
 __all__ = [
-    "attention_ref", "attention_lse_ref", "flash_fwd_np", "flash_bwd_np",
+    "attention_ref", "attention_lse_ref", "attention_lse_pt", "check_lse_within_bound", "flash_fwd_np", "flash_bwd_np",
     "generate_random_padding_mask", "generate_qkv", "check_within_bound", "max_abs_diff",
 ]
 
@@ -95,6 +97,39 @@ def attention_lse_ref(q, k, causal=False, softmax_scale=None, key_padding_mask=N
     lse = torch.logsumexp(scores, dim=-1)
     lse = torch.where(torch.isneginf(lse), torch.full_like(lse, float("inf")), lse)
     return lse.float()
+
+
+def attention_lse_pt(q, k, causal=False, key_padding_mask=None):
+    """The softmax_lse implied by the reference's PyTorch-precision path (``attention_ref`` with
+    upcast=False, reorder_ops=True: scores = einsum(q, k / sqrt(d)) in the input dtype,
+    tests/test_flash_attn.py:137-141), its logsumexp taken in fp32: the LSE side of the 2x rule."""
+    groups = q.shape[2] // k.shape[2]
+    k = _repeat_kv(k, groups)
+    scores = torch.einsum("bthd,bshd->bhts", q, k / math.sqrt(q.shape[-1])).float()
+    if key_padding_mask is not None:
+        scores.masked_fill_(~key_padding_mask[:, None, None, :], float("-inf"))
+    if causal:
+        sq, sk = q.shape[1], k.shape[1]
+        scores.masked_fill_(torch.triu(torch.ones(sq, sk, dtype=torch.bool, device=q.device), 1), float("-inf"))
+    lse = torch.logsumexp(scores, dim=-1)
+    return torch.where(torch.isneginf(lse), torch.full_like(lse, float("inf")), lse)
+
+
+def check_lse_within_bound(lse, ref, pt, atol=1e-3, rtol=1e-4, factor=2.0):
+    """softmax_lse acceptance: rows without a key must read +inf; elsewhere
+    |lse - ref| <= max(factor * max|pt - ref|, atol + rtol |ref|) -- the 2x rule of the outputs
+    (check_within_bound), never stricter than the plain atol / rtol check it replaces.
+    Returns (ok, max err, pt error)."""
+    lse, ref, pt = (x.detach().double().cpu() for x in (lse, ref, pt))
+    dead = torch.isinf(ref)
+    if dead.any() and not (torch.isinf(lse[dead]) & (lse[dead] > 0)).all():
+        return False, float("inf"), 0.0
+    live = ~dead
+    err = (lse[live] - ref[live]).abs()
+    pt_err = float((pt[live] - ref[live]).abs().max()) if live.any() else 0.0
+    bound = torch.clamp(atol + rtol * ref[live].abs(), min=factor * pt_err)
+    ok = bool((err <= bound).all()) if live.any() else True
+    return ok, float(err.max()) if live.any() else 0.0, pt_err
 
 
 # ------------------------------------------------------------------------------------------------

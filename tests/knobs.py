@@ -30,3 +30,16 @@ def knob(kid, value):
 
 def no_splitkv():
     return knob(NO_SPLITKV, 1)
+
+
+@contextlib.contextmanager
+def hip_forward():
+    """every forward through fwd_kernel (fa_fwd.hip) instead of the assembly kernels: a comparison
+    that needs the HIP kernel's arithmetic (fp32 scores; the assembly forward holds Q as
+    bf16/f16(scale log2(e) Q)) on both sides"""
+    import flash_attn_2_cuda as m
+    m._lib.flash_attn_fwd_use_asm(0)
+    try:
+        yield
+    finally:
+        m._lib.flash_attn_fwd_use_asm(1)

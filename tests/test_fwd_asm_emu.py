@@ -92,8 +92,22 @@ def test_asm_forward_refit_at_the_diagonal(asm_text):
         emu.run_wg(L, akarg)
     assert any("refit_a" in n for _, n in emu.trace) and any("refit_b" in n for _, n in emu.trace)
     o = f16_to_f32(heap.get(ao, s * d * 2).view(np.uint16)).reshape(1, s, 1, d)
-    o_ref, _ = emu_fwd.reference(qf, kf, vf, True, d ** -0.5)
-    assert np.abs(o - o_ref).max() < 2e-3
+    scale = d ** -0.5
+    o_ref, _ = emu_fwd.reference(qf, kf, vf, True, scale)
+    if os.environ.get("FA_GEN_FOLD", "1") == "1":
+        # the kernel's arithmetic (Q held as f16(c Q)) for the logic check; against the exact
+        # reference the scale fold's rounding counts under the 2x-pt rule (these scores reach ~400)
+        import torch
+        from oracle.attention_ref import attention_ref
+        c = np.float32(scale * 1.4426950408889634)
+        qc = f16_to_f32(f32_to_f16(qf.astype(np.float32) * c).astype(np.uint16)).astype(np.float64)
+        o_fold, _ = emu_fwd.reference(qc * (np.log(2.0) / scale), kf, vf, True, scale)
+        assert np.abs(o - o_fold).max() < 2e-3
+        t = [torch.from_numpy(x.astype(np.float16)) for x in (qf, kf, vf)]
+        o_pt = attention_ref(*t, causal=True, upcast=False, reorder_ops=True)[0].double().numpy()
+        assert np.abs(o - o_ref).max() <= 2 * np.abs(o_pt - o_ref).max()
+    else:
+        assert np.abs(o - o_ref).max() < 2e-3
 
 
 def test_generated_kernels_are_hazard_free():

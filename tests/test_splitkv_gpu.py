@@ -6,7 +6,7 @@ fp32-summation-order tolerance; the backward consumes the merged LSE unchanged."
 import pytest
 import torch
 
-from knobs import no_splitkv
+from knobs import hip_forward, no_splitkv
 from oracle.attention_ref import attention_ref, check_within_bound
 
 pytestmark = pytest.mark.gpu
@@ -40,7 +40,7 @@ def test_splitkv_forward(sq, sk, h, hk, d, dtype):
     kr = k.float().repeat_interleave(h // hk, dim=2)
     s = torch.einsum("bqhd,bkhd->bhqk", q.float(), kr) * d ** -0.5
     torch.testing.assert_close(lse, torch.logsumexp(s, -1), atol=1e-3, rtol=0)
-    with no_splitkv():
+    with no_splitkv(), hip_forward():   # the unsplit HIP kernel: the split's own arithmetic
         out1, _, _, _, _, lse1, _, _ = _flash_attn_forward(q, k, v, 0.0, d ** -0.5, False, False)
     torch.testing.assert_close(lse, lse1, atol=2e-5, rtol=0)
     tol = 2 ** -7 if dtype == torch.bfloat16 else 2 ** -10
@@ -76,7 +76,7 @@ def test_gqa_packing_without_split(d):
     pt, _ = attention_ref(q, k, v, upcast=False, reorder_ops=True)
     ok, err, bound = check_within_bound(out, ref, pt)
     assert ok, (err, bound)
-    with no_splitkv():
+    with no_splitkv(), hip_forward():
         out1, _, _, _, _, lse1, _, _ = _flash_attn_forward(q, k, v, 0.0, d ** -0.5, False, False)
     torch.testing.assert_close(lse, lse1, atol=2e-5, rtol=0)
     torch.testing.assert_close(out.float(), out1.float(), atol=2 ** -7, rtol=2 ** -7)

@@ -404,6 +404,8 @@ class Emu:
                 return (U(a[1]) >> U(a[2])) & ((np.uint32(1) << U(a[3])) - 1)
             if base == "v_cvt_f32_u32":
                 return f2u(U(a[1]).astype(np.float32))
+            if base == "v_cvt_f32_f16":
+                return f2u(f16_to_f32((U(a[1]) & 0xFFFF).astype(np.uint16)).astype(np.float32))
             if base in ("v_dot2_f32_bf16", "v_dot2_f32_f16"):
                 cv = bf16_to_f32 if base.endswith("bf16") else f16_to_f32
                 x, y = U(a[1]), U(a[2])

@@ -62,9 +62,12 @@ def reference(q, k, v, causal, scale, seqs_q=None, seqs_k=None):
 
 
 def run(b=1, sq=300, sk=300, h=2, hk=1, causal=True, bf16=True, seed=0, big=None, text=None, verbose=True,
-        grid=None, d=128, hp=0):
+        grid=None, d=128, hp=0, fold=None):
     """grid: workgroups of the persistent item loop (default: one per item); d: head dim (128, 64);
-    hp: heads per XCD group of the work order (0: head-fastest)"""
+    hp: heads per XCD group of the work order (0: head-fastest); fold: compare with the folded-scale
+    arithmetic (gen_fwd.py FA_GEN_FOLD, default as the generator's environment)"""
+    if fold is None:
+        fold = os.environ.get("FA_GEN_FOLD", "1") == "1"
     D = d
     rng = np.random.default_rng(seed)
     q = rng.standard_normal((b, sq, h, D)).astype(np.float32)
@@ -98,6 +101,11 @@ def run(b=1, sq=300, sk=300, h=2, hk=1, causal=True, bf16=True, seed=0, big=None
     o = dec(heap.get(ao, b * sq * h * D * 2).view(np.uint16)).reshape(b, sq, h, D).astype(np.float64)
     lse = heap.get(alse, b * h * sq * 4).view(np.float32).reshape(b, h, sq).astype(np.float64)
     o_ref, lse_ref = reference(qf, kf, vf, causal, scale)
+    if fold:
+        # the kernel's own arithmetic: Q held as bf16/f16(c Q), scores c S in the log2 domain
+        c = np.float32(scale * 1.4426950408889634)
+        qc = dec(enc(qf.astype(np.float32) * c).astype(np.uint16)).astype(np.float64)
+        o_ref, lse_ref = reference(qc * (np.log(2.0) / scale), kf, vf, causal, scale)
     eo = np.abs(o - o_ref).max()
     el = np.abs(lse - lse_ref).max()
     if verbose:

@@ -30,10 +30,14 @@ one-wave-per-SIMD" attention structure):
   * max-free online softmax: P = exp2(c S - c m_run) against the running max of the first tile; a
     tile whose per-lane partial row sum exceeds 2^8 (or is NaN) is recomputed with the true max
     ("refit", out of line, rare); the deferred-max rule of fa_fwd.hip.
+  * scale folded into Q (round 5, FA_GEN_FOLD): tile 0 rewrites the Q fragments as bf16/f16(c Q) and
+    every S chain starts from the constant tile -c m_run, so the MFMA hands over c S - c m_run and
+    P = exp2(acc) needs no v_fma (reference softmax.h:66-85 does scale * x - max_scaled per score).
   * tiles that need a mask (causal diagonal, ragged last tile) run a MASKED step variant that sets
     the masked scores to -inf before the exponent (per lane limit min(q, sk-1) - key base).
-  * work order comes from a host-built table (block -> batch, head, kv head, query block): heaviest
-    causal blocks first, heads fastest, as the HIP kernel's xcd_order_grouped.
+  * work order decoded in the kernel from the workgroup index and the round of the persistent loop
+    (fa_params.h ItemDecode, isa.item_decode_ops): heaviest causal blocks first, heads fastest or
+    grouped per XCD; varlen launches read a device-built list.
 """
 import os
 import sys
@@ -114,8 +118,17 @@ V_OOFF = (189, 190)
 V_ROW = (192, 193)                                       # row of the lane in the block, per q-block
 V_HH4 = 194                                              # 4 * (lane >> 5)
 V_TRI = 196   # 196..211: causal diagonal chain start (-inf where key > query in a 32 x 32 S^T subtile)
-V_NT = 212    # 212..227: all -inf chain start (a subtile wholly above the diagonal)
+V_NT = 212    # 212..227: all -inf chain start (a subtile wholly above the diagonal; not with the fold)
 NVGPR = 228
+# scale folded into Q (round 5 default; FA_GEN_FOLD=0 restores the per-score v_fma): the Q fragments
+# hold bf16/f16(c Q) with c = scale * log2(e), every S chain starts from the constant tile -c m_run of
+# its q-block (V_M[j], 16 registers of V_NEGMC[j]), so a score leaves the MFMA as c S - c m_run and
+# P = v_exp_f32(acc) -- one VALU op per score instead of two.  Scores wholly above the causal
+# diagonal are written as -inf (no chain), so the all -inf tile V_NT gives its registers to V_M.
+OPT_FOLD = os.environ.get("FA_GEN_FOLD", "1") == "1"
+V_M = (212, 228)      # 212..227, 228..243
+if OPT_FOLD:
+    NVGPR = 244
 
 # ---- SGPRs ----
 S_KD, S_VD, S_QD, S_OD, S_LD = 4, 8, 12, 16, 20          # buffer descriptors
@@ -209,15 +222,18 @@ OPT_EPISTAMP = os.environ.get("FA_GEN_STAMP") == "3"
 # FA_GEN_STAMP=4: the item start split -- geometry (epilogue end -> tile 0's wait) in the item-start
 # slot, tile 0's vmcnt wait in the tile-0 slot, its barrier wait in V_SSUM + 5 (record offset 96)
 OPT_T0STAMP = os.environ.get("FA_GEN_STAMP") == "4"
-V_SSUM = 240      # 240..244: compute, wait, barrier sums, step count, last stamp;
-                  # 246..249: item phases: tile 0, last step, epilogue, item start (geometry .. tile 0's barrier)
+V_SSUM = 174 if OPT_FOLD else 240   # +0..4: compute, wait, barrier sums, step count, last stamp;
+                  # +6..9: item phases: tile 0, last step, epilogue, item start (geometry .. tile 0's barrier)
 # latency-aware gap scheduling (isa.schedule lat=): "valu,trans,lds,mfma" result latencies in cycles
 _lat = os.environ.get("FA_GEN_LAT")
 OPT_LAT = None
 if _lat:
     _v = [int(x) for x in _lat.split(",")]
     OPT_LAT = {VALU: _v[0], PERM: _v[0], TRANS: _v[1], LDS: _v[2], MFMA: _v[3]}
-V_STAMP = 232     # 232..237: start memtime lo / hi, realtime lo / hi, tiles, items
+V_STAMP = 244 if OPT_FOLD else 232     # +0..5: start memtime lo / hi, realtime lo / hi, tiles, items
+# dev options whose registers the fold's V_M tiles take, or that predate it
+assert not (OPT_FOLD and (OPT_DEFER or OPT_MFZERO or OPT_T0OV or OPT_LAST2)), \
+    "FA_GEN_DEFER / MFZERO / T0OV / LAST2 need FA_GEN_FOLD=0"
 # debug: at the named point, workgroup 0 stores every register of each wave (and wave 0 the LDS) to
 # the buffer whose address is passed as the `seed` kernarg, then ends (tools/asm_dump.py)
 OPT_DUMP = os.environ.get("FA_GEN_DUMP")
@@ -254,7 +270,8 @@ class K:
     # ------------------------------------------------------------------ instruction builders
     def mfma_s(self, st_reg, kslot, j, ks, first, bias=None):
         """S^T chain step; the first step starts from 0 or from a bias tile (bias: VGPR base of a
-        16-register -inf / 0 mask tile: the causal mask folded into the chain start)"""
+        16-register chain start: a -inf / 0 mask tile, the causal mask folded into the chain start,
+        and / or, with the fold, the -c m_run tile of the q-block)"""
         if first:
             c = "0" if bias is None else rtxt("v", bias, 16)
             rc = [] if bias is None else vr(bias, 16)
@@ -311,10 +328,12 @@ class K:
                             rd=vr(reg) + vr(V_NINF) + [("vcc", 0)], wr=vr(reg), key=key0 + 4 * e))
         return ops
 
-    def softmax_ops(self, j, sreg, preg, masked, kbase_sgpr_add, key0, lm=None):
+    def softmax_ops(self, j, sreg, preg, masked, kbase_sgpr_add, key0, lm=None, fold_add=False):
         """ops of P = exp2(c S - c m) for q-block j on the 32 scores at v[sreg..+31] -> packed P at
-        v[preg..+15]; partial row sum into V_PS[j] (masked: mask_ops first).  Dependencies among the
-        ops are derived from their registers by isa.schedule.  Returns (ops, last sum op)."""
+        v[preg..+15]; partial row sum into V_PS[j] (masked: mask_ops first).  With the fold the
+        scores already are c S - c m (chain start V_M[j]): P = exp2(score); fold_add: scores c S from
+        a chain started at 0 (tile 0, refit), - c m added first.  Dependencies among the ops are
+        derived from their registers by isa.schedule.  Returns (ops, last sum op)."""
         ops = self.mask_ops(j, sreg, kbase_sgpr_add, lm or V_LM, key0) if masked else []
         k = key0
         last_sum = None
@@ -322,8 +341,12 @@ class K:
             st, g = e // 16, e % 16
             reg = sreg + e
             kk = 4 * e
-            ops.append(Inst(f"v_fma_f32 v{reg}, v{reg}, s{S_C}, v{V_NEGMC[j]}", VALU, rd=vr(reg) + sr(S_C) + vr(V_NEGMC[j]),
-                            wr=vr(reg), key=k + kk + 1))
+            if not OPT_FOLD:
+                ops.append(Inst(f"v_fma_f32 v{reg}, v{reg}, s{S_C}, v{V_NEGMC[j]}", VALU,
+                                rd=vr(reg) + sr(S_C) + vr(V_NEGMC[j]), wr=vr(reg), key=k + kk + 1))
+            elif fold_add:
+                ops.append(Inst(f"v_add_f32_e32 v{reg}, v{V_NEGMC[j]}, v{reg}", VALU, rd=vr(reg) + vr(V_NEGMC[j]),
+                                wr=vr(reg), key=k + kk + 1))
             ops.append(Inst(f"v_exp_f32_e32 v{reg}, v{reg}", TRANS, rd=vr(reg), wr=vr(reg), key=k + kk + 2))
             if e == 1:    # (p1 + p0: the first two terms in one add, no copy of p0)
                 a = Inst(f"v_add_f32_e32 v{V_PS[j]}, v{reg}, v{reg - 1}", VALU, rd=vr(reg) + vr(reg - 1),
@@ -423,7 +446,18 @@ class K:
         if last and OPT_LAST2:
             return self.step_last2(p, tag)
 
+        # fold: the triangle's chain start V_TRI + (-c m) is built per diagonal step in PA(p ^ 1), which
+        # is idle during phase X (P(n-1, a) was read by the previous step's PV, P(n+1, a) is written
+        # in phase Y): q-block a's before MFMA 0, then q-block b's once MFMA 0 has read it
+        tri = PA(p ^ 1)
+
         def bias(j, st):
+            if OPT_FOLD:
+                if variant == "diag" and j < st:
+                    return None          # chain from 0, overwritten by -inf in phase Y
+                if variant == "diag" and j == st:
+                    return tri
+                return V_M[j]
             if variant == "dead":
                 return V_NT
             if variant == "diag":
@@ -432,20 +466,34 @@ class K:
         refits = []
         # ---------------- phase X
         mx = []
-        if not last:
+        fold_dead = OPT_FOLD and variant == "dead"
+        if not last and not fold_dead:
             for i in range(NX):
                 st, ks, j = i // (2 * KS), (i % (2 * KS)) // 2, i % 2
                 f = st * KS + ks
                 sreg = (SA if j == 0 else SB(p ^ 1)) + 16 * st
                 mx.append(self.mfma_s(sreg, f % 8, j, ks, ks == 0, bias=bias(j, st)))
         fx = []
+        if OPT_FOLD and variant == "diag":
+            i_b = 2 * KS + 1              # first MFMA of q-block b's triangle chain (st 1, ks 0)
+            for j, (eg, dl) in enumerate(((None, 0), (1, i_b))):
+                for g in range(16):
+                    fx.append(Inst(f"v_add_f32_e32 v{tri + g}, v{V_NEGMC[j]}, v{V_TRI + g}", VALU,
+                                   rd=vr(V_NEGMC[j]) + vr(V_TRI + g), wr=vr(tri + g), key=-300 + 20 * j + g,
+                                   earliest=eg, deadline=dl))
+        if fold_dead:
+            # the whole tile n+1 lies above this wave's diagonal: S(n+1) = -inf, no QK
+            for base in (SA, SB(p ^ 1)):
+                for e in range(32):
+                    fx.append(Inst(f"v_mov_b32_e32 v{base + e}, v{V_NINF}", VALU, rd=vr(V_NINF), wr=vr(base + e),
+                                   key=50 + e))
         # V base of tile n (slot offset S_VOFF, already advanced at the end of the previous step)
         fx.append(Inst(f"v_add_u32_e32 v{V_VB0}, s{S_VOFF}, v{V_TB0}", VALU, rd=sr(S_VOFF) + vr(V_TB0), wr=vr(V_VB0), key=0))
         fx.append(Inst(f"v_add_u32_e32 v{V_VB1}, s{S_VOFF}, v{V_TB1}", VALU, rd=sr(S_VOFF) + vr(V_TB1), wr=vr(V_VB1), key=0))
         vb = fx[-2:]
         if not last:
             # K fragments 3..15 (0..2 were prefetched at the end of the previous step)
-            for f in range(3, 2 * KS):
+            for f in range(3, 2 * KS) if not fold_dead else ():
                 eg = max(2 * (f - 3), 2 * (f - 8) + 3)
                 fx.append(self.kread(f, f % 8, key=-100 + f, earliest=eg, deadline=2 * f - 1))
             # K DMA of tile n+4 (4 pieces)
@@ -475,7 +523,10 @@ class K:
             my.append(self.mfma_o(j, dt, f % 8, preg))
         fy = []
         rl_b = self.lab(f"{tag}_refit_b")
-        refits.append(self.refit(1, SB(p), PB, rl_b, tile_add=0, phase="Y"))
+        # (fold) a refit of q-block b moves its -c m: S(n+1, b), made in phase X from the old
+        # chain start, moves with it
+        refits.append(self.refit(1, SB(p), PB, rl_b, tile_add=0, phase="Y",
+                                 nxt=SB(p ^ 1) if (OPT_FOLD and not last) else None))
         if OPT_GUARD2:
             fy += self.guard_br(1, rl_b, key=-200, deadline=4)
         else:
@@ -488,6 +539,10 @@ class K:
             for h in range(2):
                 fy.append(self.vread(f, f % 8, h, key=-150 + 2 * f + h, earliest=eg, deadline=dl))
         t = S_TMP
+        if OPT_FOLD and variant == "diag":
+            # q-block a's key subtile 1 lies above this wave's diagonal: -inf (its chain ran from 0)
+            for e in range(16, 32):
+                fy.append(Inst(f"v_mov_b32_e32 v{SA + e}, v{V_NINF}", VALU, rd=vr(V_NINF), wr=vr(SA + e), key=-10))
         if not last:
             # softmax (n+1, a)
             sm_a, sum_a = self.softmax_ops(0, SA, PA(p ^ 1), masked, (S_N0, 64), key0=0)
@@ -631,12 +686,15 @@ class K:
         return ins
 
     # ------------------------------------------------------------------ refit (rare, out of line)
-    def refit(self, j, sreg, preg, lab, tile_add, phase):
+    def refit(self, j, sreg, preg, lab, tile_add, phase, nxt=None):
         """Out-of-line slow path (rare): recompute S of q-block j for its tile from the K slot that
         still holds it, mask it, take the true row max, rescale O_j / l_j to it and redo P and the
         partial sum.  phase 'Y' (tile n, checked before its first PV MFMA): S_KOFF still addresses
         tile n+1; phase 'end' (tile n+1, checked at the end of phase Y): S_KOFF was advanced to tile
-        n+2.  Either way the tile's K slot is S_KOFF - TILE (mod the ring)."""
+        n+2.  Either way the tile's K slot is S_KOFF - TILE (mod the ring).  With the fold the
+        recomputed scores are c S (chain from 0; Q holds c Q), the new -c m also goes into the
+        chain-start tile V_M[j], and nxt (the q-block's next S tile, already computed from the old
+        chain start) is moved by the change of -c m."""
         ins = [label(lab), nop(15), Inst("s_waitcnt lgkmcnt(0)", WAIT)]
         t = V_T
         s0 = S_TMP + 3
@@ -674,26 +732,60 @@ class K:
             else:
                 ins.append(Inst(f"v_max_f32_e32 v{mx}, v{mx}, v{sreg + e}", VALU, rd=vr(mx) + vr(sreg + e), wr=vr(mx)))
         ins += self.half_max(mx, t + 3)
-        # mnc = max(mc_old, mt * c); alpha = exp2(mc_old - mnc)
-        ins += [Inst(f"v_mul_f32_e32 v{mx}, s{S_C}, v{mx}", VALU, rd=sr(S_C) + vr(mx), wr=vr(mx)),
-                Inst(f"v_max_f32_e64 v{mx}, -v{V_NEGMC[j]}, v{mx}", VALU, rd=vr(V_NEGMC[j]) + vr(mx), wr=vr(mx)),
-                Inst(f"v_add_f32_e32 v{t + 3}, v{V_NEGMC[j]}, v{mx}", VALU, rd=vr(V_NEGMC[j]) + vr(mx), wr=vr(t + 3)),
-                Inst(f"v_exp_f32_e64 v{t + 3}, -v{t + 3}", TRANS, rd=vr(t + 3), wr=vr(t + 3)),
+        # mnc = max(mc_old, mt * c); alpha = exp2(mc_old - mnc)   (fold: the scores are c S already)
+        if not OPT_FOLD:
+            ins += [Inst(f"v_mul_f32_e32 v{mx}, s{S_C}, v{mx}", VALU, rd=sr(S_C) + vr(mx), wr=vr(mx))]
+        ins += [Inst(f"v_max_f32_e64 v{mx}, -v{V_NEGMC[j]}, v{mx}", VALU, rd=vr(V_NEGMC[j]) + vr(mx), wr=vr(mx)),
+                Inst(f"v_add_f32_e32 v{t + 3}, v{V_NEGMC[j]}, v{mx}", VALU, rd=vr(V_NEGMC[j]) + vr(mx), wr=vr(t + 3))]
+        if nxt is not None:
+            # next tile: c S + (-c m_old) -> c S + (-c m_new) = score - (mc_new - mc_old)
+            ins += [Inst(f"v_sub_f32_e32 v{nxt + e}, v{nxt + e}, v{t + 3}", VALU, rd=vr(nxt + e) + vr(t + 3),
+                         wr=vr(nxt + e)) for e in range(32)]
+        ins += [Inst(f"v_exp_f32_e64 v{t + 3}, -v{t + 3}", TRANS, rd=vr(t + 3), wr=vr(t + 3)),
                 Inst(f"v_sub_f32_e32 v{V_NEGMC[j]}, 0, v{mx}", VALU, rd=vr(mx), wr=vr(V_NEGMC[j])),
                 Inst(f"v_mul_f32_e32 v{V_L[j]}, v{V_L[j]}, v{t + 3}", VALU, rd=vr(V_L[j]) + vr(t + 3), wr=vr(V_L[j]))]
+        if OPT_FOLD:
+            ins += self.m_tile_ops(j)
         for dt in range(NP):
             for g in range(16):
                 a = O_(j, dt) + g
                 ins += [Inst(f"v_accvgpr_read_b32 v{t + 4}, a{a}", ACCR, rd=ar(a), wr=vr(t + 4)),
                         Inst(f"v_mul_f32_e32 v{t + 4}, v{t + 4}, v{t + 3}", VALU, rd=vr(t + 4, 1) + vr(t + 3), wr=vr(t + 4)),
                         Inst(f"v_accvgpr_write_b32 a{a}, v{t + 4}", ACCW, rd=vr(t + 4), wr=ar(a))]
-        sm, _ = self.softmax_ops(j, sreg, preg, False, None, key0=0)
+        sm, _ = self.softmax_ops(j, sreg, preg, False, None, key0=0, fold_add=OPT_FOLD)
         ins += sm
         ins.append(nop(7))
         ins.append(Inst(f"s_branch {lab}_back", BRANCH))
         out, _ = add_waits(ins)
         out, _ = fix_hazards(out)
         return out
+
+    def m_tile_ops(self, j, key=0):
+        """(fold) the chain-start tile of q-block j: 16 copies of its -c m"""
+        return [Inst(f"v_mov_b32_e32 v{V_M[j] + g}, v{V_NEGMC[j]}", VALU, rd=vr(V_NEGMC[j]), wr=vr(V_M[j] + g), key=key)
+                for g in range(16)]
+
+    def q_scale_ops(self):
+        """(fold) Q fragments (AGPRs, as loaded) -> bf16/f16(c Q), RNE, via v0..95 (free at tile 0)"""
+        I = Inst
+        ops = []
+        n = 4 * KS
+        X, LO, HI = 0, 32, 64
+        for j in range(2):
+            q0 = Q_(j, 0)
+            ops += [I(f"v_accvgpr_read_b32 v{X + i}, a{q0 + i}", ACCR, rd=ar(q0 + i), wr=vr(X + i)) for i in range(n)]
+            if self.bf16:
+                ops += [I(f"v_lshlrev_b32_e32 v{LO + i}, 16, v{X + i}", VALU, rd=vr(X + i), wr=vr(LO + i)) for i in range(n)]
+                ops += [I(f"v_and_b32_e32 v{HI + i}, 0xffff0000, v{X + i}", VALU, rd=vr(X + i), wr=vr(HI + i)) for i in range(n)]
+            else:
+                ops += [I(f"v_cvt_f32_f16_e32 v{LO + i}, v{X + i}", VALU, rd=vr(X + i), wr=vr(LO + i)) for i in range(n)]
+                ops += [I(f"v_lshrrev_b32_e32 v{HI + i}, 16, v{X + i}", VALU, rd=vr(X + i), wr=vr(HI + i)) for i in range(n)]
+                ops += [I(f"v_cvt_f32_f16_e32 v{HI + i}, v{HI + i}", VALU, rd=vr(HI + i), wr=vr(HI + i)) for i in range(n)]
+            for R in (LO, HI):
+                ops += [I(f"v_mul_f32_e32 v{R + i}, s{S_C}, v{R + i}", VALU, rd=sr(S_C) + vr(R + i), wr=vr(R + i)) for i in range(n)]
+            ops += [self.cvt(X + i, LO + i, HI + i) for i in range(n)]
+            ops += [I(f"v_accvgpr_write_b32 a{q0 + i}, v{X + i}", ACCW, rd=vr(X + i), wr=ar(q0 + i)) for i in range(n)]
+        return ops
 
     def dump(self, point):
         """register / LDS dump of workgroup 0 at `point` (OPT_DUMP), then s_endpgm"""
@@ -875,8 +967,9 @@ class K:
                 ins += [I(f"v_add_u32_e32 v4, {kr}, v{V_HH4}", VALU, rd=vr(V_HH4), wr=vr(4)),
                         I("v_cmp_gt_u32_e32 vcc, v4, v2", VALU, rd=vr(4) + vr(2), wr=[("vcc", 0)]),
                         I(f"v_cndmask_b32_e64 v{V_TRI + g}, 0, v{V_NINF}, vcc", VALU,
-                          rd=vr(V_NINF) + [("vcc", 0)], wr=vr(V_TRI + g)),
-                        I(f"v_mov_b32_e32 v{V_NT + g}, v{V_NINF}", VALU, rd=vr(V_NINF), wr=vr(V_NT + g))]
+                          rd=vr(V_NINF) + [("vcc", 0)], wr=vr(V_TRI + g))]
+                if not OPT_FOLD:
+                    ins += [I(f"v_mov_b32_e32 v{V_NT + g}, v{V_NINF}", VALU, rd=vr(V_NINF), wr=vr(V_NT + g))]
         ins += [I(f"s_lshl_b32 s{S_TB}, s{Rkv}, 6", SALU, rd=sr(Rkv), wr=sr(S_TB)),
                 I(f"s_mov_b32 s{S_ROUND}, 0", SALU, wr=sr(S_ROUND)),
                 I(f"s_mov_b32 s{S_WARM}, 0", SALU, wr=sr(S_WARM)),
@@ -1181,6 +1274,8 @@ class K:
             ins = [I(f"s_waitcnt vmcnt({2 * NP})", WAIT), I("s_barrier", BARRIER)]
             ins += [] if OPT_EPISTAMP else self.stamp_point(9)
         ins += self.dump("pro_lds")
+        if OPT_FOLD:
+            ins += self.q_scale_ops()
         ins += [I(f"v_add_u32_e32 v{V_KB0}, s{S_KOFF}, v{V_RB0}", VALU, rd=sr(S_KOFF) + vr(V_RB0), wr=vr(V_KB0)),
                 I(f"v_add_u32_e32 v{V_KB1}, s{S_KOFF}, v{V_RB1}", VALU, rd=sr(S_KOFF) + vr(V_RB1), wr=vr(V_KB1))]
         mfm = []
@@ -1215,14 +1310,23 @@ class K:
                 else:
                     ins.append(Inst(f"v_max_f32_e32 v{mx}, v{mx}, v{sreg + e}", VALU, rd=vr(mx) + vr(sreg + e), wr=vr(mx)))
             ins += self.half_max(mx, V_T + 3)
-            # negmc = m == -inf ? 0 : -m c
-            ins += [Inst(f"v_mul_f32_e32 v{V_T + 4}, s{S_C}, v{mx}", VALU, rd=sr(S_C) + vr(mx), wr=vr(V_T + 4)),
-                    Inst(f"v_sub_f32_e32 v{V_NEGMC[j]}, 0, v{V_T + 4}", VALU, rd=vr(V_T + 4), wr=vr(V_NEGMC[j])),
-                    Inst(f"v_cmp_eq_f32_e32 vcc, v{V_NINF}, v{mx}", VALU, rd=vr(V_NINF) + vr(mx), wr=[("vcc", 0)]),
+            # negmc = m == -inf ? 0 : -m c   (fold: the scores are c S already)
+            if OPT_FOLD:
+                ins += [Inst(f"v_sub_f32_e32 v{V_NEGMC[j]}, 0, v{mx}", VALU, rd=vr(mx), wr=vr(V_NEGMC[j]))]
+            else:
+                ins += [Inst(f"v_mul_f32_e32 v{V_T + 4}, s{S_C}, v{mx}", VALU, rd=sr(S_C) + vr(mx), wr=vr(V_T + 4)),
+                        Inst(f"v_sub_f32_e32 v{V_NEGMC[j]}, 0, v{V_T + 4}", VALU, rd=vr(V_T + 4), wr=vr(V_NEGMC[j]))]
+            ins += [Inst(f"v_cmp_eq_f32_e32 vcc, v{V_NINF}, v{mx}", VALU, rd=vr(V_NINF) + vr(mx), wr=[("vcc", 0)]),
                     Inst(f"v_cndmask_b32_e64 v{V_NEGMC[j]}, v{V_NEGMC[j]}, 0, vcc", VALU,
                          rd=vr(V_NEGMC[j]) + [("vcc", 0)], wr=vr(V_NEGMC[j]))]
+        if OPT_FOLD:
+            # S(0, b) -> c S - c m (its softmax runs in the first step, which takes the scores as
+            # they leave a V_M-started chain); the chain-start tiles of both q-blocks
+            ins += [Inst(f"v_add_f32_e32 v{SB(0) + e}, v{V_NEGMC[1]}, v{SB(0) + e}", VALU,
+                         rd=vr(V_NEGMC[1]) + vr(SB(0) + e), wr=vr(SB(0) + e)) for e in range(32)]
+            ins += self.m_tile_ops(0) + self.m_tile_ops(1)
         if not OPT_T0OV:
-            sm, _ = self.softmax_ops(0, SA, PA(0), False, None, key0=0)
+            sm, _ = self.softmax_ops(0, SA, PA(0), False, None, key0=0, fold_add=OPT_FOLD)
             ins += sm
             ins += [Inst(f"v_mov_b32_e32 v{V_L[0]}, v{V_PS[0]}", VALU, rd=vr(V_PS[0]), wr=vr(V_L[0]))]
         ins += self.dump("pro_end")

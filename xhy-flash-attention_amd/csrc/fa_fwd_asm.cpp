@@ -17,6 +17,7 @@
 // (varlen_items_kernel, below).
 #include <hip/hip_runtime.h>
 
+#include <cmath>
 #include <cstdint>
 #include <cstdlib>
 #include <cstddef>
@@ -182,6 +183,9 @@ bool launch_fwd_asm(const FwdParams& p, bool is_bf16, hipStream_t stream) {
       p.n_split != 0 || p.pack_g != 1)
     return false;
   if (p.k_row != p.v_row) return false;   // the K and V DMA share per-lane offsets
+  // The kernel holds Q as f16/bf16(c Q), c = scale * log2(e) (gen_fwd.py FA_GEN_FOLD): with fp16 and
+  // c > 1 a finite Q could overflow there, so such calls take the HIP kernel (fp32 scores).
+  if (!is_bf16 && !(std::fabs(s.scale_log2) <= 1.0f)) return false;
   if (s.b > 65535 || s.h > 65535 || p.num_m_blocks > 65535 || s.h % s.hk != 0) return false;
   const int64_t q_row = 2 * p.q_row, kv_row = 2 * p.k_row, o_row = 2 * p.o_row;
   const int64_t q_head = 2 * p.q_head, k_head = 2 * p.k_head, v_head = 2 * p.v_head, o_head = 2 * p.o_head;
