@@ -43,6 +43,19 @@ def test_asm_dkdv_in_emulator(asm_text, b, sq, sk, h, hk, causal, bf16, reduce):
 
 
 @pytest.mark.timeout(900)
+@pytest.mark.parametrize("b,sq,sk,h,hk,causal,bf16,reduce", [
+    (1, 300, 300, 1, 1, True, True, False),     # masked -> fast, ragged both
+    (1, 257, 129, 2, 1, False, False, True),    # fp16, full attention, GQA reduce
+])
+def test_asm_dkdv_unit_c_in_emulator(asm_text, b, sq, sk, h, hk, causal, bf16, reduce):
+    """the _c1 kernels (c = 1: P = exp2(S') with no multiply; launch_bwd's backward on Q')"""
+    ek, ev, *_ = emu_bwd.run(b, sq, sk, h, hk, causal, bf16, reduce, seed=5, text=asm_text, verbose=False,
+                             unit_c=True)
+    tol = 1e-2 if bf16 else 2e-3
+    assert ek <= tol and ev <= tol, (ek, ev)
+
+
+@pytest.mark.timeout(900)
 @pytest.mark.parametrize("b,sq,sk,h,hk,causal,reduce,grid", [
     (1, 200, 300, 2, 1, True, True, 1),      # one workgroup walks all 3 key blocks (+ causal skips)
     (2, 150, 130, 4, 2, False, False, 3),    # 16 items over 3 workgroups, snake rounds
@@ -61,7 +74,7 @@ def test_generated_dkdv_kernels_are_hazard_free():
     spec.loader.exec_module(isa)
     text = subprocess.run([sys.executable, os.path.join(ROOT, "xhy-flash-attention_amd", "csrc", "asm", "gen_bwd.py")],
                           check=True, capture_output=True, text=True).stdout
-    assert text.count(".amdhsa_kernel ") == 4
+    assert text.count(".amdhsa_kernel ") == 8
     assert ".amdhsa_group_segment_fixed_size 151552" in text
     lines = [x.strip() for x in text.splitlines()]
     for i, x in enumerate(lines):

@@ -193,7 +193,7 @@ def test_shipped_assembly_kernels_hazard_free():
     res = hc.check_library(LIB)
     names = sorted(res)
     assert len([n for n in names if n.startswith("fa_fwd_asm_")]) == 8, names
-    assert len([n for n in names if n.startswith("fa_bwd_dkdv_asm_")]) == 4, names
+    assert len([n for n in names if n.startswith("fa_bwd_dkdv_asm_")]) == 8, names   # (+ the c = 1 kernels)
     assert len([n for n in names if n.startswith("fa_bwd_dq_asm_")]) == 4, names
     for n, (count, bad) in res.items():
         assert count > 1000, (n, count)

@@ -1,7 +1,8 @@
 #!/bin/bash
 # Build a library variant whose assembly kernels (forward and dK/dV) are generated with dev switches
 # (A/B):   FA_GEN_X=1 FA_GBW_Y=2 ... tools/asm_variant.sh NAME  ->  variants/libfa_NAME.so
-# Every other object comes from the in-tree build (csrc/build).
+# Every other object comes from the in-tree build (csrc/build), except the CXX_FILES (e.g.
+# "fa_fwd.hip"), recompiled with CXX_FLAGS (e.g. -DFA_NO_QFOLD) when given.
 set -e
 NAME=$1
 ROOT=$(cd "$(dirname "$0")/.." && pwd)
@@ -18,9 +19,14 @@ for k in fwd bwd dq; do
   /opt/rocm/bin/hipcc -O3 -std=c++17 -fPIC --offload-arch=gfx950 -x hip -c "$W/blob_$k.cpp" -o "$W/blob_$k.o"
 done
 OBJS=""
+for f in $CXX_FILES; do
+  /opt/rocm/bin/hipcc -O3 -std=c++17 -fPIC --offload-arch=gfx950 -fno-slp-vectorize $CXX_FLAGS -x hip -c "$CS/$f" -o "$W/$f.o"
+  OBJS="$OBJS $W/$f.o"
+done
 for o in $CS/build/*.o; do
   b=$(basename $o .o)
   case $b in fa_fwd_asm|fa_fwd_asm_blob.cpp|fa_bwd_asm|fa_bwd_asm_blob.cpp|fa_dq_asm|fa_dq_asm_blob.cpp) continue;; esac
+  case " $CXX_FILES " in *" $b "*) continue;; esac
   OBJS="$OBJS $o"
 done
 /opt/rocm/bin/hipcc -shared --offload-arch=gfx950 -o "$ROOT/variants/libfa_$NAME.so" $OBJS "$W/blob_fwd.o" "$W/blob_bwd.o" "$W/blob_dq.o"

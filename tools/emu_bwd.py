@@ -73,8 +73,9 @@ def reference(q, k, v, do, causal, scale):
 
 
 def run(b=1, sq=200, sk=200, h=2, hk=1, causal=True, bf16=True, reduce=True, seed=0, text=None, verbose=True,
-        grid=None):
-    """grid: workgroups of the persistent item loop (default: one per item)"""
+        grid=None, unit_c=False):
+    """grid: workgroups of the persistent item loop (default: one per item); unit_c: the _c1 kernel
+    (c = 1: scale = ln 2, the launch of a backward on the prescaled Q')"""
     rng = np.random.default_rng(seed)
     q = rng.standard_normal((b, sq, h, D)).astype(np.float32)
     k = rng.standard_normal((b, sk, hk, D)).astype(np.float32)
@@ -83,7 +84,7 @@ def run(b=1, sq=200, sk=200, h=2, hk=1, causal=True, bf16=True, reduce=True, see
     enc, dec = (f32_to_bf16, bf16_to_f32) if bf16 else (f32_to_f16, f16_to_f32)
     q16, k16, v16, do16 = (enc(x).astype(np.uint16) for x in (q, k, v, do))
     qf, kf, vf, dof = (dec(x).astype(np.float64) for x in (q16, k16, v16, do16))
-    scale = D ** -0.5
+    scale = np.log(2.0) if unit_c else D ** -0.5
     lse, dsum, dk_ref, dv_ref = reference(qf, kf, vf, dof, causal, scale)
     g = h // hk
     if reduce and g > 1:
@@ -115,10 +116,10 @@ def run(b=1, sq=200, sk=200, h=2, hk=1, causal=True, bf16=True, reduce=True, see
               q_row=h * D * 2, k_row=hk * D * 2, v_row=hk * D * 2, do_row=h * D * 2, dk_row=nh_out * D * 2,
               dv_row=nh_out * D * 2, q_head=D * 2, k_head=D * 2, v_head=D * 2, do_head=D * 2, dk_head=D * 2,
               dv_head=D * 2, sq=sq, sk=sk, h=h, ng=ng, nh=g if red else 1, group=g,
-              c=float(np.float32(scale * 1.4426950408889634)), scale=float(np.float32(scale)), flags=2 if red else 0)
+              c=1.0 if unit_c else float(np.float32(scale * 1.4426950408889634)), scale=float(np.float32(scale)), flags=2 if red else 0)
     akarg = heap.put(np.frombuffer(pack_args(**kw), dtype=np.uint8))
     text = text or asm_text()
-    name = f"fa_bwd_dkdv_asm_d128_{'bf16' if bf16 else 'f16'}_{'causal' if causal else 'full'}"
+    name = f"fa_bwd_dkdv_asm_d128_{'bf16' if bf16 else 'f16'}_{'causal' if causal else 'full'}{'_c1' if unit_c else ''}"
     emu = Emu(text, name, heap)
     for L in range(grid or n_items):
         emu.run_wg(L, akarg)

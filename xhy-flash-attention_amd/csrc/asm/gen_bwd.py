@@ -8,7 +8,8 @@ Algorithm: the reference's dK / dV half of compute_dq_dk_dv_1colblock
 (csrc/flash_attn/src/flash_bwd_kernel.h:421-1046) for one block of keys, swept over every query row
 that can see them (and, for GQA with a reduced dK / dV, over every query head of the group):
     S' = Q K^T - LSE / scale          (chain started from -LSE / scale)
-    P  = exp2(c S')                   (c = scale log2 e; -inf where the causal mask hides the key)
+    P  = exp2(c S')                   (c = scale log2 e; -inf where the causal mask hides the key;
+                                       the _c1 kernels: c = 1, Q = the forward's bf16/f16(c Q))
     dP' = dO V^T - D                  (chain started from -D, D = rowsum(dO o O))
     dS = P o dP'
     dV^T += dO^T P,   dK^T += Q^T dS  (dK = scale dK^T^T at the end)
@@ -166,11 +167,14 @@ V_STAMP = 164          # 164..177: start lo / hi, HW_ID, XCC_ID, wg, end lo / hi
 class K:
     """one kernel variant"""
 
-    def __init__(self, bf16, causal):
+    def __init__(self, bf16, causal, unit_c=False):
         self.bf16 = bf16
         self.causal = causal
+        # unit_c: the launch passes c = 1 (the backward of a forward that held Q as bf16/f16(c Q): the
+        # Q rows are the prescaled Q', launch_bwd), so P = exp2(S') with no multiply per score
+        self.unit_c = unit_c
         self.ty = "bf16" if bf16 else "f16"
-        self.name = f"fa_bwd_dkdv_asm_d{D}_{self.ty}_{'causal' if causal else 'full'}"
+        self.name = f"fa_bwd_dkdv_asm_d{D}_{self.ty}_{'causal' if causal else 'full'}{'_c1' if unit_c else ''}"
         self.uid = 0
 
     def lab(self, s):
@@ -244,14 +248,19 @@ class K:
             if q0_add:
                 ops.append(Inst(f"v_subrev_u32 v{V_LM}, {q0_add}, v{V_LM}", VALU, rd=vr(V_LM), wr=vr(V_LM), key=0))
         for g in range(16):
-            ops.append(Inst(f"v_mul_f32_e32 v{T + g}, s{S_C}, v{S + g}", VALU, rd=sr(S_C) + vr(S + g), wr=vr(T + g),
-                            key=4 * g))
+            src = T + g      # the exponent's operand
+            if not self.unit_c:
+                ops.append(Inst(f"v_mul_f32_e32 v{T + g}, s{S_C}, v{S + g}", VALU, rd=sr(S_C) + vr(S + g), wr=vr(T + g),
+                                key=4 * g))
+            elif not masked:
+                src = S + g
             if masked:
                 const = (g & 3) + 8 * (g >> 2)
                 ops.append(Inst(f"v_cmp_lt_i32_e32 vcc, {const}, v{V_LM}", VALU, rd=vr(V_LM), wr=[("vcc", 0)], key=4 * g))
-                ops.append(Inst(f"v_cndmask_b32_e32 v{T + g}, v{T + g}, v{V_NINF}, vcc", VALU,
-                                rd=vr(T + g) + vr(V_NINF) + [("vcc", 0)], wr=vr(T + g), key=4 * g))
-            ops.append(Inst(f"v_exp_f32_e32 v{T + g}, v{T + g}", TRANS, rd=vr(T + g), wr=vr(T + g), key=4 * g + 1))
+                x = S + g if self.unit_c else T + g
+                ops.append(Inst(f"v_cndmask_b32_e32 v{T + g}, v{x}, v{V_NINF}, vcc", VALU,
+                                rd=vr(x) + vr(V_NINF) + [("vcc", 0)], wr=vr(T + g), key=4 * g))
+            ops.append(Inst(f"v_exp_f32_e32 v{T + g}, v{src}", TRANS, rd=vr(src), wr=vr(T + g), key=4 * g + 1))
             if g % 2 == 1:
                 ops.append(self.cvt(PK + g // 2, T + g - 1, T + g, key=4 * g + 2))
         for g in range(16):
@@ -981,7 +990,7 @@ class K:
 
 
 def main():
-    kernels = [K(bf, ca) for bf in (True, False) for ca in (True, False)]
+    kernels = [K(bf, ca, u) for u in (False, True) for bf in (True, False) for ca in (True, False)]
     out = ['\t.amdgcn_target "amdgcn-amd-amdhsa--gfx950"', "\t.amdhsa_code_object_version 5", "\t.text"]
     for k in kernels:
         out.append(k.render())

@@ -28,6 +28,7 @@
 //     Q^T come from the row-major LDS slice through ds_read_b64_tr_b16.
 //   * Slices that need no mask skip the mask arithmetic (one wave-uniform test per slice).
 #include <cstdlib>
+#include <cstring>
 #include <mutex>
 #include <stdexcept>
 #include <string>
@@ -225,6 +226,42 @@ __device__ unsigned long long g_fa_stamps[kStampWg * 8 * kStampIt * kStampPts];
 // Each wave needs one 32-key operand set and one D x 32 accumulator set (<= 256 registers).
 // MASKED (dense additive mask and/or FlashMask present): every slice takes the per-element path; the
 // unmasked instantiations carry no mask code (as in fwd_kernel).
+// ------------------------------------------------------------------------------------------------
+// Q' = bf16/f16(c Q) for the backward of a forward that scored with it (fwd_folds_q, launch_bwd):
+// the assembly forward rewrites its Q fragments as v_cvt_pk(v_mul_f32(q, c)) (gen_fwd.py
+// q_scale_ops) -- the same fp32 product and round-to-nearest-even pack here, so every score the
+// backward recomputes is bitwise the forward's.  HBM-bound elementwise pass, 16 bytes per thread
+// (rows and heads are 16-byte aligned: d % 8 == 0, bwd_pre_kernel's own assumption); output in the
+// compact layout (b or padded rows, seqlen_q, h, d), rows at the sequence offsets seq_geom uses.
+// ------------------------------------------------------------------------------------------------
+template <bool BF16>
+__global__ void __launch_bounds__(256) q_fold_kernel(const BwdParams p, u16* qf, float c) {
+  using E = Elt<BF16>;
+  const AttnShape& s = p.s;
+  const int bidb = blockIdx.y;
+  const SeqGeom g = seq_geom(p, bidb);
+  const int nch = s.d / 8;
+  const int64_t t = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  const int ch = (int)(t % nch);
+  const int64_t rh = t / nch;
+  const int head = (int)(rh % s.h);
+  const int64_t row = rh / s.h;
+  if (row >= g.sq) return;
+  const u32x4_t x = *(const u32x4_t*)((const u16*)p.q + g.q_off + (int64_t)head * p.q_head + row * p.q_row + 8 * ch);
+  const int64_t hd = (int64_t)s.h * s.d;
+  const int64_t base = (s.cu_seqlens_q != nullptr && !s.varlen_padded_input)
+                           ? (int64_t)s.cu_seqlens_q[bidb] * hd
+                           : (int64_t)bidb * s.seqlen_q * hd;
+  u32x4_t y;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const float lo = E::to_f32((unsigned short)(x[i] & 0xffffu)) * c;
+    const float hi = E::to_f32((unsigned short)(x[i] >> 16)) * c;
+    y[i] = E::pack2(lo, hi);
+  }
+  *(u32x4_t*)(qf + base + row * hd + (int64_t)head * s.d + 8 * ch) = y;
+}
+
 template <bool BF16, int D, bool CAUSAL, bool DROPOUT, bool MASKED>
 __global__ void __launch_bounds__(DkdvTile<D>::NW * 64, 1) bwd_dkdv_kernel(const BwdParams p) {
   using E = Elt<BF16>;
@@ -1024,7 +1061,7 @@ __global__ void __launch_bounds__(DqTile<D>::NW * 64, DqTile<D>::MINB) bwd_dq_ke
 
   if (q_ok) {
     u16* drow = (u16*)p.dq + geo.dq_off + (int64_t)head * p.dq_head + (int64_t)qi * p.dq_row;
-    const float sc = s.scale * (DROPOUT ? s.rp_dropout : 1.f);
+    const float sc = p.dq_scale * (DROPOUT ? s.rp_dropout : 1.f);
 #pragma unroll
     for (int dt = 0; dt < NP; ++dt)
 #pragma unroll
@@ -1198,6 +1235,44 @@ void launch_bwd(const BwdParams& p_in, bool is_bf16, hipStream_t stream) {
 #ifdef FA_FWD_NOGROUP
     p.dq_head_group = 0;
 #endif
+  }
+  // The forward of this output scored with Q' = bf16/f16(c Q) (the assembly forward,
+  // fwd_folds_q): score the backward with the same Q' so that the recomputed P is the forward's --
+  // S' = Q' K^T is c S in the log2 domain (c -> 1), -LSE / scale -> -LSE log2(e) (scale -> ln 2),
+  // dK = ln2 dS^T Q', dQ = scale dS K (dq_scale).  Without this the backward's exact scores
+  // would disagree with the forward's LSE by the rounding of Q' (e.g. a one-key row's P != 1).
+  p.dq_scale = p.s.scale;
+  StreamScratch qfold;
+  {
+    FwdParams f;
+    std::memset(&f, 0, sizeof(f));
+    f.s = p.s;
+    f.q = p.q; f.k = p.k; f.v = p.v; f.o = const_cast<void*>(p.o);
+    f.q_batch = p.q_batch; f.q_row = p.q_row; f.q_head = p.q_head;
+    f.k_batch = p.k_batch; f.k_row = p.k_row; f.k_head = p.k_head;
+    f.v_batch = p.v_batch; f.v_row = p.v_row; f.v_head = p.v_head;
+    f.o_batch = p.o_batch; f.o_row = p.o_row; f.o_head = p.o_head;
+    int bm, bn;
+    fwd_block_size(p.s.d, &bm, &bn);
+    f.num_m_blocks = (p.s.seqlen_q + bm - 1) / bm;
+    if (fwd_folds_q(f, is_bf16)) {
+      const int64_t hd = (int64_t)p.s.h * p.s.d;
+      const int64_t rows = (int64_t)p.s.b * p.s.seqlen_q;   // varlen: total_q <= b max_seqlen_q
+      if (!qfold.alloc((size_t)(rows * hd) * 2, stream))
+        throw std::runtime_error("flash_attn_bwd: hipMallocAsync of the prescaled Q failed");
+      const int64_t per_seq = (int64_t)p.s.seqlen_q * p.s.h * (p.s.d / 8);
+      if ((per_seq + 255) / 256 > 0x7fffffff || p.s.b > 65535)
+        throw std::runtime_error("flash_attn_bwd: prescaled-Q grid too large");
+      const dim3 grid((unsigned)((per_seq + 255) / 256), (unsigned)p.s.b);
+      if (is_bf16)
+        hipLaunchKernelGGL((q_fold_kernel<true>), grid, dim3(256), 0, stream, p, static_cast<u16*>(qfold.p), p.s.scale_log2);
+      else
+        hipLaunchKernelGGL((q_fold_kernel<false>), grid, dim3(256), 0, stream, p, static_cast<u16*>(qfold.p), p.s.scale_log2);
+      p.q = qfold.p;
+      p.q_batch = (int64_t)p.s.seqlen_q * hd; p.q_row = hd; p.q_head = p.s.d;
+      p.s.scale = kLn2;
+      p.s.scale_log2 = 1.0f;
+    }
   }
   // softmax_scale == 0 (uniform attention) would make -LSE / scale infinite: a tiny positive scale
   // gives the same P to fp32 precision (P deviates from uniform by 1e-30 |S|) and dQ, dK ~ 1e-30.

@@ -81,15 +81,19 @@ constexpr int kMaxDev = 64;
 constexpr int kBkn = 128;   // keys per workgroup
 struct DevModule {
   hipModule_t mod = nullptr, mod_dq = nullptr;
-  hipFunction_t fn[4] = {};      // dK/dV [bf16 causal, bf16 full, f16 causal, f16 full]
+  hipFunction_t fn[8] = {};      // dK/dV [bf16 causal, bf16 full, f16 causal, f16 full], then the same with c = 1
   hipFunction_t fn_dq[4] = {};   // dQ, the same order
   int cus = 0;
 };
 std::mutex g_mu;
 DevModule g_dev[kMaxDev];
 
-const char* kNames[4] = {"fa_bwd_dkdv_asm_d128_bf16_causal", "fa_bwd_dkdv_asm_d128_bf16_full",
-                         "fa_bwd_dkdv_asm_d128_f16_causal", "fa_bwd_dkdv_asm_d128_f16_full"};
+// (_c1: P = exp2(S') with no multiply, for launches with c = scale log2(e) = 1 -- the backward of a
+// forward that held Q as bf16/f16(c Q), which launch_bwd scores with that Q', c = 1)
+const char* kNames[8] = {"fa_bwd_dkdv_asm_d128_bf16_causal", "fa_bwd_dkdv_asm_d128_bf16_full",
+                         "fa_bwd_dkdv_asm_d128_f16_causal", "fa_bwd_dkdv_asm_d128_f16_full",
+                         "fa_bwd_dkdv_asm_d128_bf16_causal_c1", "fa_bwd_dkdv_asm_d128_bf16_full_c1",
+                         "fa_bwd_dkdv_asm_d128_f16_causal_c1", "fa_bwd_dkdv_asm_d128_f16_full_c1"};
 const char* kDqNames[4] = {"fa_bwd_dq_asm_d128_bf16_causal", "fa_bwd_dq_asm_d128_bf16_full",
                            "fa_bwd_dq_asm_d128_f16_causal", "fa_bwd_dq_asm_d128_f16_full"};
 
@@ -102,7 +106,7 @@ DevModule& module_for(int dev) {
   DevModule& m = g_dev[dev];
   if (m.mod == nullptr) {
     check(hipModuleLoadData(&m.mod, fa_bwd_asm_co), "hipModuleLoadData");
-    for (int i = 0; i < 4; ++i) check(hipModuleGetFunction(&m.fn[i], m.mod, kNames[i]), kNames[i]);
+    for (int i = 0; i < 8; ++i) check(hipModuleGetFunction(&m.fn[i], m.mod, kNames[i]), kNames[i]);
     check(hipModuleLoadData(&m.mod_dq, fa_dq_asm_co), "hipModuleLoadData (dQ)");
     for (int i = 0; i < 4; ++i) check(hipModuleGetFunction(&m.fn_dq[i], m.mod_dq, kDqNames[i]), kDqNames[i]);
     check(hipDeviceGetAttribute(&m.cus, hipDeviceAttributeMultiprocessorCount, dev), "hipDeviceGetAttribute");
@@ -149,7 +153,7 @@ void launch_bwd_dkdv_asm(const BwdParams& p, bool is_bf16, hipStream_t stream) {
   {
     std::lock_guard<std::mutex> lk(g_mu);
     DevModule& m = module_for(dev);
-    fn = m.fn[(is_bf16 ? 0 : 2) + (s.causal ? 0 : 1)];
+    fn = m.fn[(s.scale_log2 == 1.0f ? 4 : 0) + (is_bf16 ? 0 : 2) + (s.causal ? 0 : 1)];
     cus = m.cus;
   }
   // persistent grid (knob 6, default on): one workgroup per CU (151 KiB of LDS allows one) walking the
@@ -232,7 +236,7 @@ void launch_bwd_dq_asm(const BwdParams& p, bool is_bf16, hipStream_t stream) {
   a.sq = s.seqlen_q; a.sk = s.seqlen_k; a.lse_pitch = s.lse_pitch; a.dsum_pitch = p.seqlen_q_rounded;
   a.h = s.h; a.hk = s.hk;
   a.flags = (s.varlen_padded_input ? 1 : 0) | (p.fuse_pre ? 2 : 0);
-  a.c = s.scale_log2; a.scale = s.scale;
+  a.c = s.scale_log2; a.scale = p.dq_scale;
   a.o = p.o; a.o_batch = 2 * p.o_batch; a.o_row = (int32_t)(2 * p.o_row); a.o_head = (int32_t)(2 * p.o_head);
   a.lsed = p.lsed; a.lsed_ng = p.lsed_ng; a.nrscale = -1.0f / s.scale;
   a.dec = fwd_item_decode(s.b * s.h, s.h, s.h / s.hk, nmb, p.dq_head_group);

@@ -703,6 +703,52 @@ void fwd_block_size(int d, int* block_m, int* block_n) {
   *block_n = d <= 64 ? FwdTile<64>::BN : (d <= 128 ? FwdTile<128>::BN : FwdTile<256>::BN);
 }
 
+// Split-KV for decode-shaped calls (FA2's num_splits heuristic, flash_api.cpp): with fewer
+// workgroups than CUs, split the keys so that about two workgroups per CU stream K/V, each split
+// at least 4 tiles; plain non-causal fixed-length launches only.  FLASH_ATTN_MI355X_NO_SPLITKV=1
+// disables it (tests compare both paths).
+// GQA packing on top (decode with grouped heads): the query heads of a kv head are packed as
+// extra rows when seqlen_q * group fits one query block, so K/V are streamed once per kv head.
+// Sets n_split / split_tiles / pack_g (and the packed shape); allocates nothing.
+static void plan_split(FwdParams& p) {
+  p.n_split = 0;   // 0: the ordinary launch
+  p.pack_g = 1;
+  int bm, bn;
+  fwd_block_size(p.s.d, &bm, &bn);
+  const int nblk = (p.s.seqlen_k + bn - 1) / bn;
+  const bool plain = !p.s.causal && !p.s.dropout && p.s.mask == nullptr && p.s.fm_lts == nullptr &&
+                     p.p_out == nullptr && p.s.cu_seqlens_q == nullptr && p.s.cu_seqlens_k == nullptr;
+  const int G = p.s.h / p.s.hk;
+  const bool pack = plain && G > 1 && (long long)p.s.seqlen_q * G <= bm;
+  const long long wgs = pack ? (long long)p.s.b * p.s.hk : (long long)p.s.b * p.s.h * p.num_m_blocks;
+  if (plain && knob(kKnobNoSplitKv) != 1 && nblk > 0 && (pack || (wgs < 256 && nblk >= 8))) {
+    int ns = 1;
+    if (wgs < 256 && nblk >= 8)
+      ns = (int)std::min<long long>(64, std::min<long long>((512 + wgs - 1) / wgs, nblk / 4));
+    if (ns >= 2 || pack) {
+      p.split_tiles = (nblk + ns - 1) / ns;
+      p.n_split = (nblk + p.split_tiles - 1) / p.split_tiles;
+      if (pack) {
+        p.pack_g = G;
+        p.s.h = p.s.hk;
+        p.s.seqlen_q *= G;
+        p.num_m_blocks = 1;
+      }
+      p.head_group = 0;
+    }
+  }
+}
+
+bool fwd_folds_q(const FwdParams& p_in, bool is_bf16) {
+#ifdef FA_NO_QFOLD   // (A/B variants whose assembly forward is generated with FA_GEN_FOLD=0)
+  return false;
+#endif
+  FwdParams p = p_in;
+  if (p.s.b <= 0 || p.s.h <= 0 || p.num_m_blocks <= 0 || p.s.dropout || (p.s.d != 128 && p.s.d != 64)) return false;
+  plan_split(p);
+  return fwd_asm_applicable(p, is_bf16);
+}
+
 void launch_fwd(const FwdParams& p_in, bool is_bf16, hipStream_t stream) {
   FwdParams p = p_in;
   if (p.s.b <= 0 || p.s.h <= 0) return;
@@ -714,49 +760,16 @@ void launch_fwd(const FwdParams& p_in, bool is_bf16, hipStream_t stream) {
   if (p.num_m_blocks <= 0) return;
   if ((int64_t)p.s.b * p.s.h * p.num_m_blocks > 0x7fffffff)
     throw std::runtime_error("flash_attn_fwd: batch * heads * query blocks too large for the grid");
-  // Split-KV for decode-shaped calls (FA2's num_splits heuristic, flash_api.cpp): with fewer
-  // workgroups than CUs, split the keys so that about two workgroups per CU stream K/V, each split
-  // at least 4 tiles; plain non-causal fixed-length launches only.  FLASH_ATTN_MI355X_NO_SPLITKV=1
-  // disables it (tests compare both paths).
-  // GQA packing on top (decode with grouped heads): the query heads of a kv head are packed as
-  // extra rows when seqlen_q * group fits one query block, so K/V are streamed once per kv head.
   StreamScratch ws;
-  p.n_split = 0;   // 0: the ordinary launch
-  p.pack_g = 1;
-  {
-    int bm, bn;
-    fwd_block_size(p.s.d, &bm, &bn);
-    const int nblk = (p.s.seqlen_k + bn - 1) / bn;
-    const bool plain = !p.s.causal && !p.s.dropout && p.s.mask == nullptr && p.s.fm_lts == nullptr &&
-                       p.p_out == nullptr && p.s.cu_seqlens_q == nullptr && p.s.cu_seqlens_k == nullptr;
-    const int G = p.s.h / p.s.hk;
-    const bool pack = plain && G > 1 && (long long)p.s.seqlen_q * G <= bm;
-    const long long wgs = pack ? (long long)p.s.b * p.s.hk : (long long)p.s.b * p.s.h * p.num_m_blocks;
-    if (plain && knob(kKnobNoSplitKv) != 1 && nblk > 0 && (pack || (wgs < 256 && nblk >= 8))) {
-      int ns = 1;
-      if (wgs < 256 && nblk >= 8)
-        ns = (int)std::min<long long>(64, std::min<long long>((512 + wgs - 1) / wgs, nblk / 4));
-      if (ns >= 2 || pack) {
-        p.split_tiles = (nblk + ns - 1) / ns;
-        p.n_split = (nblk + p.split_tiles - 1) / p.split_tiles;
-        if (pack) {
-          p.pack_g = G;
-          p.s.h = p.s.hk;
-          p.s.seqlen_q *= G;
-          p.num_m_blocks = 1;
-        }
-        p.head_group = 0;
-      }
-    }
-    if (p.n_split > 0) {
-      p.acc_d = (p.s.d + 31) / 32 * 32;
-      const size_t rows = (size_t)p.n_split * p.s.b * p.s.h * p.s.seqlen_q;
-      const size_t bytes = rows * p.acc_d * sizeof(float) + rows * sizeof(float);
-      if (!ws.alloc(bytes, stream))
-        throw std::runtime_error("flash_attn_fwd: hipMallocAsync of the split-KV scratch failed");
-      p.o_acc = static_cast<float*>(ws.p);
-      p.lse_acc = p.o_acc + rows * p.acc_d;
-    }
+  plan_split(p);
+  if (p.n_split > 0) {
+    p.acc_d = (p.s.d + 31) / 32 * 32;
+    const size_t rows = (size_t)p.n_split * p.s.b * p.s.h * p.s.seqlen_q;
+    const size_t bytes = rows * p.acc_d * sizeof(float) + rows * sizeof(float);
+    if (!ws.alloc(bytes, stream))
+      throw std::runtime_error("flash_attn_fwd: hipMallocAsync of the split-KV scratch failed");
+    p.o_acc = static_cast<float*>(ws.p);
+    p.lse_acc = p.o_acc + rows * p.acc_d;
   }
   if (p.p_out != nullptr && (p.p_rows > 65535 * 4 || p.s.b * p.s.h > 65535))
     throw std::runtime_error("flash_attn_fwd: return_softmax grid too large");

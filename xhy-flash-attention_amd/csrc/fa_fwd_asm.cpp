@@ -169,7 +169,10 @@ void fwd_asm_enable(int on) {
   g_enabled = on ? 1 : 0;
 }
 
-bool launch_fwd_asm(const FwdParams& p, bool is_bf16, hipStream_t stream) {
+// Whether launch_fwd_asm takes a launch (after launch_fwd's split-KV plan).  Also asked by the
+// backward (fwd_folds_q): the assembly forward holds Q as bf16/f16(c Q), and a backward of its
+// output must compute its scores from the same rounded Q.
+bool fwd_asm_applicable(const FwdParams& p, bool is_bf16) {
   const AttnShape& s = p.s;
   {
     std::lock_guard<std::mutex> lk(g_mu);
@@ -194,12 +197,19 @@ bool launch_fwd_asm(const FwdParams& p, bool is_bf16, hipStream_t stream) {
   // K / V records of one (sequence, kv head) and the per-tile offsets must stay below 2^31 bytes
   if (!fits32(((int64_t)s.seqlen_k + 64) * kv_row)) return false;
   if (!fits32((int64_t)256 * (q_row > o_row ? q_row : o_row))) return false;
+  const long long nwg = (long long)s.b * s.h * p.num_m_blocks;
+  return nwg <= 0x7fffffff;
+}
 
+bool launch_fwd_asm(const FwdParams& p, bool is_bf16, hipStream_t stream) {
+  if (!fwd_asm_applicable(p, is_bf16)) return false;
+  const AttnShape& s = p.s;
+  const int64_t q_row = 2 * p.q_row, kv_row = 2 * p.k_row, o_row = 2 * p.o_row;
+  const int64_t q_head = 2 * p.q_head, k_head = 2 * p.k_head, v_head = 2 * p.v_head, o_head = 2 * p.o_head;
   int dev = 0;
   check(hipGetDevice(&dev), "hipGetDevice");
   const long long nwg = (long long)s.b * s.h * p.num_m_blocks;
   if (nwg <= 0) return true;
-  if (nwg > 0x7fffffff) return false;
   // Persistent grid (knob 5, default on): one workgroup per CU (the kernel's 160 KiB of LDS allows
   // one), each walking the heaviest-first item list in snake order, so the rounds pair heavy and
   // light causal blocks and every item after the first starts with its K/V tiles and Q already

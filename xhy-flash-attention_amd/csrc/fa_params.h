@@ -10,6 +10,7 @@
 
 #include <hip/hip_runtime.h>
 #include <stdint.h>
+#include <atomic>
 
 namespace fa {
 
@@ -109,6 +110,11 @@ struct BwdParams {
   float* lsed;
   int lsed_ng;
   bool fuse_pre;          // (knob 8) the assembly dQ kernel writes D, softmax_d and lsed; dQ before dK/dV
+  // dQ = dq_scale dS K.  launch_bwd sets it to the softmax scale, then -- when the forward of this
+  // output held Q as bf16/f16(c Q) (fwd_folds_q) -- scores the backward with that same rounded
+  // Q' (q / q_* strides -> a prescaled copy), c -> 1 and scale -> ln 2 (dK = ln2 dS^T Q'), so the
+  // recomputed P is the forward's P.
+  float dq_scale;
 };
 
 // calc_reduced_attn_scores (fa_reduced.hip; reference reduced_scores::Params,
@@ -143,6 +149,10 @@ void launch_fwd(const FwdParams& p, bool is_bf16, hipStream_t stream);
 // fa_fwd_asm.cpp: the assembly forward (d = 128 or 64, no dropout / mask / split-KV); false when it
 // does not apply
 bool launch_fwd_asm(const FwdParams& p, bool is_bf16, hipStream_t stream);
+bool fwd_asm_applicable(const FwdParams& p, bool is_bf16);           // fa_fwd_asm.cpp
+// true when launch_fwd runs this forward on the assembly kernel, which holds Q as bf16/f16(c Q),
+// c = scale log2(e) (gen_fwd.py FA_GEN_FOLD): its backward then scores with that rounded Q too
+bool fwd_folds_q(const FwdParams& p, bool is_bf16);                  // fa_fwd.hip
 void fwd_asm_enable(int on);
 void launch_bwd(const BwdParams& p, bool is_bf16, hipStream_t stream);
 void bwd_overlap_enable(int mode);                                  // fa_bwd.hip: dQ / dK-dV stream overlap mode (default 0: off)
@@ -239,15 +249,17 @@ inline ItemDecode dkdv_item_decode(int nbh, int h_grid, int g, int nblk) {
 // launchers' per-call scratch (split-KV partials, backward LSE rows, varlen work lists) does not hit
 // the driver (once per device).
 inline void keep_pool_memory() {
-  static bool done[64] = {};
+  // (launchers on several host threads: one relaxed flag per device; the attribute set is
+  // idempotent, so two threads racing past the check both set the same value)
+  static std::atomic<bool> done[64] = {};
   int dev = 0;
-  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64 || done[dev]) return;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64 || done[dev].load(std::memory_order_relaxed)) return;
   hipMemPool_t pool;
   if (hipDeviceGetDefaultMemPool(&pool, dev) == hipSuccess) {
     uint64_t thr = UINT64_MAX;
     (void)hipMemPoolSetAttribute(pool, hipMemPoolAttrReleaseThreshold, &thr);
   }
-  done[dev] = true;
+  done[dev].store(true, std::memory_order_relaxed);
 }
 
 // A stream-ordered scratch allocation, freed on its stream when it leaves scope -- also when a
