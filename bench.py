@@ -292,13 +292,32 @@ def cpu_threads(requested=0):
     return max(1, n)
 
 
-def load_pmc(path, workload):
+def lib_sha(path):
+    """sha256[:16] of a library file (the build a PMC profile describes, profiles/pmc_run.sh)"""
+    import hashlib
+    try:
+        with open(path, "rb") as f:
+            return hashlib.sha256(f.read()).hexdigest()[:16]
+    except OSError:
+        return None
+
+
+def load_pmc(path, workload, lib=None):
+    """(per-kernel PMC figures, source note) of the workload -- (None, note) when the profile was
+    taken on another build than `lib` (the library this run loaded): counters of kernels that no
+    longer ship must not be reported next to the timed ones"""
     try:
         with open(path) as f:
             data = json.load(f)
     except (OSError, ValueError):
         return None, None
-    return data.get("workloads", {}).get(workload), data.get("source", {}).get(workload)
+    figs, src = data.get("workloads", {}).get(workload), data.get("source", {}).get(workload)
+    want = data.get("lib_sha", {}).get(workload)
+    have = lib_sha(lib) if lib else None
+    if figs is not None and lib is not None and (want is None or want != have):
+        return None, (f"omitted: the PMC profile ({src}) is of library {want}, this run loaded {have}"
+                      " -- re-run profiles/pmc_run.sh on this build")
+    return figs, src
 
 
 # ------------------------------------------------------------------------------------------------
@@ -442,7 +461,8 @@ def main():
     value = aggregate_tflops(f_step, args.steps, world, t_step)
     fwd_tflops = aggregate_tflops(f_fwd, args.steps, world, t_fwd)
 
-    pmc, pmc_src = load_pmc(args.pmc, args.workload)
+    import flash_attn_2_cuda as fa_ext
+    pmc, pmc_src = load_pmc(args.pmc, args.workload, fa_ext.LIBRARY_PATH)
     kernels = {}
     for n, x in kt.items():
         e = {"avg_ms": round(x["avg_ms"], 4), "launches": x["launches"]}
@@ -505,6 +525,7 @@ def main():
                              "BASELINE.md); c3 only",
             "kernels": kernels,
             "kernel_windows_ms_per_step": round(windows_per_step, 4),
+            "lib_sha": lib_sha(fa_ext.LIBRARY_PATH),
             "pmc_source": pmc_src,
             "roofline": roofline,
             "cpu_baseline": cpu,

@@ -12,7 +12,8 @@ Per kernel, averaged over its dispatches in the profiled bench command:
   * mfma_flops = SQ_INSTS_MFMA * 32768 (executed, vs the algorithmic count in bench.py);
   * valu_per_mfma, lds_per_mfma, wait_inst_frac (SQ_WAIT_INST_ANY / SQ_WAVE_CYCLES), wait_any_frac,
     lds_bank_conflict_frac (SQ_LDS_BANK_CONFLICT / SQ_LDS_IDX_ACTIVE);
-  * clock_ghz = GRBM_GUI_ACTIVE / 8 / profiled duration (DVFS under the profiler).
+  * clock_ghz = GRBM_GUI_ACTIVE / 8 / profiled duration (DVFS under the profiler);
+  * lib_sha: sha256[:16] of the libflash_attn_mi355x.so the passes ran (pmc_run.sh lib_sha.txt).
     python3 profiles/pmc.py gpurun_out/pmc_c3 c3 [source-note]
 """
 import csv
@@ -88,6 +89,13 @@ def main(root, workload, note=None):
             data = json.load(f)
     data["workloads"][workload] = {k: derive(c, dur.get(k)) for k, c in sorted(counters.items())}
     data["source"][workload] = note or f"rocprofv3 --pmc passes of profiles/pmc_run.sh ({root})"
+    # the library the passes profiled (pmc_run.sh lib_sha.txt): bench.py drops these figures for
+    # any other build
+    sha = None
+    if os.path.exists(os.path.join(root, "lib_sha.txt")):
+        with open(os.path.join(root, "lib_sha.txt")) as f:
+            sha = f.read().strip() or None
+    data.setdefault("lib_sha", {})[workload] = sha
     with open(path, "w") as f:
         json.dump(data, f, indent=1, sort_keys=True)
     print(json.dumps(data["workloads"][workload], indent=1))

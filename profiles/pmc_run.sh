@@ -8,6 +8,9 @@ OUT=${1:-gpurun_out/pmc}
 WL=${2:-c3}
 mkdir -p "$OUT"
 export TMPDIR=/tmp
+# the build these counters describe (bench.py reports them only for a library with this hash)
+python3 -c "import hashlib,sys; print(hashlib.sha256(open(sys.argv[1],'rb').read()).hexdigest()[:16])" \
+  xhy-flash-attention_amd/libflash_attn_mi355x.so > "$OUT/lib_sha.txt"
 CMD="python3 bench.py --workload $WL --steps 3 --warmup 1 --ramp-s 0 --no-cpu-baseline"
 pass() {   # name counters...
   local name=$1; shift

@@ -1,0 +1,84 @@
+"""The backward's launch switches against the oracle: the fused preprocessing
+(knob 8: D = rowsum(dO o O) and the dK/dV chain starts computed inside the assembly dQ kernel,
+reference compute_dot_do_o, flash_bwd_kernel.h:112-188) and the persistent item loops (knob 6) each
+run under the reference's 2x rule (tests/test_flash_attn.py:630-639) in both settings, so the fused
+D path keeps oracle coverage whatever the defaults are.  A C3-class fixed-length case and a varlen
+case with ragged sequences; d = 128 (the assembly backward's domain)."""
+import pytest
+import torch
+
+from knobs import BWD_PERSIST, FUSE_PRE, knob
+from oracle.attention_ref import attention_ref, check_within_bound
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda"
+
+
+@pytest.fixture(scope="module", autouse=True)
+def _need_gpu():
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    import flash_attn_2_cuda  # noqa: F401
+
+
+def _bound(name, got, ref, pt):
+    ok, err, bound = check_within_bound(got.float(), ref.float(), pt.float())
+    assert ok, f"{name}: max|err| {err:.3e} > bound {bound:.3e}"
+
+
+@pytest.mark.parametrize("persist", [0, 1])
+@pytest.mark.parametrize("fuse", [0, 1])
+@pytest.mark.parametrize("causal", [True, False])
+def test_fixed_length_2x_rule(fuse, persist, causal):
+    """C3-class (bf16, d 128, 2 x 2048 x 16 heads: 256 dK/dV items, more than the CUs, so the
+    persistent loops run several rounds)"""
+    from flash_attn import flash_attn_func
+
+    torch.manual_seed(0)
+    b, s, h, d = 2, 2048, 16, 128
+    q, k, v = (torch.randn(b, s, h, d, device=DEV, dtype=torch.bfloat16, requires_grad=True) for _ in range(3))
+    out = flash_attn_func(q, k, v, causal=causal)
+    g = torch.randn_like(out)
+    with knob(FUSE_PRE, fuse), knob(BWD_PERSIST, persist):
+        dq, dk, dv = torch.autograd.grad(out, (q, k, v), g)
+    qr, kr, vr = (x.detach().clone().requires_grad_() for x in (q, k, v))
+    ref, _ = attention_ref(qr, kr, vr, causal=causal)
+    gr = torch.autograd.grad(ref, (qr, kr, vr), g)
+    qp, kp, vp = (x.detach().clone().requires_grad_() for x in (q, k, v))
+    pt, _ = attention_ref(qp, kp, vp, causal=causal, upcast=False, reorder_ops=True)
+    gp = torch.autograd.grad(pt, (qp, kp, vp), g)
+    _bound("out", out, ref, pt)
+    for name, got, r, p in zip(("dq", "dk", "dv"), (dq, dk, dv), gr, gp):
+        _bound(name, got, r, p)
+
+
+@pytest.mark.parametrize("fuse", [0, 1])
+@pytest.mark.parametrize("causal", [True, False])
+def test_varlen_2x_rule(fuse, causal):
+    from flash_attn import flash_attn_varlen_func
+
+    torch.manual_seed(1)
+    lens = [1, 300, 1500, 0, 777, 64, 255, 256, 257]
+    h, d = 4, 128
+    cu = torch.tensor([0] + lens, dtype=torch.int64).cumsum(0).to(torch.int32).to(DEV)
+    total = sum(lens)
+    q, k, v = (torch.randn(total, h, d, device=DEV, dtype=torch.bfloat16, requires_grad=True) for _ in range(3))
+    out = flash_attn_varlen_func(q, k, v, cu, cu, max(lens), max(lens), causal=causal)
+    g = torch.randn_like(out)
+    with knob(FUSE_PRE, fuse):
+        dq, dk, dv = torch.autograd.grad(out, (q, k, v), g)
+    for i, n in enumerate(lens):
+        if n == 0:
+            continue
+        a, e = int(cu[i]), int(cu[i + 1])
+        qs, ks, vs = (x.detach()[a:e].unsqueeze(0) for x in (q, k, v))
+        gs = g[a:e].unsqueeze(0)
+        qr, kr, vr = (x.clone().requires_grad_() for x in (qs, ks, vs))
+        ref, _ = attention_ref(qr, kr, vr, causal=causal)
+        gr = torch.autograd.grad(ref, (qr, kr, vr), gs)
+        qp, kp, vp = (x.clone().requires_grad_() for x in (qs, ks, vs))
+        pt, _ = attention_ref(qp, kp, vp, causal=causal, upcast=False, reorder_ops=True)
+        gp = torch.autograd.grad(pt, (qp, kp, vp), gs)
+        _bound(f"seq {i} out", out[a:e].unsqueeze(0), ref, pt)
+        for name, got, r, p in zip(("dq", "dk", "dv"), (dq, dk, dv), gr, gp):
+            _bound(f"seq {i} {name}", got[a:e].unsqueeze(0), r, p)

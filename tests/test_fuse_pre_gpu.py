@@ -37,8 +37,10 @@ def _check(fused, plain, n_rows=None):
 
 @pytest.mark.parametrize("causal", [True, False])
 @pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float16])
+# (4, 4096, 4096, 32, 32): 512 dQ items, twice the CUs, so the persistent dQ loop (knob 6, on by
+# default) reloads its fused-D state per item within one workgroup
 @pytest.mark.parametrize("b,s,sk,h,hk", [(2, 1024, 1024, 16, 16), (3, 1000, 700, 8, 2), (1, 33, 300, 4, 4),
-                                         (2, 4100, 4100, 4, 1)])
+                                         (2, 4100, 4100, 4, 1), (4, 4096, 4096, 32, 32)])
 def test_fused_pre_matches_bwd_pre(b, s, sk, h, hk, dtype, causal):
     from flash_attn.flash_attn_interface import _flash_attn_backward, _flash_attn_forward
 

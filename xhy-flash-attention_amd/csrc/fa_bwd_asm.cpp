@@ -187,7 +187,9 @@ void launch_bwd_dkdv_asm(const BwdParams& p, bool is_bf16, hipStream_t stream) {
   check(hipModuleLaunchKernel(fn, (unsigned)grid, 1, 1, 256, 1, 1, 0, stream, nullptr, cfg), "hipModuleLaunchKernel");
 }
 
-bool dq_asm_applicable(const BwdParams& p) {
+// fused: the kernel also reads O (the fused preprocessing, knob 8): its strides and 256-row records
+// must fit as well -- checked only then, so an O layout the kernel never reads does not turn it off
+bool dq_asm_applicable(const BwdParams& p, bool fused) {
   const AttnShape& s = p.s;
   if (knob(kKnobDqAsm) == 0) return false;
   if (s.d != 128 || s.dropout || s.mask != nullptr || s.fm_lts != nullptr) return false;
@@ -195,13 +197,12 @@ bool dq_asm_applicable(const BwdParams& p) {
   if (p.k_row != p.v_row || p.k_batch != p.v_batch) return false;   // K / V share the DMA offsets
   const int nmb = (s.seqlen_q + 255) / 256;
   if (nmb > 65535 || (long long)s.b * s.h * nmb > 0x7fffffffll) return false;
-  for (int64_t x : {p.q_row, p.k_row, p.do_row, p.dq_row, p.q_head, p.k_head, p.v_head, p.do_head, p.dq_head,
-                    p.o_row, p.o_head})
+  for (int64_t x : {p.q_row, p.k_row, p.do_row, p.dq_row, p.q_head, p.k_head, p.v_head, p.do_head, p.dq_head})
     if (!fits32(2 * x)) return false;
-  const int64_t sq = s.seqlen_q + 256, sk = s.seqlen_k + 64;
+  if (fused && (!fits32(2 * p.o_row) || !fits32(2 * p.o_head) || !fits32(256 * 2 * p.o_row))) return false;
+  const int64_t sk = s.seqlen_k + 64;
   for (int64_t x : {256 * 2 * p.q_row, 256 * 2 * p.do_row, 256 * 2 * p.dq_row, sk * 2 * p.k_row})
     if (!fits32(x)) return false;
-  (void)sq;
   return true;
 }
 

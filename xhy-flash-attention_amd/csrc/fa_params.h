@@ -158,7 +158,7 @@ void launch_bwd(const BwdParams& p, bool is_bf16, hipStream_t stream);
 void bwd_overlap_enable(int mode);                                  // fa_bwd.hip: dQ / dK-dV stream overlap mode (default 0: off)
 bool bwd_asm_applicable(const BwdParams& p);                        // fa_bwd_asm.cpp
 void launch_bwd_dkdv_asm(const BwdParams& p, bool is_bf16, hipStream_t stream);
-bool dq_asm_applicable(const BwdParams& p);                         // fa_bwd_asm.cpp
+bool dq_asm_applicable(const BwdParams& p, bool fused);                         // fa_bwd_asm.cpp
 void launch_bwd_dq_asm(const BwdParams& p, bool is_bf16, hipStream_t stream);
 void launch_reduced_scores(const ReducedParams& p, bool is_bf16, hipStream_t stream);
 void launch_rotary(const RotaryParams& p, bool interleaved, bool conj, bool is_bf16, hipStream_t stream);
