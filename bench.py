@@ -42,7 +42,7 @@ PEAK_TFLOPS = 2516.6          # 256 CU x 4 SIMD x 1024 bf16/f16 MFMA FLOP/clk x 
 PEAK_HBM_GBPS = 8000.0        # HBM3E spec (MI355X_MICROARCH.md)
 H100_FWD_BWD_TFLOPS = 308.0   # FA2 fwd+bwd, causal, hdim128, s=8k, H100 SXM5
 KERNELS = {0: "fwd_kernel", 1: "bwd_pre_kernel", 2: "bwd_dkdv_kernel", 3: "bwd_dq_kernel",
-           4: "bwd_dkdv_dq_window"}   # 4: from the dK/dV launch to the end of dQ (they overlap, two streams)
+           4: "bwd_dkdv_dq_window", 5: "bwd_qfold_kernel"}   # 4: from the dK/dV launch to the end of dQ (they overlap, two streams)
 # algorithmic flops of each kernel in units of F_fwd (the atomic-free backward recomputes S and dP
 # in both kernels: dK/dV = S, dP, dV, dK GEMMs; dQ = S, dP, dQ GEMMs)
 KERNEL_FLOP_FACTOR = {"fwd_kernel": 1.0, "bwd_dkdv_kernel": 2.0, "bwd_dq_kernel": 1.5}

@@ -136,6 +136,22 @@ def test_asm_dq_fused_pre_in_emulator(dq_text, b, sq, sk, h, hk, causal, bf16):
     assert e <= (1e-2 if bf16 else 2e-3), e
 
 
+@pytest.mark.timeout(900)
+@pytest.mark.parametrize("b,sq,sk,h,hk,causal,bf16,grid", [
+    (1, 330, 200, 2, 1, True, True, None),      # GQA, ragged last group (Q' rows past seqlen_q not stored)
+    (2, 130, 200, 2, 2, False, False, None),    # fp16 (v_cvt_f32_f16 unpack)
+    (1, 600, 600, 2, 1, True, True, 2),         # persistent: 6 items over 2 workgroups (fold state per item)
+])
+def test_asm_dq_q_fold_in_emulator(dq_text, b, sq, sk, h, hk, causal, bf16, grid):
+    """flags bit 2 (the backward of the folded forward, launch_bwd): the dQ kernel rewrites its Q
+    fragments as bf16/f16(c Q) and stores them for dK/dV -- compared bitwise with the forward's
+    rounding -- then scores with c = 1; dQ against float64 on that Q'"""
+    import emu_dq
+    e, *_ = emu_dq.run(b, sq, sk, h, hk, causal, bf16, seed=6, text=dq_text, verbose=False, fused=True, qfold=True,
+                       grid=grid)
+    assert e <= (1e-2 if bf16 else 2e-3), e
+
+
 def test_generated_dq_kernels_assemble_shape():
     text = subprocess.run([sys.executable, os.path.join(ROOT, "xhy-flash-attention_amd", "csrc", "asm", "gen_dq.py")],
                           check=True, capture_output=True, text=True).stdout

@@ -41,7 +41,10 @@ def pack_args(**kw):
     # fused bwd_pre (flags bit 1): o, o_batch, o_row, o_head, lsed, lsed_ng, -1 / scale
     out += struct.pack("<Qqii", kw.get("o", 0), kw.get("o_batch", 0), kw.get("o_row", 0), kw.get("o_head", 0))
     out += struct.pack("<Qif", kw.get("lsed", 0), kw.get("lsed_ng", 0), kw.get("nrscale", 0.0))
-    assert len(out) == 272, len(out)
+    # the Q fold (flags bit 2): qf, qf_batch, qf_row, qf_head, qc
+    out += struct.pack("<Qqiifi", kw.get("qf", 0), kw.get("qf_batch", 0), kw.get("qf_row", 0), kw.get("qf_head", 0),
+                       kw.get("qc", 0.0), 0)
+    assert len(out) == 304, len(out)
     return out
 
 
@@ -68,11 +71,14 @@ def reference_dq(q, k, v, do, causal, scale, o=None):
 
 
 def run(b=1, sq=300, sk=300, h=2, hk=1, causal=True, bf16=True, seed=0, text=None, verbose=True, hp=0, grid=None,
-        fused=False, wgs=None):
+        fused=False, wgs=None, qfold=False):
     """hp: heads per XCD group of the work order (0: head-fastest); grid: workgroups of the
     persistent item loop (default: one per item); fused: the kernel computes D = rowsum(dO o O) itself
     (flags bit 1, bwd_pre fused): the D input is garbage, softmax_d and the dK/dV scratch
-    [-LSE / scale | -D] are checked against float64 (the error returned is the max of the three)"""
+    [-LSE / scale | -D] are checked against float64 (the error returned is the max of the three);
+    qfold (with fused): the Q fold (flags bit 2) -- the kernel rewrites Q as bf16/f16(c Q), stores it
+    (checked bitwise against the forward's rounding) and runs with c = 1, scale ln 2 on the chain
+    starts, dQ scaled by the softmax scale, against a float64 reference on that Q'"""
     rng = np.random.default_rng(seed)
     q = rng.standard_normal((b, sq, h, D)).astype(np.float32)
     k = rng.standard_normal((b, sk, hk, D)).astype(np.float32)
@@ -86,7 +92,12 @@ def run(b=1, sq=300, sk=300, h=2, hk=1, causal=True, bf16=True, seed=0, text=Non
     if fused:
         o16 = enc(rng.standard_normal((b, sq, h, D)).astype(np.float32)).astype(np.uint16)
         of = dec(o16).astype(np.float64)
-    lse, dsum, dq_ref = reference_dq(qf, kf, vf, dof, causal, scale, o=of)
+    qc32 = np.float32(scale * 1.4426950408889634)
+    q_s = qf      # the Q the scores are made of
+    if qfold:
+        qfold16 = enc(qf.astype(np.float32) * qc32).astype(np.uint16)
+        q_s = dec(qfold16).astype(np.float64) * (np.log(2.0) / scale)
+    lse, dsum, dq_ref = reference_dq(q_s, kf, vf, dof, causal, scale, o=of)
     if fused:
         dsum = np.einsum("bshd,bshd->bhs", dof, of)
     sqr = (sq + 127) // 128 * 128
@@ -108,12 +119,19 @@ def run(b=1, sq=300, sk=300, h=2, hk=1, causal=True, bf16=True, seed=0, text=Non
               sq=sq, sk=sk, lse_pitch=sq, dsum_pitch=sqr, h=h, hk=hk, flags=0,
               c=float(np.float32(scale * 1.4426950408889634)), scale=float(np.float32(scale)))
     ng = (sq + 31) // 32
+    sc_l = np.log(2.0) if qfold else scale      # the chain starts' scale (launch_bwd: ln 2 with the fold)
     if fused:
         ao = heap.put(o16)
         alsed = heap.alloc(b * h * ng * 256)
         heap.get(alsed, b * h * ng * 256).view(np.float32)[:] = np.nan
         kw.update(o=ao, o_batch=sq * h * D * 2, o_row=h * D * 2, o_head=D * 2, lsed=alsed, lsed_ng=ng,
-                  nrscale=float(np.float32(-1.0 / scale)), flags=2)
+                  nrscale=float(np.float32(-1.0 / sc_l)), flags=2)
+    if qfold:
+        assert fused
+        aqf = heap.alloc(b * sq * h * D * 2)
+        heap.get(aqf, b * sq * h * D * 2)[:] = 0xAB
+        kw.update(qf=aqf, qf_batch=sq * h * D * 2, qf_row=h * D * 2, qf_head=D * 2, qc=float(qc32), c=1.0,
+                  flags=2 | 4)
     akarg = heap.put(np.frombuffer(pack_args(**kw), dtype=np.uint8))
     text = text or asm_text()
     name = f"fa_bwd_dq_asm_d128_{'bf16' if bf16 else 'f16'}_{'causal' if causal else 'full'}"
@@ -133,13 +151,16 @@ def run(b=1, sq=300, sk=300, h=2, hk=1, causal=True, bf16=True, seed=0, text=Non
         sc = heap.get(alsed, b * h * ng * 256).view(np.float32).reshape(b, h, ng, 2, 32)
         want = np.zeros((b, h, ng * 32, 2))
         with np.errstate(all="ignore"):
-            want[:, :, :sq, 0] = -lse / scale
+            want[:, :, :sq, 0] = -lse / sc_l
         want[:, :, :sq, 1] = -dsum
         want = want.reshape(b, h, ng, 32, 2).transpose(0, 1, 2, 4, 3)
         fin = np.isfinite(want)
         assert np.array_equal(fin, np.isfinite(sc)), "scratch: non-finite entries differ"
         assert np.array_equal(want[~fin], sc[~fin].astype(np.float64)), "scratch: infinite entries differ"
         e = max(e, np.abs(sc[fin] - want[fin]).max() / max(np.abs(want[fin]).max(), 1e-9))
+    if qfold:
+        got_qf = heap.get(aqf, b * sq * h * D * 2).view(np.uint16).reshape(b, sq, h, D)
+        assert np.array_equal(got_qf, qfold16.reshape(b, sq, h, D)), "Q': not the forward's bf16/f16(c Q)"
     if verbose:
         print(f"b={b} sq={sq} sk={sk} h={h} hk={hk} causal={causal} bf16={bf16}: rel max|ddQ| {e:.3e} "
               f"({emu.count} instructions, {emu.mfma_count} MFMAs)")

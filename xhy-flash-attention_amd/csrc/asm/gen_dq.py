@@ -124,8 +124,9 @@ S_ROUND = 100                  # round r of the persistent item loop
 S_ITEM = 101                   # the item index
 NSGPR = 102
 
-KARG_SIZE = 272
+KARG_SIZE = 304
 FUSE_OFF = 232   # DqAsmArgs: o, o_batch, o_row, o_head, lsed, lsed_ng, nrscale (flags bit 1: fused D)
+QF_OFF = 272     # DqAsmArgs: qf, qf_batch, qf_row, qf_head, qc (flags bit 2: the Q fold, q_fold)
 DEC_OFF = 184    # fa_params.h ItemDecode (40 bytes) after DqAsmArgs' 184
 NITEMS_OFF = 224  # n_items, grid (persistent item loop)
 
@@ -408,6 +409,27 @@ class K:
         ins += [I(f"s_mov_b32 s{ZERO}, 0", SALU, wr=sr(ZERO))]
         ins += desc(S_KD, Pk, KOFF, KVH, Hk, None, None, [I(f"s_mul_i32 s{S_KD + 2}, s{NEND}, s{Rkv}", SALU, rd=sr(NEND) + sr(Rkv), wr=sr(S_KD + 2))])
         ins += desc(S_VD, Pv, KOFF, KVH, Hv, None, None, [I(f"s_mul_i32 s{S_VD + 2}, s{NEND}, s{Rkv}", SALU, rd=sr(NEND) + sr(Rkv), wr=sr(S_VD + 2))])
+        # (flags bit 2, the Q fold) the Q' output of q_fold: descriptor s[56:59] (the q / k / v / dout
+        # pointers are consumed), rows [m0, m0 + nrow) of this sequence and head in the compact layout
+        # (row 0 at cu_q[bidb] qf_row varlen, bidb qf_batch otherwise); qf_row in s60, qc in s62
+        l_noqf, l_qfx, l_qfd = self.lab("noqf"), self.lab("qffixed"), self.lab("qfdone")
+        ins += [I(f"s_bitcmp1_b32 s{FLG}, 2", SALU, rd=sr(FLG), wr=[("scc", 0)]),
+                I(f"s_cbranch_scc0 {l_noqf}", BRANCH),
+                I(f"s_load_dwordx8 s[56:63], s[0:1], {QF_OFF}", SMEM, rd=sr(0, 2), wr=sr(56, 8)),
+                I("s_waitcnt lgkmcnt(0)", WAIT),
+                I(f"s_cmp_eq_u64 s[{Pcq}:{Pcq + 1}], 0", SALU, rd=sr(Pcq, 2), wr=[("scc", 0)]),
+                I(f"s_cbranch_scc1 {l_qfx}", BRANCH),
+                I(f"s_bitcmp1_b32 s{FLG}, 0", SALU, rd=sr(FLG), wr=[("scc", 0)]),
+                I(f"s_cbranch_scc1 {l_qfx}", BRANCH),
+                I(f"s_lshl_b32 s{T[2]}, s{BIDB}, 2", SALU, rd=sr(BIDB), wr=sr(T[2])),
+                I(f"s_load_dword s{T[2]}, s[{Pcq}:{Pcq + 1}], s{T[2]}", SMEM, rd=sr(Pcq, 2) + sr(T[2]), wr=sr(T[2])),
+                I("s_waitcnt lgkmcnt(0)", WAIT)]
+        ins += mul64((58, 59), T[2], 60)
+        ins += [I(f"s_branch {l_qfd}", BRANCH), label(l_qfx)]
+        ins += mul64_i64((T[1], T[2]), BIDB, 58)
+        ins += [I(f"s_mov_b32 s58, s{T[1]}", SALU), I(f"s_mov_b32 s59, s{T[2]}", SALU), label(l_qfd)]
+        ins += desc(56, 56, (58, 59), HEAD, 61, M0R, 60, [I(f"s_mul_i32 s58, s{NROW}, s60", SALU, rd=sr(NROW) + sr(60), wr=sr(58))])
+        ins += [label(l_noqf)]
         # steps: subtiles ns = ceil(n_end / 32) rounded up to even; N / 2 steps
         ins += [I(f"s_add_u32 s{T[0]}, s{NEND}, {2 * SUB - 1}", SALU, rd=sr(NEND), wr=sr(T[0])),
                 I(f"s_lshr_b32 s{T[0]}, s{T[0]}, 6", SALU, rd=sr(T[0]), wr=sr(T[0])),          # steps
@@ -627,6 +649,47 @@ class K:
         ins += [label(l_nof)]
         return ins
 
+    def q_fold(self):
+        """(flags bit 2) the backward of a forward that held Q as bf16/f16(c Q) (gen_fwd.py FA_GEN_FOLD,
+        launch_bwd): the Q fragments become bf16/f16(qc Q) -- v_mul_f32 by qc and a round-to-nearest-
+        even pack, the forward's own q_scale_ops, so the scores S^T = K Q'^T (c = 1 on this launch)
+        are bitwise the forward's -- and Q' is stored for the dK/dV kernel (descriptor s[56:59],
+        qf_row s60, qc s62; rows past seqlen_q fall outside the records).  Runs once per item after
+        the prologue's wait (the Q loads landed), in v[0:95] (the S^T / dP^T tiles, idle here)."""
+        I = Inst
+        l_no = self.lab("noqfold")
+        r_, hh, x = V_TMP, V_TMP + 1, V_TMP + 2
+        ins = [I("s_bitcmp1_b32 s99, 2", SALU, rd=sr(99), wr=[("scc", 0)]), I(f"s_cbranch_scc0 {l_no}", BRANCH),
+               I(f"v_and_b32_e32 v{r_}, 31, v{V_LANE}", VALU, rd=vr(V_LANE), wr=vr(r_)),
+               I(f"v_lshrrev_b32_e32 v{hh}, 5, v{V_LANE}", VALU, rd=vr(V_LANE), wr=vr(hh)),
+               I(f"s_lshl_b32 s{S_TMP}, s{S_WAVE}, 6", SALU, rd=sr(S_WAVE), wr=sr(S_TMP))]
+        n = 4 * KS
+        X, LO, HI = 0, 32, 64
+        for j in range(2):
+            off = x + j
+            ins += [I(f"v_add_u32_e32 v{off}, s{S_TMP}, v{r_}", VALU, rd=sr(S_TMP) + vr(r_), wr=vr(off)),
+                    I(f"v_add_u32_e32 v{off}, {32 * j}, v{off}", VALU, rd=vr(off), wr=vr(off)),
+                    I(f"v_mul_lo_u32 v{off}, v{off}, s60", VALU, rd=vr(off) + sr(60), wr=vr(off)),
+                    I(f"v_lshl_add_u32 v{off}, v{hh}, 4, v{off}", VALU, rd=vr(hh) + vr(off), wr=vr(off))]
+            q0 = QF(j, 0)
+            ins += [I(f"v_accvgpr_read_b32 v{X + i}, a{q0 + i}", ACCR, rd=ar(q0 + i), wr=vr(X + i)) for i in range(n)]
+            if self.bf16:
+                ins += [I(f"v_lshlrev_b32_e32 v{LO + i}, 16, v{X + i}", VALU, rd=vr(X + i), wr=vr(LO + i)) for i in range(n)]
+                ins += [I(f"v_and_b32_e32 v{HI + i}, 0xffff0000, v{X + i}", VALU, rd=vr(X + i), wr=vr(HI + i)) for i in range(n)]
+            else:
+                ins += [I(f"v_cvt_f32_f16_e32 v{LO + i}, v{X + i}", VALU, rd=vr(X + i), wr=vr(LO + i)) for i in range(n)]
+                ins += [I(f"v_lshrrev_b32_e32 v{HI + i}, 16, v{X + i}", VALU, rd=vr(X + i), wr=vr(HI + i)) for i in range(n)]
+                ins += [I(f"v_cvt_f32_f16_e32 v{HI + i}, v{HI + i}", VALU, rd=vr(HI + i), wr=vr(HI + i)) for i in range(n)]
+            for R in (LO, HI):
+                ins += [I(f"v_mul_f32_e32 v{R + i}, s62, v{R + i}", VALU, rd=sr(62) + vr(R + i), wr=vr(R + i)) for i in range(n)]
+            ins += [self.cvt(X + i, LO + i, HI + i) for i in range(n)]
+            ins += [I(f"v_accvgpr_write_b32 a{q0 + i}, v{X + i}", ACCW, rd=vr(X + i), wr=ar(q0 + i)) for i in range(n)]
+            ins += [I(f"buffer_store_dwordx4 v[{X + 4 * ks}:{X + 4 * ks + 3}], v{off}, s[56:59], 0 offen offset:{32 * ks}",
+                      VSTORE, rd=vr(X + 4 * ks, 4) + vr(off) + sr(56, 4)) for ks in range(KS)]
+            # (the next q-block's loads of v[0:31]: the stores read their data at issue -- WAR 2)
+        ins += [label(l_no)]
+        return ins
+
     def epilogue(self):
         """dQ = scale dQ^T^T in bf16 / f16, rows < seqlen_q (range-checked; rows on lanes as gen_fwd.py)"""
         I = Inst
@@ -683,6 +746,7 @@ class K:
         # K / V(0) and (1) landed (phase -1 reads 0, its tail prefetches 1): 16 younger DMAs
         pro += [Inst("s_waitcnt vmcnt(16)", WAIT), Inst("s_barrier", BARRIER)]
         pro += self.fused_d()
+        pro += self.q_fold()
         # no keys: epilogue (dQ = 0), after the fused D (softmax_d and the scratch are still written)
         pro += [Inst(f"s_cmp_lt_i32 s{S_NLAST}, 0", SALU, rd=sr(S_NLAST), wr=[("scc", 0)]),
                 Inst(f"s_cbranch_scc1 {l_epi}", BRANCH)]

@@ -1241,8 +1241,12 @@ void launch_bwd(const BwdParams& p_in, bool is_bf16, hipStream_t stream) {
   // S' = Q' K^T is c S in the log2 domain (c -> 1), -LSE / scale -> -LSE log2(e) (scale -> ln 2),
   // dK = ln2 dS^T Q', dQ = scale dS K (dq_scale).  Without this the backward's exact scores
   // would disagree with the forward's LSE by the rounding of Q' (e.g. a one-key row's P != 1).
+  // Q' comes from the assembly dQ kernel when it runs first (fused preprocessing: it converts its
+  // own Q fragments and stores them for dK/dV), else from q_fold_kernel.
   p.dq_scale = p.s.scale;
-  StreamScratch qfold;
+  p.qfold = nullptr;
+  bool fold = false;
+  float fold_c = p.s.scale_log2;
   {
     FwdParams f;
     std::memset(&f, 0, sizeof(f));
@@ -1255,24 +1259,11 @@ void launch_bwd(const BwdParams& p_in, bool is_bf16, hipStream_t stream) {
     int bm, bn;
     fwd_block_size(p.s.d, &bm, &bn);
     f.num_m_blocks = (p.s.seqlen_q + bm - 1) / bm;
-    if (fwd_folds_q(f, is_bf16)) {
-      const int64_t hd = (int64_t)p.s.h * p.s.d;
-      const int64_t rows = (int64_t)p.s.b * p.s.seqlen_q;   // varlen: total_q <= b max_seqlen_q
-      if (!qfold.alloc((size_t)(rows * hd) * 2, stream))
-        throw std::runtime_error("flash_attn_bwd: hipMallocAsync of the prescaled Q failed");
-      const int64_t per_seq = (int64_t)p.s.seqlen_q * p.s.h * (p.s.d / 8);
-      if ((per_seq + 255) / 256 > 0x7fffffff || p.s.b > 65535)
-        throw std::runtime_error("flash_attn_bwd: prescaled-Q grid too large");
-      const dim3 grid((unsigned)((per_seq + 255) / 256), (unsigned)p.s.b);
-      if (is_bf16)
-        hipLaunchKernelGGL((q_fold_kernel<true>), grid, dim3(256), 0, stream, p, static_cast<u16*>(qfold.p), p.s.scale_log2);
-      else
-        hipLaunchKernelGGL((q_fold_kernel<false>), grid, dim3(256), 0, stream, p, static_cast<u16*>(qfold.p), p.s.scale_log2);
-      p.q = qfold.p;
-      p.q_batch = (int64_t)p.s.seqlen_q * hd; p.q_row = hd; p.q_head = p.s.d;
-      p.s.scale = kLn2;
-      p.s.scale_log2 = 1.0f;
-    }
+    fold = fwd_folds_q(f, is_bf16);
+  }
+  if (fold) {
+    p.s.scale = kLn2;
+    p.s.scale_log2 = 1.0f;
   }
   // softmax_scale == 0 (uniform attention) would make -LSE / scale infinite: a tiny positive scale
   // gives the same P to fp32 precision (P deviates from uniform by 1e-30 |S|) and dQ, dK ~ 1e-30.
@@ -1300,6 +1291,30 @@ void launch_bwd(const BwdParams& p_in, bool is_bf16, hipStream_t stream) {
   // knob 8: the assembly dQ kernel computes D itself and writes softmax_d and the dK/dV scratch
   p.fuse_pre = asm_dkdv && knob(kKnobFusePre) != 0 && p.s.d == 128 && !p.s.dropout && p.s.mask == nullptr &&
                p.s.fm_lts == nullptr && dq_asm_applicable(p, true);
+  StreamScratch qfold;
+  if (fold) {
+    const int64_t hd = (int64_t)p.s.h * p.s.d;
+    const int64_t rows = (int64_t)p.s.b * p.s.seqlen_q;   // varlen: total_q <= b max_seqlen_q
+    if (!qfold.alloc((size_t)(rows * hd) * 2, stream))
+      throw std::runtime_error("flash_attn_bwd: hipMallocAsync of the prescaled Q failed");
+    if (p.fuse_pre) {   // the dQ kernel (first) converts and stores Q'; dK/dV reads it
+      p.qfold = qfold.p;
+      p.qfold_c = fold_c;
+    } else {
+      const int64_t per_seq = (int64_t)p.s.seqlen_q * p.s.h * (p.s.d / 8);
+      if ((per_seq + 255) / 256 > 0x7fffffff || p.s.b > 65535)
+        throw std::runtime_error("flash_attn_bwd: prescaled-Q grid too large");
+      const dim3 grid((unsigned)((per_seq + 255) / 256), (unsigned)p.s.b);
+      prof_begin(kTimeQFold, stream);
+      if (is_bf16)
+        hipLaunchKernelGGL((q_fold_kernel<true>), grid, dim3(256), 0, stream, p, static_cast<u16*>(qfold.p), fold_c);
+      else
+        hipLaunchKernelGGL((q_fold_kernel<false>), grid, dim3(256), 0, stream, p, static_cast<u16*>(qfold.p), fold_c);
+      prof_end(kTimeQFold, stream);
+      p.q = qfold.p;
+      p.q_batch = (int64_t)p.s.seqlen_q * hd; p.q_row = hd; p.q_head = p.s.d;
+    }
+  }
   if (is_bf16) launch_bwd_t<true>(p, stream); else launch_bwd_t<false>(p, stream);
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) throw std::runtime_error(std::string("flash_attn_bwd launch: ") + hipGetErrorString(e));

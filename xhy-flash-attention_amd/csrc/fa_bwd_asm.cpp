@@ -73,9 +73,14 @@ struct DqAsmArgs {
   const void* o; int64_t o_batch;                                   // bytes
   int32_t o_row, o_head;                                            // bytes
   float* lsed; int32_t lsed_ng; float nrscale;                      // -1 / scale
+  // flags bit 2 (BwdParams::qfold): the kernel converts its Q fragments to bf16/f16(qc Q) -- the
+  // forward's rounded Q' -- and stores them to qf (compact rows) for the dK/dV kernel
+  void* qf; int64_t qf_batch;                                       // bytes
+  int32_t qf_row, qf_head;                                          // bytes
+  float qc; int32_t pad2;
 };
-static_assert(sizeof(DqAsmArgs) == 272 && offsetof(DqAsmArgs, dec) == 184 && offsetof(DqAsmArgs, o) == 232,
-              "DqAsmArgs layout");
+static_assert(sizeof(DqAsmArgs) == 304 && offsetof(DqAsmArgs, dec) == 184 && offsetof(DqAsmArgs, o) == 232 &&
+              offsetof(DqAsmArgs, qf) == 272, "DqAsmArgs layout");
 
 constexpr int kMaxDev = 64;
 constexpr int kBkn = 128;   // keys per workgroup
@@ -168,10 +173,16 @@ void launch_bwd_dkdv_asm(const BwdParams& p, bool is_bf16, hipStream_t stream) {
   a.q = p.q; a.k = p.k; a.v = p.v; a.dout = p.dout; a.dk = p.dk; a.dv = p.dv;
   a.lsed = p.lsed; a.sched = nullptr; a.cu_q = s.cu_seqlens_q; a.cu_k = s.cu_seqlens_k;
   a.q_batch = 2 * p.q_batch; a.k_batch = 2 * p.k_batch; a.v_batch = 2 * p.v_batch;
+  int64_t q_row = p.q_row, q_head = p.q_head;
+  if (p.qfold != nullptr) {   // the Q' the dQ kernel wrote (it ran first: fused preprocessing)
+    a.q = p.qfold;
+    a.q_batch = 2ll * s.seqlen_q * s.h * s.d;
+    q_row = (int64_t)s.h * s.d; q_head = s.d;
+  }
   a.do_batch = 2 * p.do_batch; a.dk_batch = 2 * p.dk_batch; a.dv_batch = 2 * p.dv_batch;
-  a.q_row = (int32_t)(2 * p.q_row); a.k_row = (int32_t)(2 * p.k_row); a.v_row = (int32_t)(2 * p.v_row);
+  a.q_row = (int32_t)(2 * q_row); a.k_row = (int32_t)(2 * p.k_row); a.v_row = (int32_t)(2 * p.v_row);
   a.do_row = (int32_t)(2 * p.do_row); a.dk_row = (int32_t)(2 * p.dk_row); a.dv_row = (int32_t)(2 * p.dv_row);
-  a.q_head = (int32_t)(2 * p.q_head); a.k_head = (int32_t)(2 * p.k_head); a.v_head = (int32_t)(2 * p.v_head);
+  a.q_head = (int32_t)(2 * q_head); a.k_head = (int32_t)(2 * p.k_head); a.v_head = (int32_t)(2 * p.v_head);
   a.do_head = (int32_t)(2 * p.do_head); a.dk_head = (int32_t)(2 * p.dk_head); a.dv_head = (int32_t)(2 * p.dv_head);
   a.sq = s.seqlen_q; a.sk = s.seqlen_k; a.h = s.h; a.ng = p.lsed_ng;
   a.group = s.h / s.hk;
@@ -236,8 +247,13 @@ void launch_bwd_dq_asm(const BwdParams& p, bool is_bf16, hipStream_t stream) {
   a.do_head = (int32_t)(2 * p.do_head); a.dq_head = (int32_t)(2 * p.dq_head);
   a.sq = s.seqlen_q; a.sk = s.seqlen_k; a.lse_pitch = s.lse_pitch; a.dsum_pitch = p.seqlen_q_rounded;
   a.h = s.h; a.hk = s.hk;
-  a.flags = (s.varlen_padded_input ? 1 : 0) | (p.fuse_pre ? 2 : 0);
+  a.flags = (s.varlen_padded_input ? 1 : 0) | (p.fuse_pre ? 2 : 0) | (p.qfold != nullptr ? 4 : 0);
   a.c = s.scale_log2; a.scale = p.dq_scale;
+  if (p.qfold != nullptr) {
+    a.qf = p.qfold;
+    a.qf_batch = 2ll * s.seqlen_q * s.h * s.d; a.qf_row = 2 * s.h * s.d; a.qf_head = 2 * s.d;
+    a.qc = p.qfold_c;
+  }
   a.o = p.o; a.o_batch = 2 * p.o_batch; a.o_row = (int32_t)(2 * p.o_row); a.o_head = (int32_t)(2 * p.o_head);
   a.lsed = p.lsed; a.lsed_ng = p.lsed_ng; a.nrscale = -1.0f / s.scale;
   a.dec = fwd_item_decode(s.b * s.h, s.h, s.h / s.hk, nmb, p.dq_head_group);

@@ -115,6 +115,11 @@ struct BwdParams {
   // Q' (q / q_* strides -> a prescaled copy), c -> 1 and scale -> ln 2 (dK = ln2 dS^T Q'), so the
   // recomputed P is the forward's P.
   float dq_scale;
+  // (the fold with the fused preprocessing) the assembly dQ kernel, which runs first, converts its Q
+  // fragments to bf16/f16(qfold_c Q) itself and stores them here (compact (b | padded rows,
+  // seqlen_q, h, d)); the assembly dK/dV kernel then reads Q' from here.  nullptr otherwise.
+  void* qfold;
+  float qfold_c;
 };
 
 // calc_reduced_attn_scores (fa_reduced.hip; reference reduced_scores::Params,
@@ -169,7 +174,8 @@ void bwd_block_size(int d, int* block_m, int* block_n);
 
 // Optional HIP-event timing around each kernel launch (fa_timing.cpp).
 enum TimedKernel { kTimeFwd = 0, kTimeBwdPre = 1, kTimeBwdMain = 2 /* dK/dV */, kTimeBwdDq = 3,
-                   kTimeBwdBoth = 4 /* dK/dV + dQ window */, kNumTimedKernels = 5 };
+                   kTimeBwdBoth = 4 /* dK/dV + dQ window */, kTimeQFold = 5 /* prescaled Q' (launch_bwd) */,
+                   kNumTimedKernels = 6 };
 void prof_begin(int id, hipStream_t s);
 void prof_end(int id, hipStream_t s);
 
