@@ -252,6 +252,7 @@ class K:
         self.name = f"fa_fwd_asm_d{D}_{self.ty}_{'causal' if causal else 'full'}"
         self.lines = []
         self.uid = 0
+        self.refit_regs = {}
 
     def lab(self, s):
         self.uid += 1
@@ -365,6 +366,15 @@ class K:
                 ops.append(self.cvt(preg + 4 * kkf + w, reg - 1, reg, key=k + kk + 3))
         return ops, last_sum
 
+    def touched(self, refit_label):
+        """the registers the out-of-line refit block at refit_label writes (scc, vcc, S_TMP, V_T, its
+        fragment ring, ...): its guard branch declares them as read and written, so the gap scheduler
+        keeps every filler that uses one of them wholly before or wholly after the branch -- an
+        s_cmp / s_cselect pair or an S_TMP temporary live across the branch would be clobbered when
+        the refit runs (found in the emulator: a refit between a slot advance's s_sub and its
+        s_cselect corrupted O)"""
+        return sorted(self.refit_regs.get(refit_label, ()))
+
     def guard_ops(self, j, refit_label, key, deadline=None):
         """partial sum <= 2^8 on every lane (and not NaN), else refit; then l += partial.  The branch
         and its return label are one instruction so that nothing is scheduled between them."""
@@ -375,7 +385,9 @@ class K:
         cmp = Inst(f"v_cmp_nge_f32_e32 vcc, 0x43800000, v{V_PS[j]}", VALU, rd=vr(V_PS[j]), wr=[("vcc", 0)],
                    key=key, deadline=deadline)
         sc = Inst("s_cmp_lg_u64 vcc, 0", SALU, rd=[("vcc", 0)], wr=[("scc", 0)], key=key, deadline=deadline)
-        br = Inst(f"s_cbranch_scc1 {refit_label}\n{refit_label}_back:", BRANCH, rd=[("scc", 0)], key=key, deadline=deadline)
+        tch = self.touched(refit_label)
+        br = Inst(f"s_cbranch_scc1 {refit_label}\n{refit_label}_back:", BRANCH, rd=[("scc", 0)] + tch, wr=tch,
+                  key=key, deadline=deadline)
         add = Inst(f"v_add_f32_e32 v{V_L[j]}, v{V_L[j]}, v{V_PS[j]}", VALU, rd=vr(V_L[j]) + vr(V_PS[j]),
                    wr=vr(V_L[j]), key=key, deadline=deadline)
         return [cmp, sc, br, add]
@@ -387,8 +399,9 @@ class K:
 
     def guard_br(self, j, refit_label, key, deadline=None, eg=None):
         """(FA_GEN_GUARD2) branch to the refit on vcc (all lanes are active), then l += partial"""
-        br = Inst(f"s_cbranch_vccnz {refit_label}\n{refit_label}_back:", BRANCH, rd=[("vcc", 0)], key=key,
-                  deadline=deadline, earliest=eg)
+        tch = self.touched(refit_label)
+        br = Inst(f"s_cbranch_vccnz {refit_label}\n{refit_label}_back:", BRANCH, rd=[("vcc", 0)] + tch, wr=tch,
+                  key=key, deadline=deadline, earliest=eg)
         add = Inst(f"v_add_f32_e32 v{V_L[j]}, v{V_L[j]}, v{V_PS[j]}", VALU, rd=vr(V_L[j]) + vr(V_PS[j]),
                    wr=vr(V_L[j]), key=key, deadline=deadline, earliest=eg)
         return [br, add]
@@ -760,6 +773,7 @@ class K:
         ins.append(Inst(f"s_branch {lab}_back", BRANCH))
         out, _ = add_waits(ins)
         out, _ = fix_hazards(out)
+        self.refit_regs[lab] = set().union(*(i.wr for i in out))
         return out
 
     def m_tile_ops(self, j, key=0):
@@ -767,27 +781,77 @@ class K:
         return [Inst(f"v_mov_b32_e32 v{V_M[j] + g}, v{V_NEGMC[j]}", VALU, rd=vr(V_NEGMC[j]), wr=vr(V_M[j] + g), key=key)
                 for g in range(16)]
 
-    def q_scale_ops(self):
-        """(fold) Q fragments (AGPRs, as loaded) -> bf16/f16(c Q), RNE, via v0..95 (free at tile 0)"""
+    def q_scale_ops(self, j, X, LO, key=0, deadline=None):
+        """(fold) q-block j's Q fragments (AGPRs, as loaded) -> bf16/f16(c Q), round to nearest even,
+        through v[X..X+4KS) and v[LO..LO+4KS): lo half into LO, hi half in place, the pack into LO"""
         I = Inst
-        ops = []
         n = 4 * KS
-        X, LO, HI = 0, 32, 64
-        for j in range(2):
-            q0 = Q_(j, 0)
-            ops += [I(f"v_accvgpr_read_b32 v{X + i}, a{q0 + i}", ACCR, rd=ar(q0 + i), wr=vr(X + i)) for i in range(n)]
-            if self.bf16:
-                ops += [I(f"v_lshlrev_b32_e32 v{LO + i}, 16, v{X + i}", VALU, rd=vr(X + i), wr=vr(LO + i)) for i in range(n)]
-                ops += [I(f"v_and_b32_e32 v{HI + i}, 0xffff0000, v{X + i}", VALU, rd=vr(X + i), wr=vr(HI + i)) for i in range(n)]
-            else:
-                ops += [I(f"v_cvt_f32_f16_e32 v{LO + i}, v{X + i}", VALU, rd=vr(X + i), wr=vr(LO + i)) for i in range(n)]
-                ops += [I(f"v_lshrrev_b32_e32 v{HI + i}, 16, v{X + i}", VALU, rd=vr(X + i), wr=vr(HI + i)) for i in range(n)]
-                ops += [I(f"v_cvt_f32_f16_e32 v{HI + i}, v{HI + i}", VALU, rd=vr(HI + i), wr=vr(HI + i)) for i in range(n)]
-            for R in (LO, HI):
-                ops += [I(f"v_mul_f32_e32 v{R + i}, s{S_C}, v{R + i}", VALU, rd=sr(S_C) + vr(R + i), wr=vr(R + i)) for i in range(n)]
-            ops += [self.cvt(X + i, LO + i, HI + i) for i in range(n)]
-            ops += [I(f"v_accvgpr_write_b32 a{q0 + i}, v{X + i}", ACCW, rd=vr(X + i), wr=ar(q0 + i)) for i in range(n)]
+        q0 = Q_(j, 0)
+        kw = dict(key=key, deadline=deadline)
+        ops = [I(f"v_accvgpr_read_b32 v{X + i}, a{q0 + i}", ACCR, rd=ar(q0 + i), wr=vr(X + i), **kw) for i in range(n)]
+        if self.bf16:
+            ops += [I(f"v_lshlrev_b32_e32 v{LO + i}, 16, v{X + i}", VALU, rd=vr(X + i), wr=vr(LO + i), **kw) for i in range(n)]
+            ops += [I(f"v_and_b32_e32 v{X + i}, 0xffff0000, v{X + i}", VALU, rd=vr(X + i), wr=vr(X + i), **kw) for i in range(n)]
+        else:
+            ops += [I(f"v_cvt_f32_f16_e32 v{LO + i}, v{X + i}", VALU, rd=vr(X + i), wr=vr(LO + i), **kw) for i in range(n)]
+            ops += [I(f"v_lshrrev_b32_e32 v{X + i}, 16, v{X + i}", VALU, rd=vr(X + i), wr=vr(X + i), **kw) for i in range(n)]
+            ops += [I(f"v_cvt_f32_f16_e32 v{X + i}, v{X + i}", VALU, rd=vr(X + i), wr=vr(X + i), **kw) for i in range(n)]
+        for R in (LO, X):
+            ops += [I(f"v_mul_f32_e32 v{R + i}, s{S_C}, v{R + i}", VALU, rd=sr(S_C) + vr(R + i), wr=vr(R + i), **kw)
+                    for i in range(n)]
+        ops += [self.cvt(LO + i, LO + i, X + i, **kw) for i in range(n)]
+        ops += [I(f"v_accvgpr_write_b32 a{q0 + i}, v{LO + i}", ACCW, rd=vr(LO + i), wr=ar(q0 + i), **kw) for i in range(n)]
         return ops
+
+    def tile0_fold(self, l_entry_last, l_entry_fast, l_entry_masked):
+        """(fold) tile 0 with the Q conversion overlapped: q-block a's Q is converted first, then
+        S(0, a) runs its MFMAs while q-block b's Q is converted in their gaps, and S(0, b) runs while
+        a's mask, row max, -c m and P(0, a) fill its gaps (at d = 128 the K fragments are read again
+        for b: the 8-slot ring does not hold all 16).  S(0, b) then gets its own max, its -c m added
+        (the first step's softmax takes scores from a V_M-started chain) and both V_M tiles are set."""
+        I = Inst
+        if OPT_T0STAMP:
+            ins = (self.stamp_point(9) + [I(f"s_waitcnt vmcnt({2 * NP})", WAIT)] + self.stamp_point(6) +
+                   [I("s_barrier", BARRIER)] + self.stamp_point(5))
+        else:
+            ins = [I(f"s_waitcnt vmcnt({2 * NP})", WAIT), I("s_barrier", BARRIER)]
+            ins += [] if OPT_EPISTAMP else self.stamp_point(9)
+        ins += self.dump("pro_lds")
+        ins += self.q_scale_ops(0, 0, 32)
+        ins += [I(f"v_add_u32_e32 v{V_KB0}, s{S_KOFF}, v{V_RB0}", VALU, rd=sr(S_KOFF) + vr(V_RB0), wr=vr(V_KB0)),
+                I(f"v_add_u32_e32 v{V_KB1}, s{S_KOFF}, v{V_RB1}", VALU, rd=sr(S_KOFF) + vr(V_RB1), wr=vr(V_KB1))]
+        n2 = 2 * KS
+        mfm = []
+        for j in range(2):
+            for f in range(n2):
+                st, ks = f // KS, f % KS
+                mfm.append(self.mfma_s((SA if j == 0 else SB(0)) + 16 * st, f % 8, j, ks, ks == 0))
+        fill = []
+        for f in range(n2):
+            fill.append(self.kread(f, f % 8, key=-100 + f, earliest=(f - 8) if f >= 8 else None, deadline=max(f - 2, 0)))
+        if n2 > 8:
+            for f in range(n2):
+                fill.append(self.kread(f, f % 8, key=-60 + f, earliest=f + 8, deadline=n2 + f - 2))
+        # q-block b's Q (temporaries: S(b) buffer 1 and the P(a) packs, idle in tile 0)
+        fill += self.q_scale_ops(1, SB(1), PA(0), key=0, deadline=n2)
+        if OPT_T0ZERO:
+            fill += self.o_zero_ops(key=100)
+        tail = self.tile0_maxops(0, SA, key=400)
+        tail += self.softmax_ops(0, SA, PA(0), False, None, key0=600, fold_add=True)[0]
+        tail += [Inst(f"v_mov_b32_e32 v{V_L[0]}, v{V_PS[0]}", VALU, rd=vr(V_PS[0]), wr=vr(V_L[0]), key=900)]
+        for op in tail:
+            op.eg = n2 - 1     # after S(0, a)'s last MFMA
+        fill += tail
+        ins += schedule(mfm, fill) + [nop(15)]
+        ins += self.dump("pro_qk")
+        ins += self.tile0_maxops(1, SB(0), key=0)
+        ins += [Inst(f"v_add_f32_e32 v{SB(0) + e}, v{V_NEGMC[1]}, v{SB(0) + e}", VALU,
+                     rd=vr(V_NEGMC[1]) + vr(SB(0) + e), wr=vr(SB(0) + e)) for e in range(32)]
+        ins += self.m_tile_ops(0) + self.m_tile_ops(1)
+        ins += self.dump("pro_end")
+        ins += [] if (OPT_EPISTAMP or OPT_T0STAMP) else self.stamp_point(6)
+        ins += self.tile0_exit(l_entry_last, l_entry_fast, l_entry_masked)
+        return ins
 
     def dump(self, point):
         """register / LDS dump of workgroup 0 at `point` (OPT_DUMP), then s_endpgm"""
@@ -1268,6 +1332,8 @@ class K:
     def tile0(self, l_entry_last, l_entry_fast, l_entry_masked, stores=False):
         """Q + tiles 0, 1, 2 landed (tile 3 in flight); tile 0: S(0, a), S(0, b) -> masked, explicit
         row max, P(0, a); then into the step loop"""
+        if OPT_FOLD:
+            return self.tile0_fold(l_entry_last, l_entry_fast, l_entry_masked)
         I = Inst
         if OPT_T0STAMP:
             ins = (self.stamp_point(9) + [I(f"s_waitcnt vmcnt({2 * NP})", WAIT)] + self.stamp_point(6) +
@@ -1276,8 +1342,6 @@ class K:
             ins = [I(f"s_waitcnt vmcnt({2 * NP})", WAIT), I("s_barrier", BARRIER)]
             ins += [] if OPT_EPISTAMP else self.stamp_point(9)
         ins += self.dump("pro_lds")
-        if OPT_FOLD:
-            ins += self.q_scale_ops()
         ins += [I(f"v_add_u32_e32 v{V_KB0}, s{S_KOFF}, v{V_RB0}", VALU, rd=sr(S_KOFF) + vr(V_RB0), wr=vr(V_KB0)),
                 I(f"v_add_u32_e32 v{V_KB1}, s{S_KOFF}, v{V_RB1}", VALU, rd=sr(S_KOFF) + vr(V_RB1), wr=vr(V_KB1))]
         mfm = []
@@ -1312,27 +1376,25 @@ class K:
                 else:
                     ins.append(Inst(f"v_max_f32_e32 v{mx}, v{mx}, v{sreg + e}", VALU, rd=vr(mx) + vr(sreg + e), wr=vr(mx)))
             ins += self.half_max(mx, V_T + 3)
-            # negmc = m == -inf ? 0 : -m c   (fold: the scores are c S already)
-            if OPT_FOLD:
-                ins += [Inst(f"v_sub_f32_e32 v{V_NEGMC[j]}, 0, v{mx}", VALU, rd=vr(mx), wr=vr(V_NEGMC[j]))]
-            else:
-                ins += [Inst(f"v_mul_f32_e32 v{V_T + 4}, s{S_C}, v{mx}", VALU, rd=sr(S_C) + vr(mx), wr=vr(V_T + 4)),
-                        Inst(f"v_sub_f32_e32 v{V_NEGMC[j]}, 0, v{V_T + 4}", VALU, rd=vr(V_T + 4), wr=vr(V_NEGMC[j]))]
-            ins += [Inst(f"v_cmp_eq_f32_e32 vcc, v{V_NINF}, v{mx}", VALU, rd=vr(V_NINF) + vr(mx), wr=[("vcc", 0)]),
+            # negmc = m == -inf ? 0 : -m c
+            ins += [Inst(f"v_mul_f32_e32 v{V_T + 4}, s{S_C}, v{mx}", VALU, rd=sr(S_C) + vr(mx), wr=vr(V_T + 4)),
+                    Inst(f"v_sub_f32_e32 v{V_NEGMC[j]}, 0, v{V_T + 4}", VALU, rd=vr(V_T + 4), wr=vr(V_NEGMC[j])),
+                    Inst(f"v_cmp_eq_f32_e32 vcc, v{V_NINF}, v{mx}", VALU, rd=vr(V_NINF) + vr(mx), wr=[("vcc", 0)]),
                     Inst(f"v_cndmask_b32_e64 v{V_NEGMC[j]}, v{V_NEGMC[j]}, 0, vcc", VALU,
                          rd=vr(V_NEGMC[j]) + [("vcc", 0)], wr=vr(V_NEGMC[j]))]
-        if OPT_FOLD:
-            # S(0, b) -> c S - c m (its softmax runs in the first step, which takes the scores as
-            # they leave a V_M-started chain); the chain-start tiles of both q-blocks
-            ins += [Inst(f"v_add_f32_e32 v{SB(0) + e}, v{V_NEGMC[1]}, v{SB(0) + e}", VALU,
-                         rd=vr(V_NEGMC[1]) + vr(SB(0) + e), wr=vr(SB(0) + e)) for e in range(32)]
-            ins += self.m_tile_ops(0) + self.m_tile_ops(1)
         if not OPT_T0OV:
-            sm, _ = self.softmax_ops(0, SA, PA(0), False, None, key0=0, fold_add=OPT_FOLD)
+            sm, _ = self.softmax_ops(0, SA, PA(0), False, None, key0=0)
             ins += sm
             ins += [Inst(f"v_mov_b32_e32 v{V_L[0]}, v{V_PS[0]}", VALU, rd=vr(V_PS[0]), wr=vr(V_L[0]))]
         ins += self.dump("pro_end")
         ins += [] if (OPT_EPISTAMP or OPT_T0STAMP) else self.stamp_point(6)
+        ins += self.tile0_exit(l_entry_last, l_entry_fast, l_entry_masked)
+        return ins
+
+    def tile0_exit(self, l_entry_last, l_entry_fast, l_entry_masked):
+        """end of tile 0: V read slot, K(1) base and its first fragments, into the step loop"""
+        I = Inst
+        ins = []
         # V reads tile 0 (slot S_KOFF); S_KOFF -> tile 1 (the LAST step's refit takes S_KOFF - TILE)
         ins += [I(f"s_add_u32 s{S_VOFF}, s{S_KOFF}, {VBASE}", SALU),
                 I(f"s_add_u32 s{S_KOFF}, s{S_KOFF}, {TILE}", SALU),
@@ -1366,9 +1428,12 @@ class K:
         for op in self.half_max(mx, V_T + 3):
             op.key = key + 200
             ops.append(op)
-        ops += [Inst(f"v_mul_f32_e32 v{V_T + 4}, s{S_C}, v{mx}", VALU, rd=sr(S_C) + vr(mx), wr=vr(V_T + 4), key=key + 200),
-                Inst(f"v_sub_f32_e32 v{V_NEGMC[j]}, 0, v{V_T + 4}", VALU, rd=vr(V_T + 4), wr=vr(V_NEGMC[j]), key=key + 200),
-                Inst(f"v_cmp_eq_f32_e32 vcc, v{V_NINF}, v{mx}", VALU, rd=vr(V_NINF) + vr(mx), wr=[("vcc", 0)], key=key + 200),
+        if OPT_FOLD:   # (the scores are c S already)
+            ops += [Inst(f"v_sub_f32_e32 v{V_NEGMC[j]}, 0, v{mx}", VALU, rd=vr(mx), wr=vr(V_NEGMC[j]), key=key + 200)]
+        else:
+            ops += [Inst(f"v_mul_f32_e32 v{V_T + 4}, s{S_C}, v{mx}", VALU, rd=sr(S_C) + vr(mx), wr=vr(V_T + 4), key=key + 200),
+                    Inst(f"v_sub_f32_e32 v{V_NEGMC[j]}, 0, v{V_T + 4}", VALU, rd=vr(V_T + 4), wr=vr(V_NEGMC[j]), key=key + 200)]
+        ops += [Inst(f"v_cmp_eq_f32_e32 vcc, v{V_NINF}, v{mx}", VALU, rd=vr(V_NINF) + vr(mx), wr=[("vcc", 0)], key=key + 200),
                 Inst(f"v_cndmask_b32_e64 v{V_NEGMC[j]}, v{V_NEGMC[j]}, 0, vcc", VALU,
                      rd=vr(V_NEGMC[j]) + [("vcc", 0)], wr=vr(V_NEGMC[j]), key=key + 200)]
         return ops
@@ -1634,6 +1699,7 @@ class K:
     # ------------------------------------------------------------------ whole kernel
     def build(self):
         self.switches = []
+        self.refit_regs = {}
         l_end = self.lab("end")
         self.l_tile0w = self.lab("tile0w")
         self.l_empty = self.lab("empty")
