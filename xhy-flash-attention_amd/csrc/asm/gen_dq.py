@@ -649,46 +649,60 @@ class K:
         ins += [label(l_nof)]
         return ins
 
-    def q_fold(self):
-        """(flags bit 2) the backward of a forward that held Q as bf16/f16(c Q) (gen_fwd.py FA_GEN_FOLD,
-        launch_bwd): the Q fragments become bf16/f16(qc Q) -- v_mul_f32 by qc and a round-to-nearest-
-        even pack, the forward's own q_scale_ops, so the scores S^T = K Q'^T (c = 1 on this launch)
-        are bitwise the forward's -- and Q' is stored for the dK/dV kernel (descriptor s[56:59],
-        qf_row s60, qc s62; rows past seqlen_q fall outside the records).  Runs once per item after
-        the prologue's wait (the Q loads landed), in v[0:95] (the S^T / dP^T tiles, idle here)."""
+    def q_fold_setup(self):
+        """(the Q fold) lane offsets of the Q' stores: (64 w + 32 j + r) qf_row + 16 hh -> v[V_TMP + 2 + j]"""
         I = Inst
-        l_no = self.lab("noqfold")
         r_, hh, x = V_TMP, V_TMP + 1, V_TMP + 2
-        ins = [I("s_bitcmp1_b32 s99, 2", SALU, rd=sr(99), wr=[("scc", 0)]), I(f"s_cbranch_scc0 {l_no}", BRANCH),
-               I(f"v_and_b32_e32 v{r_}, 31, v{V_LANE}", VALU, rd=vr(V_LANE), wr=vr(r_)),
+        ins = [I(f"v_and_b32_e32 v{r_}, 31, v{V_LANE}", VALU, rd=vr(V_LANE), wr=vr(r_)),
                I(f"v_lshrrev_b32_e32 v{hh}, 5, v{V_LANE}", VALU, rd=vr(V_LANE), wr=vr(hh)),
                I(f"s_lshl_b32 s{S_TMP}, s{S_WAVE}, 6", SALU, rd=sr(S_WAVE), wr=sr(S_TMP))]
-        n = 4 * KS
-        X, LO, HI = 0, 32, 64
         for j in range(2):
             off = x + j
             ins += [I(f"v_add_u32_e32 v{off}, s{S_TMP}, v{r_}", VALU, rd=sr(S_TMP) + vr(r_), wr=vr(off)),
                     I(f"v_add_u32_e32 v{off}, {32 * j}, v{off}", VALU, rd=vr(off), wr=vr(off)),
                     I(f"v_mul_lo_u32 v{off}, v{off}, s60", VALU, rd=vr(off) + sr(60), wr=vr(off)),
                     I(f"v_lshl_add_u32 v{off}, v{hh}, 4, v{off}", VALU, rd=vr(hh) + vr(off), wr=vr(off))]
-            q0 = QF(j, 0)
-            ins += [I(f"v_accvgpr_read_b32 v{X + i}, a{q0 + i}", ACCR, rd=ar(q0 + i), wr=vr(X + i)) for i in range(n)]
-            if self.bf16:
-                ins += [I(f"v_lshlrev_b32_e32 v{LO + i}, 16, v{X + i}", VALU, rd=vr(X + i), wr=vr(LO + i)) for i in range(n)]
-                ins += [I(f"v_and_b32_e32 v{HI + i}, 0xffff0000, v{X + i}", VALU, rd=vr(X + i), wr=vr(HI + i)) for i in range(n)]
-            else:
-                ins += [I(f"v_cvt_f32_f16_e32 v{LO + i}, v{X + i}", VALU, rd=vr(X + i), wr=vr(LO + i)) for i in range(n)]
-                ins += [I(f"v_lshrrev_b32_e32 v{HI + i}, 16, v{X + i}", VALU, rd=vr(X + i), wr=vr(HI + i)) for i in range(n)]
-                ins += [I(f"v_cvt_f32_f16_e32 v{HI + i}, v{HI + i}", VALU, rd=vr(HI + i), wr=vr(HI + i)) for i in range(n)]
-            for R in (LO, HI):
-                ins += [I(f"v_mul_f32_e32 v{R + i}, s62, v{R + i}", VALU, rd=sr(62) + vr(R + i), wr=vr(R + i)) for i in range(n)]
-            ins += [self.cvt(X + i, LO + i, HI + i) for i in range(n)]
-            ins += [I(f"v_accvgpr_write_b32 a{q0 + i}, v{X + i}", ACCW, rd=vr(X + i), wr=ar(q0 + i)) for i in range(n)]
-            ins += [I(f"buffer_store_dwordx4 v[{X + 4 * ks}:{X + 4 * ks + 3}], v{off}, s[56:59], 0 offen offset:{32 * ks}",
-                      VSTORE, rd=vr(X + 4 * ks, 4) + vr(off) + sr(56, 4)) for ks in range(KS)]
-            # (the next q-block's loads of v[0:31]: the stores read their data at issue -- WAR 2)
-        ins += [label(l_no)]
         return ins
+
+    def q_fold_fill(self):
+        """(flags bit 2) the backward of a forward that held Q as bf16/f16(c Q) (gen_fwd.py FA_GEN_FOLD,
+        launch_bwd): each Q fragment becomes bf16/f16(qc Q) -- v_mul_f32 by qc and a round-to-nearest-
+        even pack, the forward's own q_scale_ops, so the scores S^T = K Q'^T (c = 1 on this launch)
+        are bitwise the forward's -- before the phase -1 MFMA that reads it (fillers with deadlines:
+        the conversion hides in the phase's gaps), and Q' is stored for the dK/dV kernel (descriptor
+        s[56:59], qc s62; rows past seqlen_q fall outside the records).  Temporaries: the idle S^T /
+        dP^T buffers 1 (v[32:63], v[96:127]), 8 rotating 4-register slots."""
+        I = Inst
+        x = V_TMP + 2
+        ops = []
+        for ks in range(KS):
+            for j in range(2):
+                slot = (2 * ks + j) % 8
+                X, LO = 32 + 4 * slot, 96 + 4 * slot
+                q = QF(j, ks)
+                kw = dict(key=-150 + 8 * ks + 2 * j, deadline=4 * ks + j)
+                ops += [I(f"v_accvgpr_read_b32 v{X + i}, a{q + i}", ACCR, rd=ar(q + i), wr=vr(X + i), **kw) for i in range(4)]
+                if self.bf16:
+                    ops += [I(f"v_lshlrev_b32_e32 v{LO + i}, 16, v{X + i}", VALU, rd=vr(X + i), wr=vr(LO + i), **kw)
+                            for i in range(4)]
+                    ops += [I(f"v_and_b32_e32 v{X + i}, 0xffff0000, v{X + i}", VALU, rd=vr(X + i), wr=vr(X + i), **kw)
+                            for i in range(4)]
+                else:
+                    ops += [I(f"v_cvt_f32_f16_e32 v{LO + i}, v{X + i}", VALU, rd=vr(X + i), wr=vr(LO + i), **kw)
+                            for i in range(4)]
+                    ops += [I(f"v_lshrrev_b32_e32 v{X + i}, 16, v{X + i}", VALU, rd=vr(X + i), wr=vr(X + i), **kw)
+                            for i in range(4)]
+                    ops += [I(f"v_cvt_f32_f16_e32 v{X + i}, v{X + i}", VALU, rd=vr(X + i), wr=vr(X + i), **kw)
+                            for i in range(4)]
+                for R in (LO, X):
+                    ops += [I(f"v_mul_f32_e32 v{R + i}, s62, v{R + i}", VALU, rd=sr(62) + vr(R + i), wr=vr(R + i), **kw)
+                            for i in range(4)]
+                ops += [self.cvt(LO + i, LO + i, X + i, **kw) for i in range(4)]
+                ops += [I(f"v_accvgpr_write_b32 a{q + i}, v{LO + i}", ACCW, rd=vr(LO + i), wr=ar(q + i), **kw)
+                        for i in range(4)]
+                ops.append(I(f"buffer_store_dwordx4 v[{LO}:{LO + 3}], v{x + j}, s[56:59], 0 offen offset:{32 * ks}",
+                             VSTORE, rd=vr(LO, 4) + vr(x + j) + sr(56, 4), key=kw["key"] + 1))
+        return ops
 
     def epilogue(self):
         """dQ = scale dQ^T^T in bf16 / f16, rows < seqlen_q (range-checked; rows on lanes as gen_fwd.py)"""
@@ -711,6 +725,35 @@ class K:
                     ins.append(I(f"buffer_store_dwordx4 v[{w}:{w + 3}], v{V_QOFF[j]}, s[92:95], 0 offen offset:{64 * dt + 16 * u}",
                                  VSTORE, rd=vr(w, 4) + vr(V_QOFF[j]) + sr(92, 4)))
         return ins
+
+    def phase_m1(self, fold):
+        """phase -1: S^T / dP^T(0) -> buffers 0, then the first step's wait and barrier"""
+        # -LSE log2 e (LSE = +inf -> -inf: P = 0); the loads landed with the prologue's wait
+        ph = [Inst(f"v_mul_f32_e32 v{V_NLC[j]}, 0xbfb8aa3b, v{V_NLC[j]}", VALU, rd=vr(V_NLC[j]), wr=vr(V_NLC[j]), key=-500)
+              for j in range(2)]
+        ph += [Inst(f"s_mov_b32 s{S_SROW}, 0", SALU, wr=sr(S_SROW)),
+               Inst(f"s_mov_b32 s{S_STR}, {RING - 2 * SLOT}", SALU, wr=sr(S_STR)),
+               Inst(f"v_add_u32_e32 v{V_KB0}, 0, v{V_RB0}", VALU, rd=vr(V_RB0), wr=vr(V_KB0)),
+               Inst(f"v_add_u32_e32 v{V_KB1}, 0, v{V_RB1}", VALU, rd=vr(V_RB1), wr=vr(V_KB1))]
+        mf, frags = self.phase_mfmas(1, True, False)
+        fill = []
+        for f, (t, i) in enumerate(frags):
+            fill += self.frag_reads(f, t, i, key=-100 + f, deadline=max(2 * f - OPT_LEAD, 0))
+        if fold:
+            fill += self.q_fold_fill()
+        fill += self.slot_advance(S_SROW, key=400) + self.slot_advance(S_STR, key=400)
+        fill += [Inst(f"v_add_u32_e32 v{V_KB0}, s{S_SROW}, v{V_RB0}", VALU, rd=sr(S_SROW) + vr(V_RB0), wr=vr(V_KB0), key=401),
+                 Inst(f"v_add_u32_e32 v{V_KB1}, s{S_SROW}, v{V_RB1}", VALU, rd=sr(S_SROW) + vr(V_RB1), wr=vr(V_KB1), key=401),
+                 Inst(f"v_add_u32_e32 v{V_VB0}, s{S_STR}, v{V_TB0}", VALU, rd=sr(S_STR) + vr(V_TB0), wr=vr(V_VB0), key=401),
+                 Inst(f"v_add_u32_e32 v{V_VB1}, s{S_STR}, v{V_TB1}", VALU, rd=sr(S_STR) + vr(V_TB1), wr=vr(V_VB1), key=401)]
+        nfr = self.phase_frags(True, False)
+        for f in range(3):
+            t, i = nfr[f]
+            fill += self.frag_reads(f, t, i, key=600 + f, earliest=2 * f + 1)
+        sch = schedule(mf, ph + fill)
+        # (the fold's 16 Q' stores are younger than the K / V DMAs this wait is about)
+        sch += [Inst(f"s_waitcnt vmcnt({VMCNT_STEP + (2 * KS if fold else 0)}) lgkmcnt(0)", WAIT), Inst("s_barrier", BARRIER)]
+        return sch
 
     # ------------------------------------------------------------------ whole kernel
     def build(self):
@@ -746,35 +789,18 @@ class K:
         # K / V(0) and (1) landed (phase -1 reads 0, its tail prefetches 1): 16 younger DMAs
         pro += [Inst("s_waitcnt vmcnt(16)", WAIT), Inst("s_barrier", BARRIER)]
         pro += self.fused_d()
-        pro += self.q_fold()
         # no keys: epilogue (dQ = 0), after the fused D (softmax_d and the scratch are still written)
         pro += [Inst(f"s_cmp_lt_i32 s{S_NLAST}, 0", SALU, rd=sr(S_NLAST), wr=[("scc", 0)]),
                 Inst(f"s_cbranch_scc1 {l_epi}", BRANCH)]
         emit(pro, pre=[nop(15)])
-        # phase -1: S^T / dP^T(0) -> buffers 0
-        # -LSE log2 e (LSE = +inf -> -inf: P = 0); the loads landed with the prologue's wait
-        ph = [Inst(f"v_mul_f32_e32 v{V_NLC[j]}, 0xbfb8aa3b, v{V_NLC[j]}", VALU, rd=vr(V_NLC[j]), wr=vr(V_NLC[j]), key=-500)
-              for j in range(2)]
-        ph += [Inst(f"s_mov_b32 s{S_SROW}, 0", SALU, wr=sr(S_SROW)),
-              Inst(f"s_mov_b32 s{S_STR}, {RING - 2 * SLOT}", SALU, wr=sr(S_STR)),
-              Inst(f"v_add_u32_e32 v{V_KB0}, 0, v{V_RB0}", VALU, rd=vr(V_RB0), wr=vr(V_KB0)),
-              Inst(f"v_add_u32_e32 v{V_KB1}, 0, v{V_RB1}", VALU, rd=vr(V_RB1), wr=vr(V_KB1))]
-        mf, frags = self.phase_mfmas(1, True, False)
-        fill = []
-        for f, (t, i) in enumerate(frags):
-            fill += self.frag_reads(f, t, i, key=-100 + f, deadline=max(2 * f - OPT_LEAD, 0))
-        fill += self.slot_advance(S_SROW, key=400) + self.slot_advance(S_STR, key=400)
-        fill += [Inst(f"v_add_u32_e32 v{V_KB0}, s{S_SROW}, v{V_RB0}", VALU, rd=sr(S_SROW) + vr(V_RB0), wr=vr(V_KB0), key=401),
-                 Inst(f"v_add_u32_e32 v{V_KB1}, s{S_SROW}, v{V_RB1}", VALU, rd=sr(S_SROW) + vr(V_RB1), wr=vr(V_KB1), key=401),
-                 Inst(f"v_add_u32_e32 v{V_VB0}, s{S_STR}, v{V_TB0}", VALU, rd=sr(S_STR) + vr(V_TB0), wr=vr(V_VB0), key=401),
-                 Inst(f"v_add_u32_e32 v{V_VB1}, s{S_STR}, v{V_TB1}", VALU, rd=sr(S_STR) + vr(V_TB1), wr=vr(V_VB1), key=401)]
-        nfr = self.phase_frags(True, False)
-        for f in range(3):
-            t, i = nfr[f]
-            fill += self.frag_reads(f, t, i, key=600 + f, earliest=2 * f + 1)
-        sch = schedule(mf, ph + fill)
-        sch += [Inst(f"s_waitcnt vmcnt({VMCNT_STEP}) lgkmcnt(0)", WAIT), Inst("s_barrier", BARRIER)]
-        emit(sch, pre=[nop(15)])
+        # phase -1: S^T / dP^T(0) -> buffers 0; with the Q fold (flags bit 2) a variant that converts
+        # the Q fragments in its gaps (q_fold_fill)
+        l_fold, l_after = self.lab("ph1fold"), self.lab("ph1done")
+        code += [Inst("s_bitcmp1_b32 s99, 2", SALU), Inst(f"s_cbranch_scc1 {l_fold}", BRANCH)]
+        emit(self.phase_m1(False) + [Inst(f"s_branch {l_after}", BRANCH)], pre=[nop(15)])
+        code.append(label(l_fold))
+        emit(self.q_fold_setup() + self.phase_m1(True), pre=[nop(15)])
+        code.append(label(l_after))
         L = {}
         variants = [(f, l, m) for f in (True, False) for l in (True, False) for m in ((True, False) if self.causal else (False,))]
         for v in variants:
