@@ -51,16 +51,21 @@ def main(path, b=4, s=8192, h=16, c4=False):
         torch.cuda.synchronize()
     lib.flash_attn_debug_bwd_stamps(ctypes.c_void_p(0))
     if steps:   # FA_GBW_STAMP=2: per wave {compute, wait, barrier, steps, -, prologue, epilogue, items}
-        a = buf.cpu().numpy().view(np.uint32).reshape(nwg * 4, 16)[:, :8].astype(np.int64)
+        a = buf.cpu().numpy().view(np.uint32).reshape(nwg * 4, 16).astype(np.int64)
         a = a[a[:, 7] > 0]
         st = np.maximum(a[:, 3], 1)
         it = np.maximum(a[:, 7], 1)
-        tot = a[:, 0] + a[:, 1] + a[:, 2] + a[:, 5] + a[:, 6]
+        tot = a[:, 0] + a[:, 1] + a[:, 2] + a[:, 5] + a[:, 6] + a[:, 10:16].sum(1)
+        a[:, 5] += a[:, 10:16].sum(1)   # the prologue: its parts (10..15) and phase -1 (5)
         print(f"waves {len(a)}, items per wave med {np.median(a[:, 7]):.0f}, steps per wave med {np.median(a[:, 3]):.0f}")
         for i, nm in ((0, "compute"), (1, "vmwait"), (2, "barrier")):
             print(f"  {nm}: per step med {np.median(a[:, i] / st):.0f} cycles, share {np.median(a[:, i] / tot):.3f}")
         for i, nm in ((5, "prologue"), (6, "tail+epilogue")):
             print(f"  {nm}: per item med {np.median(a[:, i] / it):.0f} cycles, share {np.median(a[:, i] / tot):.3f}")
+        for i, nm in ((10, "head (barrier, item)"), (11, "kernargs + work order"), (12, "geometry"),
+                      (13, "K / V loads + lane values"), (14, "DMA issue"), (15, "first wait + barrier")):
+            print(f"    prologue part {nm}: per item med {np.median(a[:, i] / it):.0f} cycles")
+        print(f"    prologue part phase -1 + wait: per item med {np.median((a[:, 5] - a[:, 10:16].sum(1)) / it):.0f} cycles")
         print(f"  total per wave med {np.median(tot):.0f} cycles; ideal MFMA cycles per step 2048 (64 MFMAs)")
         return
     start = a[:, 0].astype(np.int64) | (a[:, 1].astype(np.int64) << 32)

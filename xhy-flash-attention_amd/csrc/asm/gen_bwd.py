@@ -157,7 +157,9 @@ OPT_ZLATE = os.environ.get("FA_GBW_ZEARLY") != "1"
 # ablations (wrong results; which resource bounds the steady state): novalu / nofrag / nodma
 OPT_ABL = os.environ.get("FA_GBW_ABL", "")
 V_SS = 186             # 186..193: compute, wait, barrier, steps, last stamp, prologue, epilogue, items
-                       # (194, 195: temporaries)
+                       # (194, 195: temporaries); 196..201: the prologue's parts (head, kernargs + work
+                       # order, geometry, fragment loads + lane values, DMA issue, first wait; phase -1 is
+                       # `prologue` above)
 V_ROUND = 184          # round r of the persistent item loop (uniform)
 S_ITEM = 28            # the item index, until the sweep geometry takes the register (S_QF)
 V_STAMP = 164          # 164..177: start lo / hi, HW_ID, XCC_ID, wg, end lo / hi, wave, -, -, loop start lo / hi,
@@ -493,6 +495,7 @@ class K:
         ins += [I(f"s_load_dwordx8 s[36:43], s[0:1], {DEC_OFF}", SMEM),
                 I(f"s_load_dwordx2 s[44:45], s[0:1], {DEC_OFF + 32}", SMEM),
                 I("s_waitcnt lgkmcnt(0)", WAIT)]
+        ins += self.stamp(V_SS + 11)
         BIDB, HX, KVH, KB = 24, 25, 26, 27      # S_N .. S_Q0V, set at the end
         ins += item_decode_ops(L=S_ITEM, M=36, pa=T1, pb=T3, t=T5, u=T6, o_blk=KB, reverse=False)
         ins += [I(f"s_mov_b32 s{BIDB}, s{T3}", SALU), I(f"s_mov_b32 s{HX}, s{T6}", SALU),
@@ -571,6 +574,7 @@ class K:
         KD, VD = 72, 76
         ins += desc_at(KD, Pk, KOFF, KVH, Hk, KW0, Rk, REM)
         ins += desc_at(VD, Pv, VOFF, KVH, Hv, KW0, Rv, REM)
+        ins += self.stamp(V_SS + 12)
         r_, hh = V_TMP, V_TMP + 1
         ins += [I(f"v_and_b32_e32 v{r_}, 31, v{V_LANE}", VALU, rd=vr(V_LANE), wr=vr(r_)),
                 I(f"v_lshrrev_b32_e32 v{hh}, 5, v{V_LANE}", VALU, rd=vr(V_LANE), wr=vr(hh)),
@@ -809,7 +813,7 @@ class K:
               Inst(f"v_readfirstlane_b32 s{S_WAVE}, v1", RFL, rd=vr(1), wr=sr(S_WAVE)),
               Inst(f"v_and_b32_e32 v{V_LANE}, 63, v0", VALU, rd=vr(0), wr=vr(V_LANE)),
               Inst(f"v_mov_b32_e32 v{V_ROUND}, 0", VALU, wr=vr(V_ROUND))] +
-             ([Inst(f"v_mov_b32_e32 v{V_SS + i}, 0", VALU) for i in range(8)] + self.stamp(None) if OPT_STEPSTAMP else []))
+             ([Inst(f"v_mov_b32_e32 v{V_SS + i}, 0", VALU) for i in range(16)] + self.stamp(None) if OPT_STEPSTAMP else []))
         # persistent item loop (fa_bwd_asm.cpp, knob 6): workgroup w runs items r G + (r odd ? rev(w) :
         # w); G = n_items runs one item per workgroup.  The barrier keeps every wave's LDS reads of
         # the previous item ahead of the DMA of this one.
@@ -822,10 +826,12 @@ class K:
                 Inst("s_waitcnt lgkmcnt(0)", WAIT)]
         head += item_pos_ops(S_ITEM, T0, 2, T2, T3, T4)
         head += [Inst(f"s_cmp_ge_u32 s{S_ITEM}, s{T1}", SALU), Inst(f"s_cbranch_scc1 {self.lab_end}", BRANCH)]
-        pro = head + self.prologue(l_epi) + self.prologue_dma()
+        head += self.stamp(V_SS + 10)
+        pro = head + self.prologue(l_epi) + self.stamp(V_SS + 13) + self.prologue_dma() + self.stamp(V_SS + 14)
         # wait: Q / dO(0) (phase -1), Q / dO(1) (its tail prefetches fragments of 1), LSE / D(0, 1)
         # landed; younger than Q / dO(1): L3, Q2, L4, Q3, L5, Q4, L6, Q5, L7 = 21
         pro += [Inst("s_waitcnt vmcnt(21)", WAIT), Inst("s_barrier", BARRIER)]
+        pro += self.stamp(V_SS + 15)
         if OPT_STAMP:
             pro += [Inst(f"s_memtime s[{S_TMP + 1}:{S_TMP + 2}]", SMEM), Inst("s_waitcnt lgkmcnt(0)", WAIT),
                     Inst(f"v_mov_b32_e32 v{V_STAMP + 10}, s{S_TMP + 1}", VALU), Inst(f"v_mov_b32_e32 v{V_STAMP + 11}, s{S_TMP + 2}", VALU)]
@@ -912,6 +918,8 @@ class K:
                          I("s_lshl_b32 s50, s50, 6", SALU), I(f"v_mov_b32_e32 v{V_SS + 8}, 0", VALU), nop(4),
                          I(f"buffer_store_dwordx4 v[{V_SS}:{V_SS + 3}], v{V_SS + 8}, s[52:55], s50 offen", VSTORE),
                          I(f"buffer_store_dwordx4 v[{V_SS + 4}:{V_SS + 7}], v{V_SS + 8}, s[52:55], s50 offen offset:16", VSTORE),
+                         I(f"buffer_store_dwordx4 v[{V_SS + 8}:{V_SS + 11}], v{V_SS + 8}, s[52:55], s50 offen offset:32", VSTORE),
+                         I(f"buffer_store_dwordx4 v[{V_SS + 12}:{V_SS + 15}], v{V_SS + 8}, s[52:55], s50 offen offset:48", VSTORE),
                          I("s_waitcnt vmcnt(0)", WAIT)])
         if OPT_STAMP:
             I = Inst
