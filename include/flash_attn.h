@@ -428,7 +428,10 @@ void flash_attn_timing_read(int kernel_id, double * total_ms, long * count);
  * heads grouped per XCD whenever the shape allows), 8 the backward preprocessing fused into the
  * assembly dQ kernel (FLASH_ATTN_MI355X_FUSE_PRE, default 1: D = rowsum(dO o O), softmax_d and the
  * dK/dV kernel's scratch are written by dQ, which then runs before dK/dV; 0 launches the separate
- * preprocessing kernel).  Each is read from its environment variable once, at first use. */
+ * preprocessing kernel), 9 items per workgroup of the assembly dK/dV kernel on varlen calls
+ * (FLASH_ATTN_MI355X_VARLEN_ROUNDS, default 2, in snake-paired rounds; 1: one workgroup per item).
+ * Knob 6 = 2 also runs varlen dK/dV persistent, from a device-built work list.  Each is read from
+ * its environment variable once, at first use. */
 void flash_attn_set_knob(int id, int value);
 int flash_attn_get_knob(int id);
 /* 0 routes every forward to the HIP kernel, 1 (default) lets head dim 128 and 64 take the assembly

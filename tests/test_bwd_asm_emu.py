@@ -67,6 +67,40 @@ def test_asm_dkdv_persistent_loop(asm_text, b, sq, sk, h, hk, causal, reduce, gr
     assert ek <= 1e-2 and ev <= 1e-2, (ek, ev)
 
 
+@pytest.mark.timeout(900)
+@pytest.mark.parametrize("lens,h,hk,causal,reduce,grid", [
+    ([200, 70, 300], 2, 1, True, True, None),     # varlen, one workgroup per item (empty key blocks exit)
+    ([200, 70, 300], 2, 1, True, True, 4),        # 2-3 items per workgroup: an item without keys, then none
+    ([130, 0, 260, 40], 2, 1, True, True, 3),     # an empty sequence; short items (< 3 steps) -> stalled cursors
+    ([90, 257, 33], 3, 3, False, False, 2),       # full attention, heads expanded
+])
+@pytest.mark.parametrize("table", [False, True])
+def test_asm_dkdv_varlen_in_emulator(asm_text, lens, h, hk, causal, reduce, grid, table):
+    """varlen (cu_seqlens) launches, one workgroup per item and the item loop over several items
+    (FLASH_ATTN_MI355X_VARLEN_ROUNDS): the pipelined loop switches items whose work order skips
+    blocks past a sequence's end; table: the items from the device-built list (flags bit 2, the
+    persistent varlen launch)"""
+    ek, ev, *_ = emu_bwd.run(h=h, hk=hk, causal=causal, bf16=True, reduce=reduce, seed=1, text=asm_text, verbose=False,
+                             grid=grid, lens=lens, table=table)
+    assert ek <= 1e-2 and ev <= 1e-2, (ek, ev)
+
+
+@pytest.mark.timeout(900)
+def test_asm_dkdv_pipelined_loop_in_emulator():
+    """the pipelined item loop (dev switch FA_GBW_CONT=1, off in the shipped build: the next item's
+    subtiles DMA'd and its K / V loaded under the current item's last steps, a stalled cursor
+    re-issued at the item switch): fixed length over 3 workgroups, varlen with short items, empty
+    sequences and blocks without keys, from the decoded order and from the device list"""
+    env = dict(os.environ, FA_GBW_CONT="1")
+    text = subprocess.run([sys.executable, emu_bwd.GEN], check=True, capture_output=True, text=True, env=env).stdout
+    ek, ev, *_ = emu_bwd.run(2, 150, 130, 4, 2, False, True, False, seed=3, text=text, verbose=False, grid=3)
+    assert ek <= 1e-2 and ev <= 1e-2, (ek, ev)
+    for table in (False, True):
+        ek, ev, *_ = emu_bwd.run(h=2, hk=1, causal=True, bf16=True, reduce=True, seed=1, text=text, verbose=False,
+                                 grid=3, lens=[130, 0, 260, 40], table=table)
+        assert ek <= 1e-2 and ev <= 1e-2, (table, ek, ev)
+
+
 def test_generated_dkdv_kernels_are_hazard_free():
     spec = importlib.util.spec_from_file_location(
         "asm_isa", os.path.join(ROOT, "xhy-flash-attention_amd", "csrc", "asm", "isa.py"))

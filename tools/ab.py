@@ -3,6 +3,10 @@
 
     python tools/ab.py LIB_A.so LIB_B.so ... [--workload c3] [--rounds 5] [--iters 10] [--bwd]
 
+A variant may carry knob settings, ``LIB.so@9=2,6=0``: flash_attn_set_knob before each of its turns
+(the same library may then appear several times; knobs another variant sets return to their
+default values for the variants that do not).
+
 Every variant library is loaded side by side (ctypes, RTLD_LOCAL) and driven through the same
 ``flash_attn_2_cuda`` Python mirror by swapping its ``_lib`` handle; rounds interleave the variants
 so clock / thermal drift hits all of them alike (cdna_hip_programming.md §5.4 rule 24).  Each
@@ -89,13 +93,22 @@ def main():
             return m.varlen_bwd(dout, q, k, v, res[0], res[5], None, None, None, cu, cu, ms_, ms_, pd, scale, False,
                                 causal, None, res[7])
         return m.bwd(dout, q, k, v, res[0], res[5], None, None, None, pd, scale, causal, None, res[7])
-    libs = [load(p) for p in args.libs]
-    names = [os.path.basename(p) for p in args.libs]
+    specs = [(p.split("@")[0], dict(tuple(int(x) for x in kv.split("=")) for kv in p.split("@")[1].split(",")) if "@" in p else {})
+             for p in args.libs]
+    cache = {}
+    libs = [cache.setdefault(p, load(p)) if p not in cache else cache[p] for p, _ in specs]
+    for lib in cache.values():
+        lib.flash_attn_get_knob.restype = ctypes.c_int
+    touched = sorted({kid for _, kn in specs for kid in kn})
+    defaults = {kid: cache[specs[0][0]].flash_attn_get_knob(kid) for kid in touched}
+    names = [os.path.basename(p) + ("@" + ",".join(f"{kid}={val}" for kid, val in kn.items()) if kn else "") for p, kn in specs]
     times = {n: {} for n in names}
     ref = None
     for rnd in range(args.rounds):
-        for lib, name in zip(libs, names):
+        for lib, name, (_, kn) in zip(libs, names, specs):
             m._lib = lib
+            for kid in touched:
+                lib.flash_attn_set_knob(kid, kn.get(kid, defaults[kid]))
             gen = torch.Generator(device="cuda").manual_seed(7) if pd > 0 else None
             res = fwd(gen)
             out, lse = res[0], res[5]

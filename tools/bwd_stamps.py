@@ -55,6 +55,15 @@ def main(path, b=4, s=8192, h=16, c4=False):
         a = a[a[:, 7] > 0]
         st = np.maximum(a[:, 3], 1)
         it = np.maximum(a[:, 7], 1)
+        cont = "cont" in sys.argv[2:]   # a pipelined-loop build: 10, 11 = item switch parts, 12 = the last steps' compute
+        if cont:
+            a[:, 0] += a[:, 12]
+            print(f"  (pipelined loop) last step compute per item med {np.median(a[:, 12] / np.maximum(a[:, 7], 1)):.0f}; "
+                  f"switch: record {np.median(a[:, 10] / np.maximum(a[:, 7], 1)):.0f}, DMA drain {np.median(a[:, 11] / np.maximum(a[:, 7], 1)):.0f}")
+            print(f"  (pipelined loop) the 2 steps before the last: compute per item med {np.median(a[:, 13] / np.maximum(a[:, 7], 1)):.0f}; "
+                  f"switch tail (re-issue, C) {np.median(a[:, 14] / np.maximum(a[:, 7], 1)):.0f}, item barrier {np.median(a[:, 15] / np.maximum(a[:, 7], 1)):.0f}")
+            a[:, 12] = 0
+            a[:, 13] = 0
         tot = a[:, 0] + a[:, 1] + a[:, 2] + a[:, 5] + a[:, 6] + a[:, 10:16].sum(1)
         a[:, 5] += a[:, 10:16].sum(1)   # the prologue: its parts (10..15) and phase -1 (5)
         print(f"waves {len(a)}, items per wave med {np.median(a[:, 7]):.0f}, steps per wave med {np.median(a[:, 3]):.0f}")

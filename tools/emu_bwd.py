@@ -73,9 +73,12 @@ def reference(q, k, v, do, causal, scale):
 
 
 def run(b=1, sq=200, sk=200, h=2, hk=1, causal=True, bf16=True, reduce=True, seed=0, text=None, verbose=True,
-        grid=None, unit_c=False):
+        grid=None, unit_c=False, lens=None, table=False):
     """grid: workgroups of the persistent item loop (default: one per item); unit_c: the _c1 kernel
-    (c = 1: scale = ln 2, the launch of a backward on the prescaled Q')"""
+    (c = 1: scale = ln 2, the launch of a backward on the prescaled Q'); lens: varlen (unpadded,
+    cu_seqlens_q = cu_seqlens_k from these lengths; b, sq, sk follow from them)"""
+    if lens is not None:
+        return run_varlen(lens, h, hk, causal, bf16, reduce, seed, text, verbose, grid, table)
     rng = np.random.default_rng(seed)
     q = rng.standard_normal((b, sq, h, D)).astype(np.float32)
     k = rng.standard_normal((b, sk, hk, D)).astype(np.float32)
@@ -130,6 +133,92 @@ def run(b=1, sq=200, sk=200, h=2, hk=1, causal=True, bf16=True, reduce=True, see
     if verbose:
         print(f"b={b} sq={sq} sk={sk} h={h} hk={hk} causal={causal} bf16={bf16} reduce={red}: "
               f"rel max|ddK| {ek:.3e} rel max|ddV| {ev:.3e} ({emu.count} instructions, {emu.mfma_count} MFMAs)")
+    return ek, ev, dk, dk_ref, dv, dv_ref
+
+
+def varlen_items(lens, nh, gdiv, rows, nlev, reverse):
+    """the device-built work list (fa_fwd_asm.cpp varlen_items_kernel), restated: levels from the
+    highest down, within a level the sequences with more blocks first, then heads; entries
+    (bidb | head << 16, kvh | block << 16) after [count, 0]"""
+    nb = [min((L + rows - 1) // rows, nlev) if L > 0 else 0 for L in lens]
+    order = sorted(range(len(lens)), key=lambda s_: -nb[s_])
+    out = []
+    for lv in range(nlev - 1, -1, -1):
+        for s_ in order:
+            if nb[s_] > lv:
+                for hd in range(nh):
+                    blk = nb[s_] - 1 - lv if reverse else lv
+                    out += [s_ | (hd << 16), (hd // gdiv) | (blk << 16)]
+    return np.array([len(out) // 2, 0] + out, dtype=np.uint32)
+
+
+def run_varlen(lens, h, hk, causal, bf16, reduce, seed, text, verbose, grid, table=False):
+    """varlen launch (flags bit 0 clear: row offsets from cu_seqlens): packed (total, heads, D);
+    table: the items from the device-built list (flags bit 2, the persistent varlen launch)"""
+    rng = np.random.default_rng(seed)
+    b, total, mx = len(lens), sum(lens), max(lens)
+    cu = np.concatenate([[0], np.cumsum(lens)]).astype(np.int32)
+    q = rng.standard_normal((total, h, D)).astype(np.float32)
+    k = rng.standard_normal((total, hk, D)).astype(np.float32)
+    v = rng.standard_normal((total, hk, D)).astype(np.float32)
+    do = rng.standard_normal((total, h, D)).astype(np.float32)
+    enc, dec = (f32_to_bf16, bf16_to_f32) if bf16 else (f32_to_f16, f16_to_f32)
+    q16, k16, v16, do16 = (enc(x).astype(np.uint16) for x in (q, k, v, do))
+    qf, kf, vf, dof = (dec(x).astype(np.float64) for x in (q16, k16, v16, do16))
+    scale = D ** -0.5
+    g = h // hk
+    red = reduce and g > 1
+    nh_out = hk if red else h
+    ng = (mx + 31) // 32 + 1
+    lsed = np.zeros((b, h, ng, 64), np.float32)
+    dk_ref = np.zeros((total, nh_out, D))
+    dv_ref = np.zeros((total, nh_out, D))
+    for bi, L in enumerate(lens):
+        if L == 0:
+            continue
+        sl = slice(cu[bi], cu[bi + 1])
+        lse, dsum, dkr, dvr = reference(qf[None, sl], kf[None, sl], vf[None, sl], dof[None, sl], causal, scale)
+        if red:
+            dkr = dkr.reshape(1, L, hk, g, D).sum(axis=3)
+            dvr = dvr.reshape(1, L, hk, g, D).sum(axis=3)
+        dk_ref[sl], dv_ref[sl] = dkr[0], dvr[0]
+        for hi in range(h):
+            for r in range(L):
+                lsed[bi, hi, r // 32, r % 32] = np.float32(-lse[0, hi, r] / np.float32(scale))
+                lsed[bi, hi, r // 32, 32 + r % 32] = np.float32(-dsum[0, hi, r])
+    heap = Heap(64 << 20)
+    aq, ak, av, ado = heap.put(q16), heap.put(k16), heap.put(v16), heap.put(do16)
+    nbytes = total * nh_out * D * 2
+    adk, adv = heap.alloc(nbytes), heap.alloc(nbytes)
+    heap.get(adk, nbytes)[:] = 0xAB
+    heap.get(adv, nbytes)[:] = 0xAB
+    alsed = heap.put(lsed)
+    acu = heap.put(cu)
+    nblk = (mx + BKN - 1) // BKN
+    n_items = b * nh_out * nblk
+    asch = heap.put(varlen_items(lens, nh_out, 1 if red else g, BKN, nblk, True)) if table else 0
+    kw = dict(q=aq, k=ak, v=av, do=ado, dk=adk, dv=adv, lsed=alsed, sched=asch, cuq=acu, cuk=acu,
+              dec=dkdv_item_decode(b * nh_out, nh_out, 1 if red else g, nblk), n_items=n_items,
+              grid=grid or n_items,
+              q_batch=0, k_batch=0, v_batch=0, do_batch=0, dk_batch=0, dv_batch=0,
+              q_row=h * D * 2, k_row=hk * D * 2, v_row=hk * D * 2, do_row=h * D * 2, dk_row=nh_out * D * 2,
+              dv_row=nh_out * D * 2, q_head=D * 2, k_head=D * 2, v_head=D * 2, do_head=D * 2, dk_head=D * 2,
+              dv_head=D * 2, sq=mx, sk=mx, h=h, ng=ng, nh=g if red else 1, group=g,
+              c=float(np.float32(scale * 1.4426950408889634)), scale=float(np.float32(scale)),
+              flags=(2 if red else 0) | (4 if table else 0))
+    akarg = heap.put(np.frombuffer(pack_args(**kw), dtype=np.uint8))
+    text = text or asm_text()
+    name = f"fa_bwd_dkdv_asm_d128_{'bf16' if bf16 else 'f16'}_{'causal' if causal else 'full'}"
+    emu = Emu(text, name, heap)
+    for L in range(grid or n_items):
+        emu.run_wg(L, akarg)
+    dk = dec(heap.get(adk, nbytes).view(np.uint16)).reshape(total, nh_out, D).astype(np.float64)
+    dv = dec(heap.get(adv, nbytes).view(np.uint16)).reshape(total, nh_out, D).astype(np.float64)
+    ek = np.abs(dk - dk_ref).max() / max(np.abs(dk_ref).max(), 1e-9)
+    ev = np.abs(dv - dv_ref).max() / max(np.abs(dv_ref).max(), 1e-9)
+    if verbose:
+        print(f"varlen {lens} h={h} hk={hk} causal={causal} bf16={bf16} reduce={red} grid={grid}: "
+              f"rel max|ddK| {ek:.3e} rel max|ddV| {ev:.3e} ({emu.count} instructions)")
     return ek, ev, dk, dk_ref, dv, dv_ref
 
 

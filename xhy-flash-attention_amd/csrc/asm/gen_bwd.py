@@ -165,6 +165,40 @@ S_ITEM = 28            # the item index, until the sweep geometry takes the regi
 V_STAMP = 164          # 164..177: start lo / hi, HW_ID, XCC_ID, wg, end lo / hi, wave, -, -, loop start lo / hi,
                        # epilogue start lo / hi (with OPT_STAMP)
 
+# ---- the pipelined item loop (OPT_CONT): the DMA of the next item's first subtiles and the loads of
+# its K / V fragments run under the current item's last steps; the next item's geometry is computed
+# at the start of the current one (geometry(), into the record N) ----
+# (dev switch, off: C3 +-0, C4 +1..3 % -- the last step's K / V loads and slower steps ate the
+# prologue it saves, profiles/r05/ab_cont_*_r05h.txt)
+OPT_CONT = os.environ.get("FA_GBW_CONT", "0") == "1"
+V_N = 202               # record of the next item (202..236), fields:
+N_QH, N_OH, N_LH = 0, 2, 4          # head bases (64-bit)
+N_QREC, N_OREC, N_LREC, N_NSP = 6, 7, 8, 9
+N_KD, N_VD = 10, 13                 # K / V fragment descriptors (base lo, hi, records)
+N_QF, N_NLAST, N_LANEK = 16, 17, 18
+N_ST = 19                           # the epilogue's scalars (15, as V_ST)
+N_HL0 = 34                          # heads of the sweep - 1
+N_LEN = 35
+V_C = 64                # the record of the item starting (transient, at the item switch: v64..98)
+V_SAVE = 0              # the DMA side's registers across geometry() (v0..v32, at the item switch)
+V_ZERO = 140            # 140..143: zeros (the stores of an item with keys and no rows)
+V_KLO, V_VLO = 160, 161 # lane offsets of the K / V fragment loads (launch constants)
+# where the next item's K / V fragment loads go (dev A/B): the last step's phase B, the tail, the epilogue
+OPT_KVAT = os.environ.get("FA_GBW_KVAT", "last")
+# DMA-side registers of the pipelined loop (beside S_QD .. S_LREC0); the kernarg block s56.. is free
+# during the steps, geometry() clobbers them (saved across it)
+S_NSPD, S_NSPL = (96, 97) if OPT_CONT else (S_NSP, S_NSP)   # subtiles per head of the DMA cursors' items
+S_DSW, S_LSW = 98, 99              # the cursor has switched to the next item (ahead of the compute)
+S_DSTALL, S_LSTALL = 100, 101      # slot where the cursor stalled (-1: running): a second switch must
+                                   # wait for the item switch, which re-issues the stalled subtiles
+S_KVN = 88                         # 88..95: the next item's K / V descriptors
+S_EPD = 80                         # 80..87: the epilogue's store descriptors
+# ... and the launch constants the DMA uses: a geometry() pass that ends on an item without keys or on
+# no item at all leaves them clobbered (the work order's loads land in s36..45)
+DMA_SIDE = (list(range(S_QD, S_QD + 12)) + [S_SDMA, S_LDMA, S_LOCD, S_HLD, S_LOCL, S_HLL] +
+            list(range(S_QH, S_QH + 6)) + [S_QREC0, S_OREC0, S_LREC0, S_NSPD, S_NSPL, S_DSW, S_LSW, S_DSTALL, S_LSTALL] +
+            [S_W2K, S_QHS, S_OHS, S_LHS, S_Q32, S_O32])
+
 
 class K:
     """one kernel variant"""
@@ -394,8 +428,11 @@ class K:
         """phases A (p = 2n) and B (2n+1) of step n"""
         a = self.phase(0, sdp=True, dvdk=not first, valu=True, masked=masked, q0_add=0, dma=True,
                        next_kind="dvdk" if last else "full", first_pref=True, tail_of_step=None)
+        # (OPT_CONT) the last step loads the next item's K / V fragments: phase A issued the item's
+        # last S / dP MFMAs, the last readers of a[KF..], a[VF..]
+        tail = self.step_tail_ops() + (self.kv_next_ops(earliest=4) if OPT_CONT and last and OPT_KVAT == "last" else [])
         b = self.phase(1, sdp=not last, dvdk=True, valu=True, masked=masked, q0_add=SUB, dma=True,
-                       next_kind="dvdk" if last else "full", first_pref=True, tail_of_step=self.step_tail_ops())
+                       next_kind="dvdk" if last else "full", first_pref=True, tail_of_step=tail)
         return a + b
 
     def wrap_check(self, name):
@@ -406,8 +443,12 @@ class K:
         loc, hl, curs = {"d": (S_LOCD, S_HLD, ((S_QD, S_QH, S_QHS, S_QREC0), (S_OD, S_OH, S_OHS, S_OREC0))),
                          "l": (S_LOCL, S_HLL, ((S_LD, S_LH, S_LHS, S_LREC0),))}[name]
         lab = self.lab("wrap" + name)
-        check = [I(f"s_cmp_ge_u32 s{loc}, s{S_NSP}", SALU, rd=sr(loc) + sr(S_NSP), wr=[("scc", 0)]),
+        nsp = S_NSPD if name == "d" else S_NSPL
+        check = [I(f"s_cmp_ge_u32 s{loc}, s{nsp}", SALU, rd=sr(loc) + sr(nsp), wr=[("scc", 0)]),
                  I(f"s_cbranch_scc1 {lab}\n{lab}_back:", BRANCH, rd=[("scc", 0)])]
+        if OPT_CONT:
+            self.ool.extend(self.wrap_cont(name, lab))
+            return check
         blk = [label(lab), I(f"s_mov_b32 s{loc}, 0", SALU),
                I(f"s_cmp_eq_u32 s{hl}, 0", SALU),
                I(f"s_cselect_b32 s{t}, 0, 1", SALU),
@@ -421,6 +462,67 @@ class K:
         blk.append(I(f"s_branch {lab}_back", BRANCH))
         self.ool.extend(blk)
         return check
+
+    def wrap_cont(self, name, lab):
+        """(OPT_CONT) out-of-line block of a head wrap: the next head of the group; none left -> the next
+        item (record N), once per item switch of the compute; a second time -> stall (zero records,
+        the slot noted: item_switch re-issues from there)"""
+        I = Inst
+        loc, hl, sw, stall, slot, curs = {
+            "d": (S_LOCD, S_HLD, S_DSW, S_DSTALL, S_SDMA, ((S_QD, S_QH, S_QHS, S_QREC0, N_QH, N_QREC),
+                                                           (S_OD, S_OH, S_OHS, S_OREC0, N_OH, N_OREC))),
+            "l": (S_LOCL, S_HLL, S_LSW, S_LSTALL, S_LDMA, ((S_LD, S_LH, S_LHS, S_LREC0, N_LH, N_LREC),))}[name]
+        l_item, l_stall = lab + "_item", lab + "_stall"
+        blk = [label(lab), I(f"s_mov_b32 s{loc}, 0", SALU),
+               I(f"s_cmp_eq_u32 s{hl}, 0", SALU), I(f"s_cbranch_scc1 {l_item}", BRANCH),
+               I(f"s_sub_u32 s{hl}, s{hl}, 1", SALU)]
+        for desc, hb, hs, rec0, _, _ in curs:
+            blk += [I(f"s_add_u32 s{hb}, s{hb}, s{hs}", SALU), I(f"s_addc_u32 s{hb + 1}, s{hb + 1}, 0", SALU),
+                    I(f"s_mov_b32 s{desc}, s{hb}", SALU), I(f"s_and_b32 s{desc + 1}, s{hb + 1}, 0xffff", SALU),
+                    I(f"s_mov_b32 s{desc + 2}, s{rec0}", SALU)]
+        blk += [I(f"s_branch {lab}_back", BRANCH),
+                label(l_item), I(f"s_cmp_eq_u32 s{sw}, 0", SALU), I(f"s_cbranch_scc0 {l_stall}", BRANCH)]
+        blk += self.switch_ops(name)
+        blk += [I(f"s_branch {lab}_back", BRANCH),
+                label(l_stall), I(f"s_cmp_eq_u32 s{stall}, -1", SALU), I(f"s_cselect_b32 s{stall}, s{slot}, s{stall}", SALU)]
+        blk += [I(f"s_mov_b32 s{desc + 2}, 0", SALU) for desc, *_ in curs]
+        blk += [I(f"s_branch {lab}_back", BRANCH)]
+        return blk
+
+    def switch_ops(self, name, rec=V_N):
+        """(OPT_CONT) a DMA cursor ('d' or 'l') moves to the first head of the item in the record at
+        v[rec]; the cursor's position resets, its side is marked switched"""
+        I = Inst
+        loc, hl, sw, nsp, curs = {
+            "d": (S_LOCD, S_HLD, S_DSW, S_NSPD, ((S_QD, S_QH, S_QREC0, N_QH, N_QREC), (S_OD, S_OH, S_OREC0, N_OH, N_OREC))),
+            "l": (S_LOCL, S_HLL, S_LSW, S_NSPL, ((S_LD, S_LH, S_LREC0, N_LH, N_LREC),))}[name]
+
+        def rf(s_, f):
+            return I(f"v_readfirstlane_b32 s{s_}, v{rec + f}", RFL, rd=vr(rec + f), wr=sr(s_))
+        ops = [I(f"s_mov_b32 s{loc}, 0", SALU, wr=sr(loc)), I(f"s_mov_b32 s{sw}, 1", SALU, wr=sr(sw)),
+               rf(hl, N_HL0), rf(nsp, N_NSP)]
+        for desc, hb, rec0, fb, fr in curs:
+            ops += [rf(hb, fb), rf(hb + 1, fb + 1), rf(rec0, fr),
+                    I(f"s_mov_b32 s{desc}, s{hb}", SALU, rd=sr(hb), wr=sr(desc)),
+                    I(f"s_and_b32 s{desc + 1}, s{hb + 1}, 0xffff", SALU, rd=sr(hb + 1), wr=sr(desc + 1)),
+                    I(f"s_mov_b32 s{desc + 2}, s{rec0}", SALU, rd=sr(rec0), wr=sr(desc + 2)),
+                    I(f"s_mov_b32 s{desc + 3}, 0x20000", SALU, wr=sr(desc + 3))]
+        return ops
+
+    def kv_next_ops(self, rec=V_N, key=700, earliest=None):
+        """(OPT_CONT) the K / V fragments of the item in the record at v[rec] into a[KF..], a[VF..]
+        (records 0: no item, zeros)"""
+        I = Inst
+        ops = []
+        for d0, f in ((S_KVN, N_KD), (S_KVN + 4, N_VD)):
+            ops += [I(f"v_readfirstlane_b32 s{d0 + i}, v{rec + f + i}", RFL, rd=vr(rec + f + i), wr=sr(d0 + i), key=key,
+                      earliest=earliest) for i in range(3)]
+            ops += [I(f"s_mov_b32 s{d0 + 3}, 0x20000", SALU, wr=sr(d0 + 3), key=key, earliest=earliest)]
+        for base, d0, lo in ((KF, S_KVN, V_KLO), (VF, S_KVN + 4, V_VLO)):
+            for ks in range(KS):
+                ops.append(I(f"buffer_load_dwordx4 {rtxt('a', base + 4 * ks, 4)}, v{lo}, s[{d0}:{d0 + 3}], 0 offen offset:{32 * ks}",
+                             VLOAD, rd=vr(lo) + sr(d0, 4), wr=ar(base + 4 * ks, 4), key=key + 1, earliest=earliest))
+        return ops
 
     def stamp(self, acc, count=None):
         """(FA_GBW_STAMP=2) v[acc] += now - last; last = now (acc None: only last = now); v[count] += 1"""
@@ -437,11 +539,21 @@ class K:
             ins += [Inst(f"v_add_u32_e32 v{count}, 1, v{count}", VALU)]
         return ins
 
-    def step_end(self):
-        """after a step: head wraps of the DMA cursors, wait for the subtiles the next step reads, barrier"""
+    def step_end(self, last=False):
+        """after a step: head wraps of the DMA cursors, wait for the subtiles the next step reads, barrier
+        (the last step: the tail reads subtiles the step before waited for; OPT_CONT leaves the next
+        item's K / V loads in flight)"""
         ins = self.wrap_check("d") + self.wrap_check("l")
-        ins += self.stamp(V_SS + 0, count=V_SS + 3)
-        ins += [Inst(f"s_waitcnt vmcnt({VMCNT_STEP}) lgkmcnt(0)", WAIT)]
+        # (the last step's compute is also kept apart: v[V_SS + 12] under OPT_CONT)
+        ins += self.stamp(V_SS + 12 if OPT_CONT and last else V_SS + 0, count=V_SS + 3)
+        if OPT_STEPSTAMP and OPT_CONT and not last:
+            # the two steps before the last (their DMA runs into the next item) also into v[V_SS + 13]
+            t = S_TMP + 1
+            ins += [Inst(f"s_sub_u32 s{t}, s{S_NLAST}, s{S_N}", SALU), Inst(f"s_cmp_le_u32 s{t}, 1", SALU),
+                    Inst("s_cselect_b64 vcc, -1, 0", SALU),
+                    Inst(f"v_cndmask_b32_e32 v{V_SS + 9}, 0, v{V_SS + 9}, vcc", VALU),
+                    Inst(f"v_add_u32_e32 v{V_SS + 13}, v{V_SS + 13}, v{V_SS + 9}", VALU)]
+        ins += [Inst(f"s_waitcnt vmcnt({VMCNT_STEP + (2 * KS if OPT_CONT and last else 0)}) lgkmcnt(0)", WAIT)]
         ins += self.stamp(V_SS + 1)
         ins += [Inst("s_barrier", BARRIER)]
         ins += self.stamp(V_SS + 2)
@@ -456,12 +568,19 @@ class K:
                 continue
             fill += self.frag_reads(m, t, i, key=-100 + m, earliest=max(m - 16, -1) if m >= 16 else None,
                                     deadline=max(m - 2, 0))
+        if OPT_CONT and OPT_KVAT == "tail":
+            fill += self.kv_next_ops(earliest=0)
         return schedule([x[0] for x in mf], fill)
 
     # ------------------------------------------------------------------ prologue
-    def prologue(self, l_epi):
+    def prologue(self, l_epi, l_nokeys=None, cont=False):
+        """the item S_ITEM's geometry, DMA cursors and loop state (as the item loop head); cont
+        (OPT_CONT, geometry()): only the geometry, packed into the record N -- no loads, no loop state,
+        no zeroing; l_nokeys: no keys in the block (default: the next item), l_epi: keys and no rows"""
         I = Inst
         ins = []
+        l_nokeys = l_nokeys or self.lab_next
+        substamp = self.stamp if not OPT_CONT else (lambda *a, **k: [])
         # kernarg dwords 0..45 -> s56..s101; 46..49 (h, ng, nh, group) -> s20..s23 (free until the loop
         # state is set); 50, 51 (c, scale) -> S_C, S_SCALE; 52 (flags) -> s3
         ka = 56
@@ -495,11 +614,22 @@ class K:
         ins += [I(f"s_load_dwordx8 s[36:43], s[0:1], {DEC_OFF}", SMEM),
                 I(f"s_load_dwordx2 s[44:45], s[0:1], {DEC_OFF + 32}", SMEM),
                 I("s_waitcnt lgkmcnt(0)", WAIT)]
-        ins += self.stamp(V_SS + 11)
+        ins += substamp(V_SS + 11)
         BIDB, HX, KVH, KB = 24, 25, 26, 27      # S_N .. S_Q0V, set at the end
+        # varlen with a device-built work list (flags bit 2, fa_fwd_asm.cpp varlen_items_kernel: the
+        # key blocks of every sequence, heaviest level first, none past a sequence's end): its entry
+        # (bidb | head << 16, kvh | key block << 16); else decoded from the item index
+        l_tab, l_dec = self.lab("tab"), self.lab("dec")
+        ins += [I(f"s_bitcmp1_b32 s{FLG}, 2", SALU), I(f"s_cbranch_scc1 {l_tab}", BRANCH)]
         ins += item_decode_ops(L=S_ITEM, M=36, pa=T1, pb=T3, t=T5, u=T6, o_blk=KB, reverse=False)
         ins += [I(f"s_mov_b32 s{BIDB}, s{T3}", SALU), I(f"s_mov_b32 s{HX}, s{T6}", SALU),
-                I(f"s_mov_b32 s{KVH}, s{T1}", SALU)]
+                I(f"s_mov_b32 s{KVH}, s{T1}", SALU), I(f"s_branch {l_dec}", BRANCH), label(l_tab),
+                I(f"s_lshl_b32 s{T0}, s{S_ITEM}, 3", SALU), I(f"s_add_u32 s{T0}, s{T0}, 8", SALU),
+                I(f"s_load_dwordx2 s[{T1}:{T1 + 1}], s[{Psch}:{Psch + 1}], s{T0}", SMEM),
+                I("s_waitcnt lgkmcnt(0)", WAIT),
+                I(f"s_and_b32 s{BIDB}, s{T1}, 0xffff", SALU), I(f"s_lshr_b32 s{HX}, s{T1}, 16", SALU),
+                I(f"s_and_b32 s{KVH}, s{T1 + 1}, 0xffff", SALU), I(f"s_lshr_b32 s{KB}, s{T1 + 1}, 16", SALU),
+                label(l_dec)]
         # varlen geometry (BlockInfo, block_info.h:14-31): 64-bit byte offsets of row 0 of this sequence;
         # seqlens into SQ / SK
         QOFF, DOOFF, KOFF, VOFF, DKOFF, DVOFF = (34, 35), (36, 37), (38, 39), (40, 41), (42, 43), (44, 45)
@@ -536,7 +666,7 @@ class K:
         N0, KW0 = T4, T5
         ins += [I(f"s_lshl_b32 s{N0}, s{KB}, 7", SALU, rd=sr(KB), wr=sr(N0)),
                 I(f"s_cmp_ge_i32 s{N0}, s{SK}", SALU, rd=sr(N0) + sr(SK), wr=[("scc", 0)]),
-                I(f"s_cbranch_scc1 {self.lab_next}", BRANCH),
+                I(f"s_cbranch_scc1 {l_nokeys}", BRANCH),
                 I(f"s_lshl_b32 s{KW0}, s{S_WAVE}, 5", SALU, rd=sr(S_WAVE), wr=sr(KW0)),
                 I(f"s_add_u32 s{KW0}, s{KW0}, s{N0}", SALU, rd=sr(KW0) + sr(N0), wr=sr(KW0))]
         # dK / dV head: the kv head (reduced GQA, flags bit 1) or the query head
@@ -545,8 +675,9 @@ class K:
                 I(f"s_cselect_b32 s{HD}, s{KVH}, s{HX}", SALU, rd=sr(KVH) + sr(HX) + [("scc", 0)], wr=sr(HD))]
         # the epilogue's scalars, stashed in VGPRs (readfirstlane there)
         stash = [KW0, HD, DKOFF[0], DKOFF[1], DVOFF[0], DVOFF[1], Pdk, Pdk + 1, Pdv, Pdv + 1, Rdk, Rdv, Hdk, Hdv, SK]
+        st0 = V_N + N_ST if cont else V_ST
         for i, x in enumerate(stash):
-            ins.append(I(f"v_mov_b32_e32 v{V_ST + i}, s{x}", VALU, rd=sr(x), wr=vr(V_ST + i)))
+            ins.append(I(f"v_mov_b32_e32 v{st0 + i}, s{x}", VALU, rd=sr(x), wr=vr(st0 + i)))
 
         def desc_at(dst4, ptr, off64, head, hstride, row, rstride, nrec_rows):
             """descriptor for ptr + off64 + head * hstride + row * rstride, records nrec_rows * rstride"""
@@ -574,7 +705,7 @@ class K:
         KD, VD = 72, 76
         ins += desc_at(KD, Pk, KOFF, KVH, Hk, KW0, Rk, REM)
         ins += desc_at(VD, Pv, VOFF, KVH, Hv, KW0, Rv, REM)
-        ins += self.stamp(V_SS + 12)
+        ins += substamp(V_SS + 12)
         r_, hh = V_TMP, V_TMP + 1
         ins += [I(f"v_and_b32_e32 v{r_}, 31, v{V_LANE}", VALU, rd=vr(V_LANE), wr=vr(r_)),
                 I(f"v_lshrrev_b32_e32 v{hh}, 5, v{V_LANE}", VALU, rd=vr(V_LANE), wr=vr(hh)),
@@ -582,12 +713,16 @@ class K:
                 I(f"v_lshl_add_u32 v{V_TMP + 2}, v{hh}, 4, v{V_TMP + 2}", VALU, rd=vr(hh) + vr(V_TMP + 2), wr=vr(V_TMP + 2)),
                 I(f"v_mul_lo_u32 v{V_TMP + 3}, v{r_}, s{Rv}", VALU, rd=vr(r_) + sr(Rv), wr=vr(V_TMP + 3)),
                 I(f"v_lshl_add_u32 v{V_TMP + 3}, v{hh}, 4, v{V_TMP + 3}", VALU, rd=vr(hh) + vr(V_TMP + 3), wr=vr(V_TMP + 3))]
-        for ks in range(KS):
-            ins.append(I(f"buffer_load_dwordx4 {rtxt('a', KF + 4 * ks, 4)}, v{V_TMP + 2}, s[{KD}:{KD + 3}], 0 offen offset:{32 * ks}",
-                         VLOAD, rd=vr(V_TMP + 2) + sr(KD, 4), wr=ar(KF + 4 * ks, 4)))
-        for ks in range(KS):
-            ins.append(I(f"buffer_load_dwordx4 {rtxt('a', VF + 4 * ks, 4)}, v{V_TMP + 3}, s[{VD}:{VD + 3}], 0 offen offset:{32 * ks}",
-                         VLOAD, rd=vr(V_TMP + 3) + sr(VD, 4), wr=ar(VF + 4 * ks, 4)))
+        if cont:
+            ins += [I(f"v_mov_b32_e32 v{V_KLO}, v{V_TMP + 2}", VALU, rd=vr(V_TMP + 2), wr=vr(V_KLO)),
+                    I(f"v_mov_b32_e32 v{V_VLO}, v{V_TMP + 3}", VALU, rd=vr(V_TMP + 3), wr=vr(V_VLO))]
+        else:
+            for ks in range(KS):
+                ins.append(I(f"buffer_load_dwordx4 {rtxt('a', KF + 4 * ks, 4)}, v{V_TMP + 2}, s[{KD}:{KD + 3}], 0 offen offset:{32 * ks}",
+                             VLOAD, rd=vr(V_TMP + 2) + sr(KD, 4), wr=ar(KF + 4 * ks, 4)))
+            for ks in range(KS):
+                ins.append(I(f"buffer_load_dwordx4 {rtxt('a', VF + 4 * ks, 4)}, v{V_TMP + 3}, s[{VD}:{VD + 3}], 0 offen offset:{32 * ks}",
+                             VLOAD, rd=vr(V_TMP + 3) + sr(VD, 4), wr=ar(VF + 4 * ks, 4)))
         # ---- per-lane values (while the fragments load) ----
         # DMA voffsets: wave w, half f: row = 16 f + lane / 4, col = 64 w + 16 ((lane & 3) ^ ((lane >> 4) & 3))
         x = V_TMP + 2
@@ -689,6 +824,21 @@ class K:
                 I(f"s_mov_b32 s{S_OHS}, s{Hdo}", SALU, rd=sr(Hdo), wr=sr(S_OHS)),
                 I(f"s_lshl_b32 s{S_Q32}, s{Rq}, 5", SALU, rd=sr(Rq), wr=sr(S_Q32)),
                 I(f"s_lshl_b32 s{S_O32}, s{Rdo}, 5", SALU, rd=sr(Rdo), wr=sr(S_O32))]
+        if cont:
+            # keys and no rows: the caller stores zeros; else the record N
+            ins += [I(f"s_lshl_b32 s{S_W2K}, s{S_WAVE}, 11", SALU, rd=sr(S_WAVE), wr=sr(S_W2K)),
+                    I(f"s_cmp_lt_i32 s{T2}, 0", SALU, rd=sr(T2), wr=[("scc", 0)]),
+                    I(f"s_cbranch_scc1 {l_epi}", BRANCH)]
+
+            def put(f, x):
+                return I(f"v_mov_b32_e32 v{V_N + f}, s{x}", VALU, rd=sr(x), wr=vr(V_N + f))
+            ins += [put(N_QH, S_QH), put(N_QH + 1, S_QH + 1), put(N_OH, S_OH), put(N_OH + 1, S_OH + 1),
+                    put(N_LH, S_LH), put(N_LH + 1, S_LH + 1), put(N_QREC, S_QREC0), put(N_OREC, S_OREC0),
+                    put(N_LREC, S_LREC0), put(N_NSP, S_NSP), put(N_KD, KD), put(N_KD + 1, KD + 1), put(N_KD + 2, KD + 2),
+                    put(N_VD, VD), put(N_VD + 1, VD + 1), put(N_VD + 2, VD + 2), put(N_QF, QF), put(N_NLAST, T2),
+                    put(N_HL0, S_HLD),
+                    I(f"v_mov_b32_e32 v{V_N + N_LANEK}, v{V_LANEK}", VALU, rd=vr(V_LANEK), wr=vr(V_N + N_LANEK))]
+            return ins
         # ---- loop state ----
         ins += [I(f"s_lshl_b32 s{S_W2K}, s{S_WAVE}, 11", SALU, rd=sr(S_WAVE), wr=sr(S_W2K)),
                 I(f"s_mov_b32 s{S_SDMA}, 0", SALU, wr=sr(S_SDMA)),
@@ -719,7 +869,7 @@ class K:
         for vs in range(3):
             ins += self.dma_subtile(True) + self.dma_subtile(True)
             ins += self.wrap_check("d") + self.wrap_check("l")
-            if vs == 0 and OPT_ZLATE:
+            if vs == 0 and OPT_ZLATE and not OPT_CONT:
                 ins += [Inst(f"v_accvgpr_write_b32 a{i}, 0", ACCW, wr=ar(i)) for i in range(128)]
         return ins
 
@@ -736,11 +886,12 @@ class K:
         ops += self.lslot_advance(S_LDMA)
         return ops
 
-    def epilogue(self):
-        """dV = (dV^T)^T, dK = scale (dK^T)^T in bf16 / f16, rows of keys < seqlen_k (range-checked)"""
+    def epilogue(self, stash=V_ST, zero=False):
+        """dV = (dV^T)^T, dK = scale (dK^T)^T in bf16 / f16, rows of keys < seqlen_k (range-checked);
+        zero: store zeros (an item with keys and no rows, OPT_CONT) for the scalars at v[stash]"""
         I = Inst
         ins = []
-        KW0v, HDv, DKO, DVO, PDK, PDV, RDK, RDV, HDK, HDV, SKv = (V_ST + i for i in (0, 1, 2, 4, 6, 8, 10, 11, 12, 13, 14))
+        KW0v, HDv, DKO, DVO, PDK, PDV, RDK, RDV, HDK, HDV, SKv = (stash + i for i in (0, 1, 2, 4, 6, 8, 10, 11, 12, 13, 14))
         T0, T1, T2, T3, T4, T5, T6 = (S_TMP + i for i in range(7))
 
         def rf(v, s):
@@ -751,10 +902,21 @@ class K:
 
         # the last steps' DMA (zero records past the sweep) must have landed before the workgroup's LDS
         # is released (moving this wait after the stores measured ±0 at C3 / C5, +0.3..1.8 % at C4)
-        ins += [I("s_waitcnt vmcnt(0)", WAIT)]
+        # (OPT_CONT: the DMA in flight is the next item's, into ring slots no wave reads now; the item
+        # switch waits for it)
+        if not OPT_CONT:
+            ins += [I("s_waitcnt vmcnt(0)", WAIT)]
+        elif OPT_KVAT == "epi" and not zero:
+            ins += self.kv_next_ops()
+        kvi = []
+        if OPT_CONT and OPT_KVAT == "epii" and not zero:    # one load per store group, under the VALU work
+            kvi = self.kv_next_ops()
+            ins += kvi[:8]
+            kvi = kvi[8:]
         ins += [rf(KW0v, T4), rf(HDv, T5), rf(SKv, T6)]
-        for dst, ptr, off, rowv, headv, acc, scale in ((S_QD, PDV, DVO, RDV, HDV, DV, False),
-                                                        (S_OD, PDK, DKO, RDK, HDK, DK, True)):
+        d0, d1 = (S_EPD, S_EPD + 4) if OPT_CONT else (S_QD, S_OD)
+        for dst, ptr, off, rowv, headv, acc, scale in ((d0, PDV, DVO, RDV, HDV, DV, False),
+                                                        (d1, PDK, DKO, RDK, HDK, DK, True)):
             ins += [rf(ptr, T0), rf(ptr + 1, T1), rf(off, T2), rf(off + 1, T3),
                     sa("s_add_u32", T0, T0, T2), sa("s_addc_u32", T1, T1, T3, [("scc", 0)]),
                     rf(headv, T2),
@@ -778,6 +940,12 @@ class K:
             x = 0
             for dt in range(NP):
                 for u0 in (0, 2):
+                    if kvi:
+                        ins.append(kvi.pop(0))
+                    if zero:
+                        ins.append(I(f"buffer_store_dwordx4 v[{V_ZERO}:{V_ZERO + 3}], v{V_TMP + 2}, s[{dst}:{dst + 3}], 0 offen offset:{64 * dt + 16 * u0}",
+                                     VSTORE, rd=vr(V_ZERO, 4) + vr(V_TMP + 2) + sr(dst, 4)))
+                        continue
                     w = x + 8
                     for uu in range(2):
                         a = acc + 16 * dt + 4 * (u0 + uu)
@@ -824,6 +992,7 @@ class K:
                 Inst(f"s_load_dwordx2 s[{T1}:{T2}], s[0:1], {NITEMS_OFF}", SMEM),     # n_items, grid
                 Inst(f"v_readfirstlane_b32 s{T0}, v{V_ROUND}", RFL),
                 Inst("s_waitcnt lgkmcnt(0)", WAIT)]
+        head += self.n_items_ops(T1)
         head += item_pos_ops(S_ITEM, T0, 2, T2, T3, T4)
         head += [Inst(f"s_cmp_ge_u32 s{S_ITEM}, s{T1}", SALU), Inst(f"s_cbranch_scc1 {self.lab_end}", BRANCH)]
         head += self.stamp(V_SS + 10)
@@ -894,7 +1063,7 @@ class K:
         for v in variants:
             f, l, m = v
             code.append(label(L[v]))
-            emit(self.step(f, l, m) + self.step_end(), pre=pad)
+            emit(self.step(f, l, m) + self.step_end(l), pre=pad)
             code.append(Inst(f"s_branch {l_disp}", BRANCH))
         code.append(label(l_tail))
         emit(self.tail(), pre=pad)
@@ -942,8 +1111,267 @@ class K:
         code.extend(self.ool)
         return code
 
+    def n_items_ops(self, dst):
+        """s[dst] = the item count: kernarg n_items, or with a device-built work list (flags bit 2)
+        its first dword (the host only knows an upper bound); uses s56..59"""
+        I = Inst
+        l = self.lab("nitems")
+        return [I(f"s_load_dword s{dst}, s[0:1], {NITEMS_OFF}", SMEM, rd=sr(0, 2), wr=sr(dst)),
+                I("s_load_dword s56, s[0:1], 0xd0", SMEM, rd=sr(0, 2), wr=sr(56)),
+                I("s_load_dwordx2 s[58:59], s[0:1], 0x38", SMEM, rd=sr(0, 2), wr=sr(58, 2)),
+                I("s_waitcnt lgkmcnt(0)", WAIT),
+                I("s_bitcmp1_b32 s56, 2", SALU), I(f"s_cbranch_scc0 {l}", BRANCH),
+                I(f"s_load_dword s{dst}, s[58:59], 0x0", SMEM, rd=sr(58, 2), wr=sr(dst)),
+                I("s_waitcnt lgkmcnt(0)", WAIT), label(l)]
+
+    # ------------------------------------------------------------------ the pipelined item loop
+    def geometry_loop(self):
+        """(OPT_CONT) the record N of the workgroup's next item with keys and rows, from round V_ROUND
+        on; an item with keys and no rows stores zero dK / dV on the way; no item left: an empty
+        record (NLAST -1, zero records: the cursors that switch to it DMA zeros)"""
+        I = Inst
+        T0, T1, T2, T3, T4 = (S_TMP + i for i in range(5))
+        top, zero, none, done = self.lab("g_top"), self.lab("g_zero"), self.lab("g_none"), self.lab("g_done")
+        ins = [label(top),
+               I(f"s_load_dwordx2 s[{T1}:{T2}], s[0:1], {NITEMS_OFF}", SMEM, rd=sr(0, 2), wr=sr(T1, 2)),
+               I(f"v_readfirstlane_b32 s{T0}, v{V_ROUND}", RFL, rd=vr(V_ROUND), wr=sr(T0)),
+               I("s_waitcnt lgkmcnt(0)", WAIT)]
+        ins += self.n_items_ops(T1)
+        ins += item_pos_ops(S_ITEM, T0, 2, T2, T3, T4)
+        ins += [I(f"s_cmp_ge_u32 s{S_ITEM}, s{T1}", SALU), I(f"s_cbranch_scc1 {none}", BRANCH),
+                I(f"v_add_u32_e32 v{V_ROUND}, 1, v{V_ROUND}", VALU, rd=vr(V_ROUND), wr=vr(V_ROUND))]
+        ins += self.prologue(zero, l_nokeys=top, cont=True)
+        ins += [I(f"s_branch {done}", BRANCH), label(zero)]
+        ins += self.epilogue(stash=V_N + N_ST, zero=True)
+        ins += [I(f"s_branch {top}", BRANCH), label(none)]
+        empty = {N_NLAST: -1, N_NSP: 2}
+        ins += [I(f"v_mov_b32_e32 v{V_N + f}, {empty.get(f, 0)}", VALU, wr=vr(V_N + f)) for f in range(N_LEN)]
+        ins += [label(done)]
+        return ins
+
+    def copy_record(self):
+        """(OPT_CONT) C <- N"""
+        return [Inst(f"v_mov_b32_e32 v{V_C + f}, v{V_N + f}", VALU, rd=vr(V_N + f), wr=vr(V_C + f)) for f in range(N_LEN)]
+
+    def compute_from_c(self, first):
+        """(OPT_CONT) the compute side of the item in C: sweep geometry, mask lane values, the
+        epilogue's scalars, the ring read slots (first: from 0; else continuing: v99, v100)"""
+        I = Inst
+        T1, T2 = S_TMP + 1, S_TMP + 2
+
+        def rf(s_, v):
+            return I(f"v_readfirstlane_b32 s{s_}, v{v}", RFL, rd=vr(v), wr=sr(s_))
+        ins = [rf(S_QF, V_C + N_QF), rf(S_NLAST, V_C + N_NLAST), rf(S_NSP, V_C + N_NSP),
+               I(f"v_mov_b32_e32 v{V_LANEK}, v{V_C + N_LANEK}", VALU, rd=vr(V_C + N_LANEK), wr=vr(V_LANEK))]
+        ins += [I(f"v_mov_b32_e32 v{V_ST + i}, v{V_C + N_ST + i}", VALU, rd=vr(V_C + N_ST + i), wr=vr(V_ST + i))
+                for i in range(15)]
+        ins += [I(f"s_mov_b32 s{S_Q0V}, s{S_QF}", SALU, rd=sr(S_QF), wr=sr(S_Q0V)),
+                I(f"s_mov_b32 s{S_LOCV}, 0", SALU, wr=sr(S_LOCV)), I(f"s_mov_b32 s{S_N}, 0", SALU, wr=sr(S_N))]
+        if first:
+            ins += [I(f"s_mov_b32 s{S_SROW}, 0", SALU, wr=sr(S_SROW)),
+                    I(f"s_mov_b32 s{S_STR}, {RING - 2 * SLOT}", SALU, wr=sr(S_STR)),
+                    I(f"s_mov_b32 s{S_LRD}, {LBASE}", SALU, wr=sr(S_LRD))]
+        else:
+            ins += [rf(S_SROW, 99), rf(S_LRD, 100),
+                    I(f"s_sub_u32 s{T1}, s{S_SROW}, {2 * SLOT}", SALU, rd=sr(S_SROW), wr=sr(T1)),
+                    I(f"s_add_u32 s{T2}, s{T1}, {RING}", SALU, rd=sr(T1), wr=sr(T2)),
+                    I(f"s_cmp_lt_i32 s{T1}, 0", SALU, rd=sr(T1), wr=[("scc", 0)]),
+                    I(f"s_cselect_b32 s{S_STR}, s{T2}, s{T1}", SALU, rd=sr(T1) + sr(T2) + [("scc", 0)], wr=sr(S_STR))]
+        return ins
+
+    def reissue(self, name):
+        """(OPT_CONT, at the item switch) the cursor `name` now runs on the compute's item; if it
+        stalled at the end of that item, it moves to the next one (record N) and the subtiles it
+        DMA'd as zeros are issued again, from the slot where it stalled"""
+        I = Inst
+        T3, T4 = S_TMP + 3, S_TMP + 4
+        sw, stall, slot = (S_DSW, S_DSTALL, S_SDMA) if name == "d" else (S_LSW, S_LSTALL, S_LDMA)
+        ok, loop = self.lab("re_ok" + name), self.lab("re_loop" + name)
+        ins = [I(f"s_mov_b32 s{sw}, 0", SALU), I(f"s_cmp_eq_u32 s{stall}, -1", SALU), I(f"s_cbranch_scc1 {ok}", BRANCH),
+               I(f"s_sub_u32 s{T3}, s{slot}, s{stall}", SALU)]
+        if name == "d":
+            assert SLOT == 1 << 14
+            ins += [I(f"s_add_u32 s{T4}, s{T3}, {RING}", SALU), I(f"s_cmp_lt_i32 s{T3}, 0", SALU),
+                    I(f"s_cselect_b32 s{T3}, s{T4}, s{T3}", SALU), I(f"s_lshr_b32 s{T3}, s{T3}, 14", SALU)]
+        else:
+            ins += [I(f"s_and_b32 s{T3}, s{T3}, {NLS * LSLOT - 1}", SALU), I(f"s_lshr_b32 s{T3}, s{T3}, 8", SALU)]
+        ins += [I(f"s_mov_b32 s{slot}, s{stall}", SALU), I(f"s_mov_b32 s{stall}, -1", SALU)]
+        ins += self.switch_ops(name)
+        ins += [label(loop), I(f"s_cmp_eq_u32 s{T3}, 0", SALU), I(f"s_cbranch_scc1 {ok}", BRANCH)]
+        if name == "d":
+            ins += self.dma_subtile(False) + self.dma_subtile(False)
+        else:
+            ins += self.dma_l_only() + self.dma_l_only()
+        ins += self.wrap_check(name)
+        ins += [I(f"s_sub_u32 s{T3}, s{T3}, 2", SALU), I(f"s_branch {loop}", BRANCH), label(ok)]
+        return ins
+
+    def phase_m1(self):
+        """phase -1: chain starts of subtiles 0 (-> buffers 0) and 1 (-> 1), S / dP(0); the ring read
+        slots S_SROW, S_STR, S_LRD of subtiles 0, -2, 0 (set by the caller under OPT_CONT)"""
+        if OPT_CONT:
+            ph = [Inst(f"v_add_u32_e32 v{V_KB0}, s{S_SROW}, v{V_RB0}", VALU, rd=sr(S_SROW) + vr(V_RB0), wr=vr(V_KB0)),
+                  Inst(f"v_add_u32_e32 v{V_KB1}, s{S_SROW}, v{V_RB1}", VALU, rd=sr(S_SROW) + vr(V_RB1), wr=vr(V_KB1))]
+        else:
+            ph = [Inst(f"s_mov_b32 s{S_SROW}, 0", SALU, wr=sr(S_SROW)),
+                  Inst(f"s_mov_b32 s{S_STR}, {RING - 2 * SLOT}", SALU, wr=sr(S_STR)),   # slot of subtile -2
+                  Inst(f"s_mov_b32 s{S_LRD}, {LBASE}", SALU, wr=sr(S_LRD)),
+                  Inst(f"v_add_u32_e32 v{V_KB0}, 0, v{V_RB0}", VALU, rd=vr(V_RB0), wr=vr(V_KB0)),
+                  Inst(f"v_add_u32_e32 v{V_KB1}, 0, v{V_RB1}", VALU, rd=vr(V_RB1), wr=vr(V_KB1))]
+        ph += [Inst(f"v_add_u32_e32 v{V_LCUR}, s{S_LRD}, v{V_LB}", VALU, rd=sr(S_LRD) + vr(V_LB), wr=vr(V_LCUR))]
+        ini0 = self.init_reads(0)
+        for op in ini0:
+            op.dl = 0            # S / dP(0) chains start from them
+        ph += ini0
+        ph += self.lslot_advance(S_LRD)
+        ph += [Inst(f"v_add_u32_e32 v{V_LCUR}, s{S_LRD}, v{V_LB}", VALU, rd=sr(S_LRD) + vr(V_LB), wr=vr(V_LCUR))]
+        ph += self.init_reads(1)
+        ph += self.lslot_advance(S_LRD)
+        ph += [Inst(f"v_add_u32_e32 v{V_LCUR}, s{S_LRD}, v{V_LB}", VALU, rd=sr(S_LRD) + vr(V_LB), wr=vr(V_LCUR))]
+        mf = self.phase_mfmas(1, True, False)     # S / dP(0) -> buffers 0
+        fill = []
+        for m, (_, t, i) in enumerate(mf):
+            fill += self.frag_reads(m, t, i, key=-100 + m, deadline=max(m - 2, 0))
+        fill += self.slot_advance(S_SROW, key=400) + self.slot_advance(S_STR, key=400)
+        fill += [Inst(f"v_add_u32_e32 v{V_KB0}, s{S_SROW}, v{V_RB0}", VALU, rd=sr(S_SROW) + vr(V_RB0), wr=vr(V_KB0), key=401),
+                 Inst(f"v_add_u32_e32 v{V_KB1}, s{S_SROW}, v{V_RB1}", VALU, rd=sr(S_SROW) + vr(V_RB1), wr=vr(V_KB1), key=401),
+                 Inst(f"v_add_u32_e32 v{V_VB0}, s{S_STR}, v{V_TB0}", VALU, rd=sr(S_STR) + vr(V_TB0), wr=vr(V_VB0), key=401),
+                 Inst(f"v_add_u32_e32 v{V_VB1}, s{S_STR}, v{V_TB1}", VALU, rd=sr(S_STR) + vr(V_TB1), wr=vr(V_VB1), key=401)]
+        nm = self.phase_mfmas(0, True, False)     # phase 0 of the first step: S / dP only
+        for m in range(3):
+            _, t, i = nm[m]
+            fill += self.frag_reads(m, t, i, key=600 + m, earliest=m)
+        sch = schedule([x[0] for x in mf], ph + fill)
+        # step 0 reads Q / dO <= 3 and LSE / D <= 3: the same wait as at every step's end
+        sch += [Inst(f"s_waitcnt vmcnt({VMCNT_STEP}) lgkmcnt(0)", WAIT), Inst("s_barrier", BARRIER)]
+        sch += self.stamp(V_SS + 5)
+        return sch
+
+    def steps_code(self, emit, code):
+        """the step dispatch, the step variants and the tail (control flow as build())"""
+        L = {}
+        variants = [(f, l, m) for f in (True, False) for l in (True, False) for m in ((True, False) if self.causal else (False,))
+                    if not (f and self.causal and not m)]
+        for v in variants:
+            L[v] = self.lab("step_" + ("".join(c for c, on in zip("FLM", v) if on) or "R"))
+        l_tail = self.lab("tail")
+        l_disp = self.lab("dispatch")
+        l_notlast = self.lab("notlast")
+        fm = self.causal
+        code += [Inst(f"s_cmp_eq_u32 s{S_NLAST}, 0", SALU), Inst(f"s_cbranch_scc1 {L[(True, True, fm)]}", BRANCH),
+                 Inst(f"s_branch {L[(True, False, fm)]}", BRANCH)]
+        code += [label(l_disp), Inst(f"s_cmp_gt_u32 s{S_N}, s{S_NLAST}", SALU), Inst(f"s_cbranch_scc1 {l_tail}", BRANCH),
+                 Inst(f"s_cmp_lt_u32 s{S_N}, s{S_NLAST}", SALU), Inst(f"s_cbranch_scc1 {l_notlast}", BRANCH)]
+        if self.causal:
+            code += [Inst(f"s_cmp_lt_u32 s{S_LOCV}, 4", SALU), Inst(f"s_cbranch_scc1 {L[(False, True, True)]}", BRANCH)]
+        code += [Inst(f"s_branch {L[(False, True, False)]}", BRANCH), label(l_notlast)]
+        if self.causal:
+            code += [Inst(f"s_cmp_lt_u32 s{S_LOCV}, 4", SALU), Inst(f"s_cbranch_scc1 {L[(False, False, True)]}", BRANCH)]
+        code += [Inst(f"s_branch {L[(False, False, False)]}", BRANCH)]
+        pad = [nop(15)]
+        for v in variants:
+            f, l, m = v
+            code.append(label(L[v]))
+            emit(self.step(f, l, m) + self.step_end(l), pre=pad)
+            code.append(Inst(f"s_branch {l_disp}", BRANCH))
+        code.append(label(l_tail))
+        emit(self.tail(), pre=pad)
+
+    def build_cont(self):
+        """the kernel with the pipelined item loop (OPT_CONT): per workgroup
+             N <- record(first item); C <- N; N <- record(next); DMA and K / V loads of C's first
+             subtiles; then per item: phase -1, steps (the cursors run into N's subtiles at the end
+             of C's sweep, the last step loads N's K / V), tail, epilogue; C <- N;
+             N <- record(next) (the DMA side's registers saved across it); re-issue a stalled
+             cursor; next item"""
+        assert not OPT_STAMP, "the workgroup timeline build (FA_GBW_STAMP=1) is for the item-at-a-time loop"
+        self.lab_end = self.lab("end")
+        self.lab_next = None
+        self.ool = []
+        code = []
+        I = Inst
+        pad = [nop(15)]
+
+        def emit(insts, pre=()):
+            out, _ = add_waits(insts)
+            out, _ = fix_hazards(out, pre=pre)
+            code.extend(out)
+
+        T0, T1 = S_TMP, S_TMP + 1
+        l_common, l_switch, l_drain = self.lab("common"), self.lab("switch"), self.lab("drain")
+        emit([I("v_lshrrev_b32_e32 v1, 6, v0", VALU, rd=vr(0), wr=vr(1)),
+              I(f"v_readfirstlane_b32 s{S_WAVE}, v1", RFL, rd=vr(1), wr=sr(S_WAVE)),
+              I(f"v_and_b32_e32 v{V_LANE}, 63, v0", VALU, rd=vr(0), wr=vr(V_LANE)),
+              I(f"v_mov_b32_e32 v{V_ROUND}, 0", VALU, wr=vr(V_ROUND))] +
+             [I(f"v_mov_b32_e32 v{V_ZERO + i}, 0", VALU, wr=vr(V_ZERO + i)) for i in range(4)] +
+             ([I(f"v_mov_b32_e32 v{V_SS + i}, 0", VALU) for i in range(16)] + self.stamp(None) if OPT_STEPSTAMP else []))
+        zero_acc = [I(f"v_accvgpr_write_b32 a{i}, 0", ACCW, wr=ar(i)) for i in range(128)]
+        no_item = [I(f"v_readfirstlane_b32 s{T0}, v{V_N + N_NLAST}", RFL, rd=vr(V_N + N_NLAST), wr=sr(T0)),
+                   I(f"s_cmp_lt_i32 s{T0}, 0", SALU, rd=sr(T0), wr=[("scc", 0)]),
+                   I(f"s_cbranch_scc1 {l_drain}", BRANCH)]
+        # ---- the first item ----
+        emit(self.geometry_loop(), pre=pad)
+        save = [I(f"v_mov_b32_e32 v{V_SAVE + i}, s{r}", VALU, rd=sr(r), wr=vr(V_SAVE + i)) for i, r in enumerate(DMA_SIDE)]
+        restore = [I(f"v_readfirstlane_b32 s{r}, v{V_SAVE + i}", RFL, rd=vr(V_SAVE + i), wr=sr(r)) for i, r in enumerate(DMA_SIDE)]
+        emit(no_item + self.copy_record() + save, pre=pad)
+        emit(self.geometry_loop(), pre=pad)
+        start = restore + self.switch_ops("d", rec=V_C) + self.switch_ops("l", rec=V_C)
+        start += [I(f"s_mov_b32 s{r}, {v}", SALU, wr=sr(r)) for r, v in
+                  ((S_DSW, 0), (S_LSW, 0), (S_DSTALL, -1), (S_LSTALL, -1), (S_SDMA, 0), (S_LDMA, LBASE))]
+        start += self.kv_next_ops(rec=V_C)
+        start += self.prologue_dma()
+        start += self.compute_from_c(first=True) + zero_acc
+        # Q / dO(0), (1), LSE / D(0, 1) and K / V landed; younger than Q / dO(1): 21 (as build())
+        start += [I("s_waitcnt vmcnt(21)", WAIT)]
+        emit(start, pre=pad)
+        code.append(I(f"s_branch {l_common}", BRANCH))
+        # ---- the item switch (after the epilogue) ----
+        code.append(label(l_switch))
+        sw = list(no_item)
+        # the continuing ring read slots of the next item's subtile 0 / LSE subtile 0
+        sw += [I(f"s_sub_u32 s{T1}, s{S_SROW}, {SLOT}", SALU, rd=sr(S_SROW), wr=sr(T1)),
+               I(f"s_add_u32 s{T0}, s{T1}, {RING}", SALU, rd=sr(T1), wr=sr(T0)),
+               I(f"s_cmp_lt_i32 s{T1}, 0", SALU, rd=sr(T1), wr=[("scc", 0)]),
+               I(f"s_cselect_b32 s{T1}, s{T0}, s{T1}", SALU, rd=sr(T0) + sr(T1) + [("scc", 0)], wr=sr(T1)),
+               I(f"v_mov_b32_e32 v99, s{T1}", VALU, rd=sr(T1), wr=vr(99)),
+               I(f"s_sub_u32 s{T1}, s{S_LRD}, {2 * LSLOT}", SALU, rd=sr(S_LRD), wr=sr(T1)),
+               I(f"s_and_b32 s{T1}, s{T1}, {NLS * LSLOT - 1}", SALU, rd=sr(T1), wr=sr(T1)),
+               I(f"s_or_b32 s{T1}, s{T1}, {LBASE}", SALU, rd=sr(T1), wr=sr(T1)),
+               I(f"v_mov_b32_e32 v100, s{T1}", VALU, rd=sr(T1), wr=vr(100))]
+        sw += self.copy_record() + save
+        emit(sw, pre=pad)
+        emit(self.geometry_loop(), pre=pad)
+        rs = list(restore)
+        rs += self.stamp(V_SS + 10)
+        rs += zero_acc + [I("s_waitcnt vmcnt(0)", WAIT)]
+        rs += self.stamp(V_SS + 11)
+        rs += self.reissue("d") + self.reissue("l")
+        rs += self.compute_from_c(first=False)
+        emit(rs, pre=pad)
+        # ---- one item ----
+        code.append(label(l_common))
+        emit(self.stamp(V_SS + 14) + [I("s_barrier", BARRIER)] + self.stamp(V_SS + 15) + self.phase_m1(), pre=pad)
+        self.steps_code(emit, code)
+        emit([nop(15)] + self.epilogue() + self.stamp(V_SS + 6, count=V_SS + 7), pre=pad)
+        code.append(I(f"s_branch {l_switch}", BRANCH))
+        code.append(label(l_drain))
+        code.append(I("s_waitcnt vmcnt(0)", WAIT))
+        code.append(label(self.lab_end))
+        if OPT_STEPSTAMP:
+            code.extend([I("s_waitcnt vmcnt(0)", WAIT), I("s_load_dwordx2 s[52:53], s[0:1], 0xd8", SMEM),
+                         I("s_waitcnt lgkmcnt(0)", WAIT),
+                         I("s_cmp_eq_u64 s[52:53], 0", SALU), I("s_cselect_b32 s54, 0, 0x7fffffff", SALU),
+                         I("s_mov_b32 s55, 0x20000", SALU), I("s_and_b32 s53, s53, 0xffff", SALU),
+                         I("s_lshl_b32 s50, s2, 2", SALU), I(f"s_add_u32 s50, s50, s{S_WAVE}", SALU),
+                         I("s_lshl_b32 s50, s50, 6", SALU), I(f"v_mov_b32_e32 v{V_SS + 8}, 0", VALU), nop(4)] +
+                        [I(f"buffer_store_dwordx4 v[{V_SS + 4 * j}:{V_SS + 4 * j + 3}], v{V_SS + 8}, s[52:55], s50 offen offset:{16 * j}", VSTORE)
+                         for j in range(4)] + [I("s_waitcnt vmcnt(0)", WAIT)])
+        code.append(Inst("s_endpgm", SOPP))
+        code.extend(self.ool)
+        return code
+
     def render(self):
-        code = self.build()
+        code = self.build_cont() if OPT_CONT else self.build()
         out = [f"\t.globl {self.name}", "\t.p2align 8", f"\t.type {self.name},@function", f"{self.name}:"]
         for ins in code:
             out.append(ins.text if ins.kind == LABEL else "\t" + ins.text)

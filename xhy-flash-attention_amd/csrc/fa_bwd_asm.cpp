@@ -46,7 +46,8 @@ struct BwdAsmArgs {
   int32_t q_head, k_head, v_head, do_head, dk_head, dv_head;           // bytes
   int32_t sq, sk, h, ng, nh, group;
   float c, scale;
-  int32_t flags;    // bit 0: varlen_padded_input, bit 1: dK / dV reduced over the GQA group
+  int32_t flags;    // bit 0: varlen_padded_input, bit 1: dK / dV reduced over the GQA group, bit 2: the
+                    // items come from the device-built list at sched (count first, entries 8 bytes in)
   int32_t pad;
   void* stamps;     // dev timeline buffer (a generator build with FA_GBW_STAMP=1 writes it), else unused
   ItemDecode dec;   // the work order, computed in the kernel from the item index
@@ -162,16 +163,31 @@ void launch_bwd_dkdv_asm(const BwdParams& p, bool is_bf16, hipStream_t stream) {
     cus = m.cus;
   }
   // persistent grid (knob 6, default on): one workgroup per CU (151 KiB of LDS allows one) walking the
-  // heaviest-first item list in snake order -- no workgroup dispatch between items.  Fixed length
-  // only: varlen items range from empty to a full sweep, and the static snake assignment then
-  // leaves CUs idle where the dispatcher's dynamic one does not (C4: dK/dV 3.48 vs 3.16 ms, dQ
-  // 2.25 vs 2.07, profiles/r04/ab_bwd_persist_c4_r04l.txt)
-  const bool persist = knob(kKnobBwdPersist) != 0 && s.cu_seqlens_q == nullptr && s.cu_seqlens_k == nullptr;
-  const long long grid = (persist && cus > 0 && nwg > cus) ? cus : nwg;
+  // heaviest-first item list in snake order -- no workgroup dispatch between items.  Fixed length;
+  // varlen only with knob 6 = 2, from a device-built list (varlen_items_kernel, as the forward: the
+  // key blocks of every sequence, heaviest level first, none past a sequence's end).  The
+  // dispatcher's dynamic balance over the decoded order (a head's key blocks on one XCD) beats it:
+  // C4 dK/dV 2.89 ms one workgroup per item, 3.23 from the list, 3.48 walking the decoded order
+  // (profiles/r05/ab_list_c4_r05h.txt, r04/ab_bwd_persist_c4_r04l.txt)
+  const bool varlen = s.cu_seqlens_q != nullptr || s.cu_seqlens_k != nullptr;
+  const bool dev_list = varlen && knob(kKnobBwdPersist) >= 2 && s.cu_seqlens_k != nullptr &&
+                        varlen_items_fit(s.b, nblk) && nwg <= (1ll << 28);
+  const bool persist = knob(kKnobBwdPersist) != 0 && (!varlen || dev_list);
+  long long grid = (persist && cus > 0 && nwg > cus) ? cus : nwg;
+  StreamScratch vbuf;          // device-built varlen work list (stream-ordered allocation)
+  uint32_t* vtab = dev_list ? build_varlen_items(vbuf, s.cu_seqlens_k, s.b, nh_grid, p.gqa_reduce ? 1 : s.h / s.hk,
+                                                 kBkn, nblk, true, nwg, stream)
+                            : nullptr;
+  // varlen, one workgroup per item: R items per workgroup instead (knob 9, default 2) in snake-paired
+  // rounds (item w, then the mirror of w, ...), the dispatcher still balancing the workgroups; G a
+  // multiple of 8 keeps each on its XCD's items.  C4 dK/dV -2 % at R = 2
+  // (profiles/r05/ab_rounds_c4_r05h.txt)
+  const int rounds = knob(kKnobVarlenRounds);
+  if (!persist && varlen && rounds > 1 && nwg > 8ll * rounds) grid = ((nwg + rounds - 1) / rounds + 7) / 8 * 8;
   BwdAsmArgs a;
   std::memset(&a, 0, sizeof(a));
   a.q = p.q; a.k = p.k; a.v = p.v; a.dout = p.dout; a.dk = p.dk; a.dv = p.dv;
-  a.lsed = p.lsed; a.sched = nullptr; a.cu_q = s.cu_seqlens_q; a.cu_k = s.cu_seqlens_k;
+  a.lsed = p.lsed; a.sched = vtab; a.cu_q = s.cu_seqlens_q; a.cu_k = s.cu_seqlens_k;
   a.q_batch = 2 * p.q_batch; a.k_batch = 2 * p.k_batch; a.v_batch = 2 * p.v_batch;
   int64_t q_row = p.q_row, q_head = p.q_head;
   if (p.qfold != nullptr) {   // the Q' the dQ kernel wrote (it ran first: fused preprocessing)
@@ -188,7 +204,7 @@ void launch_bwd_dkdv_asm(const BwdParams& p, bool is_bf16, hipStream_t stream) {
   a.group = s.h / s.hk;
   a.nh = p.gqa_reduce ? a.group : 1;
   a.c = s.scale_log2; a.scale = s.scale;
-  a.flags = (s.varlen_padded_input ? 1 : 0) | (p.gqa_reduce ? 2 : 0);
+  a.flags = (s.varlen_padded_input ? 1 : 0) | (p.gqa_reduce ? 2 : 0) | (vtab != nullptr ? 4 : 0);
   a.stamps = g_stamps;
   a.dec = dkdv_item_decode(s.b * nh_grid, nh_grid, p.gqa_reduce ? 1 : s.h / s.hk, nblk);
   a.n_items = (int32_t)nwg;
@@ -235,6 +251,8 @@ void launch_bwd_dq_asm(const BwdParams& p, bool is_bf16, hipStream_t stream) {
   // persistent grid (knob 6): one workgroup per CU walking the item list in snake order (fixed
   // length only, as dK/dV)
   const bool persist = knob(kKnobBwdPersist) != 0 && s.cu_seqlens_q == nullptr && s.cu_seqlens_k == nullptr;
+  // (varlen: one workgroup per query block -- two per workgroup as dK/dV's knob 9 measured C4 dQ
+  // 2.151 vs 2.140 ms, profiles/r05/ab_rounds2_c4_r05h.txt)
   const long long grid = (persist && cus > 0 && nwg > cus) ? cus : nwg;
   DqAsmArgs a;
   std::memset(&a, 0, sizeof(a));

@@ -189,13 +189,16 @@ enum Knob { kKnobNoSplitKv = 0 /* FLASH_ATTN_MI355X_NO_SPLITKV: 1 = never split 
             kKnobFwdPersist = 5 /* FLASH_ATTN_MI355X_FWD_PERSIST: 0 = assembly forward with one
                                    workgroup per item, 1 = one persistent workgroup per CU */,
             kKnobBwdPersist = 6 /* FLASH_ATTN_MI355X_BWD_PERSIST: the same for the assembly dK/dV and
-                                   dQ kernels */,
+                                   dQ kernels, fixed length; 2 also varlen dK/dV (device-built list) */,
             kKnobAsmXcdGroupMinMiB = 7 /* FLASH_ATTN_MI355X_ASM_XCD_GROUP_MIN_MIB: knob 2's threshold
                                           for the persistent assembly forward / dQ (default 0) */,
             kKnobFusePre = 8 /* FLASH_ATTN_MI355X_FUSE_PRE: 1 (default) = the assembly dQ kernel computes
                                 D and writes softmax_d and the dK/dV scratch itself (no bwd_pre_kernel);
                                 dQ runs first.  0 = bwd_pre_kernel, then dK/dV and dQ */,
-            kNumKnobs = 9 };
+            kKnobVarlenRounds = 9 /* FLASH_ATTN_MI355X_VARLEN_ROUNDS: items per workgroup of the assembly
+                                     dK/dV kernel on varlen calls (default 2, snake-paired
+                                     rounds; 1 = one workgroup per item, the dispatcher balancing) */,
+            kNumKnobs = 10 };
 int knob(int id);
 void set_knob(int id, int value);
 
