@@ -224,6 +224,7 @@ OPT_EPISTAMP = os.environ.get("FA_GEN_STAMP") == "3"
 # FA_GEN_STAMP=4: the item start split -- geometry (epilogue end -> tile 0's wait) in the item-start
 # slot, tile 0's vmcnt wait in the tile-0 slot, its barrier wait in V_SSUM + 5 (record offset 96)
 OPT_T0STAMP = os.environ.get("FA_GEN_STAMP") == "4"
+OPT_STAMP_NONFAST = os.environ.get("FA_GEN_STAMP_ONLY") == "nonfast"
 V_SSUM = 174 if OPT_FOLD else 240   # +0..4: compute, wait, barrier sums, step count, last stamp;
                   # +6..9: item phases: tile 0, last step, epilogue, item start (geometry .. tile 0's barrier)
 # latency-aware gap scheduling (isa.schedule lat=): "valu,trans,lds,mfma" result latencies in cycles
@@ -615,7 +616,18 @@ class K:
                Inst(f"s_cselect_b32 s{S_VOFF}, s{t + 2}, s{S_VOFF}", SALU, rd=sr(t + 2) + sr(S_VOFF) + [("scc", 0)], wr=sr(S_VOFF), key=803)]
         ys = schedule(my, fy, budget=(OPT_BUDGET64 if D == 64 else OPT_BUDGET), lat=OPT_LAT)
         body = xs + ys
-        if not last and OPT_STEPSTAMP:
+        if not last and OPT_STEPSTAMP and OPT_STAMP_NONFAST and variant == "fast":
+            # (FA_GEN_STAMP_ONLY=nonfast: the fast steps only move the last stamp, so the sums and the
+            # count are those of the masked / diagonal / dead steps alone)
+            A, t0 = S_TMP, V_T
+            body += [Inst(f"s_add_u32 s{S_N}, s{S_N}, 1", SALU, rd=sr(S_N), wr=sr(S_N) + [("scc", 0)]),
+                     Inst(f"s_add_u32 s{S_N0}, s{S_N0}, {BN}", SALU, rd=sr(S_N0), wr=sr(S_N0) + [("scc", 0)]),
+                     Inst(f"s_waitcnt vmcnt({2 * NP}) lgkmcnt(0)", WAIT),
+                     Inst("s_barrier", BARRIER),
+                     Inst(f"s_memtime s[{A}:{A + 1}]", SMEM),
+                     Inst("s_waitcnt lgkmcnt(0)", WAIT),
+                     Inst(f"v_mov_b32_e32 v{V_SSUM + 4}, s{A}", VALU)]
+        elif not last and OPT_STEPSTAMP:
             A, B, t0 = S_TMP, S_TMP + 2, V_T
             body += [Inst(f"s_add_u32 s{S_N}, s{S_N}, 1", SALU, rd=sr(S_N), wr=sr(S_N) + [("scc", 0)]),
                      Inst(f"s_add_u32 s{S_N0}, s{S_N0}, {BN}", SALU, rd=sr(S_N0), wr=sr(S_N0) + [("scc", 0)]),
