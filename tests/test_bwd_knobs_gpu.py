@@ -7,7 +7,7 @@ case with ragged sequences; d = 128 (the assembly backward's domain)."""
 import pytest
 import torch
 
-from knobs import BWD_PERSIST, FUSE_PRE, knob
+from knobs import BWD_PERSIST, FUSE_PRE, VARLEN_ROUNDS, knob
 from oracle.attention_ref import attention_ref, check_within_bound
 
 pytestmark = pytest.mark.gpu
@@ -84,3 +84,31 @@ def test_varlen_2x_rule(fuse, causal):
                 dst[name][a:e] = t[0].float()
     for name, got in (("out", out), ("dq", dq), ("dk", dk), ("dv", dv)):
         _bound(name, got, refs[name], pts[name])
+
+
+@pytest.mark.parametrize("causal", [True, False])
+@pytest.mark.parametrize("hk", [4, 1])
+def test_varlen_rounds_bitwise(causal, hk):
+    """knob 9 (items per dK/dV workgroup on varlen launches, snake-paired rounds) and knob 6 = 2 (the
+    persistent loop over the device-built work list): the same per-item arithmetic in any work
+    order, so dK / dV are bitwise those of one workgroup per item -- for items without keys (an
+    empty sequence, blocks past a sequence's end) and GQA reduced in the kernel as well"""
+    from flash_attn import flash_attn_varlen_func
+
+    torch.manual_seed(2)
+    lens = [700, 0, 130, 2100, 64, 1025, 9]
+    h, d = 4, 128
+    cu = torch.tensor([0] + lens, dtype=torch.int64).cumsum(0).to(torch.int32).to(DEV)
+    total = sum(lens)
+    q = torch.randn(total, h, d, device=DEV, dtype=torch.bfloat16, requires_grad=True)
+    k, v = (torch.randn(total, hk, d, device=DEV, dtype=torch.bfloat16, requires_grad=True) for _ in range(2))
+    out = flash_attn_varlen_func(q, k, v, cu, cu, max(lens), max(lens), causal=causal)
+    g = torch.randn_like(out)
+    res = {}
+    for rounds, persist in ((1, 1), (2, 1), (3, 1), (1, 2)):
+        with knob(VARLEN_ROUNDS, rounds), knob(BWD_PERSIST, persist):
+            res[(rounds, persist)] = torch.autograd.grad(out, (q, k, v), g, retain_graph=True)
+    base = res[(1, 1)]
+    for key, grads in res.items():
+        for name, x, y in zip(("dq", "dk", "dv"), grads, base):
+            assert torch.equal(x, y), (key, name, (x.float() - y.float()).abs().max().item())
