@@ -144,6 +144,9 @@ NITEMS_OFF = 264  # n_items, grid (persistent item loop)
 
 # dev A/B switches, read when the .s is generated (tools/asm_variant.sh)
 OPT_WIN = int(os.environ.get("FA_GBW_WIN", "16"))     # an A fragment may be read up to WIN MFMAs ahead
+# (a read more than 16 MFMAs ahead would overwrite the ring slot (16 fragments) an earlier MFMA
+# still reads: the scheduler orders fillers among themselves, the MFMA sequence only by earliest)
+assert 2 <= OPT_WIN <= 16, "FA_GBW_WIN must be within the 16-slot fragment ring"
 OPT_LEAD = int(os.environ.get("FA_GBW_LEAD", "2"))    # ... and at least LEAD MFMAs ahead
 # dev timeline: every workgroup stores {start, end} s_memtime, HW_ID, XCC_ID, id at the `stamps`
 # kernarg address + 32 id (tools/bwd_stamps.py)

@@ -58,6 +58,9 @@ KQ = 6                  # K / V subtile s is DMA'd in step (s - KQ) / 2
 VMCNT_STEP = 8
 
 OPT_WIN = int(os.environ.get("FA_GDQ_WIN", "16"))
+# (a read more than 16 MFMAs ahead would overwrite the ring slot (16 fragments) an earlier MFMA
+# still reads: the scheduler orders fillers among themselves, the MFMA sequence only by earliest)
+assert 2 <= OPT_WIN <= 16, "FA_GDQ_WIN must be within the 16-slot fragment ring"
 OPT_LEAD = int(os.environ.get("FA_GDQ_LEAD", "2"))
 OPT_OWAIT = int(os.environ.get("FA_GDQ_OWAIT", "23"))
 
