@@ -173,7 +173,9 @@ OPT_NOZERO = os.environ.get("FA_GEN_NOZERO") == "1"          # never zero K/V re
 OPT_NODIAG = os.environ.get("FA_GEN_NODIAG") == "1"          # causal diagonal: generic masked steps only
 OPT_PLAIN_SNAKE = os.environ.get("FA_GEN_PLAIN_SNAKE") == "1"  # snake reversal over single workgroups
 OPT_BUDGET = int(os.environ.get("FA_GEN_BUDGET", "24"))        # filler issue cycles per MFMA gap
-OPT_BUDGET64 = int(os.environ.get("FA_GEN_BUDGET64", str(OPT_BUDGET)))  # ... at head dim 64
+# ... at head dim 64, where the softmax VALU outweighs the 16 MFMAs of a phase: a fuller gap (32)
+# ran C2 -0.7 / -0.9 % in two one-process A/Bs, 40 +-0, 48 / 64 +3 / +5 % (profiles/r05/ab_b64*_c2_r05p.txt)
+OPT_BUDGET64 = int(os.environ.get("FA_GEN_BUDGET64", "32"))
 OPT_ZERO_NOP = int(os.environ.get("FA_GEN_ZERO_NOP", "0"))    # s_nop 15 x N before zeroing them
 OPT_SHIFT = int(os.environ.get("FA_GEN_SHIFT", "0"))          # s_nop 0 x N at the kernel entry (code placement)
 OPT_ALIGN = int(os.environ.get("FA_GEN_ALIGN", "0"))          # .p2align N before each step body (code placement)
