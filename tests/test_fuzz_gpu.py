@@ -1,0 +1,125 @@
+"""Seeded random shapes through the full autograd path against the oracle (2x rule of the reference,
+tests/test_flash_attn.py:630-639): odd and ragged sequence lengths, GQA ratios, causal or not,
+bf16 / fp16, fixed length and varlen.  Head dims 64 and 128 run the hand-scheduled assembly kernels
+(forward, dK/dV, dQ), whose schedules are generated -- a random sweep of shapes is the cheap way to
+catch a latent schedule bug (a register live across an out-of-line branch, a ring slot reused early)
+that the fixed parametrizations miss; head dim 96 runs the HIP kernels."""
+import random
+
+import pytest
+import torch
+
+from oracle.attention_ref import (attention_lse_pt, attention_lse_ref, attention_ref,
+                                  check_lse_within_bound, check_within_bound)
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda"
+
+
+@pytest.fixture(scope="module", autouse=True)
+def _need_gpu():
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    import flash_attn_2_cuda  # noqa: F401
+
+
+def _case(seed):
+    r = random.Random(seed)
+    d = r.choice([64, 128, 128, 128, 96])
+    hk = r.choice([1, 2, 4])
+    h = hk * r.choice([1, 2, 3, 4])
+    dtype = r.choice([torch.bfloat16, torch.bfloat16, torch.float16])
+    causal = r.random() < 0.6
+    varlen = r.random() < 0.35
+    if varlen:
+        lens = [r.choice([0, 1, r.randint(2, 130), r.randint(131, 900)]) for _ in range(r.randint(1, 5))]
+        if sum(lens) == 0:
+            lens[0] = 77
+        return dict(d=d, h=h, hk=hk, dtype=dtype, causal=causal, lens=lens)
+    b = r.randint(1, 3)
+    sq = r.choice([1, r.randint(2, 200), r.randint(200, 1100)])
+    sk = sq if r.random() < 0.6 else r.choice([1, r.randint(2, 300), r.randint(300, 1100)])
+    return dict(d=d, h=h, hk=hk, dtype=dtype, causal=causal, b=b, sq=sq, sk=sk)
+
+
+def _bound(name, got, ref, pt, c):
+    # floor: with one key dS = P (dP - D) is exactly 0 and so is the reference dK, which PyTorch's
+    # softmax backward reproduces exactly (pt error 0); the kernel's dP and D are two fp32 dot products
+    # summed in different orders, so dK keeps their rounding noise summed over the rows (~1e-5)
+    ok, err, bound = check_within_bound(got.float(), ref.float(), pt.float(), floor=1e-4)
+    assert ok, f"{c}: {name} max|err| {err:.3e} > bound {bound:.3e}"
+
+
+def _ref_grads(q, k, v, g, causal):
+    out = {}
+    for upcast, key in ((True, "ref"), (False, "pt")):
+        qr, kr, vr = (x.detach().clone().requires_grad_() for x in (q, k, v))
+        o, _ = attention_ref(qr, kr, vr, causal=causal, upcast=upcast, reorder_ops=not upcast)
+        out[key] = (o,) + tuple(torch.autograd.grad(o, (qr, kr, vr), g))
+    return out
+
+
+def _check_lse(lse, q, k, c):
+    """the 2x rule / atol of check_lse_within_bound, plus -- on the assembly forward (d 64 / 128),
+    which scores with Q' = round(scale log2e Q) (DESIGN.md deviation 8) -- that rounding's a-priori
+    bound: |dQ'| <= u |Q'| per element, so each score moves by at most u sum_i |scale q_i k_i| and the
+    LSE, a smooth maximum of the scores, by at most the largest of those over the row's keys (taken
+    over all keys: an upper bound).  With many keys the rounding averages out; a row with one key
+    (sq = sk = 1) sees it whole."""
+    causal = c["causal"]
+    ref, pt = attention_lse_ref(q, k, causal), attention_lse_pt(q, k, causal)
+    ok, err, pt_err = check_lse_within_bound(lse, ref, pt)
+    if ok or c["d"] not in (64, 128):
+        assert ok, f"{c}: lse err {err:.3e} (pt {pt_err:.3e})"
+        return
+    u = 2.0 ** -8 if q.dtype == torch.bfloat16 else 2.0 ** -11
+    g = q.shape[2] // k.shape[2]
+    kk = k.detach().float().abs().repeat_interleave(g, dim=2)
+    fold = torch.einsum("bqhd,bkhd->bhqk", q.detach().float().abs(), kk).amax(-1) * (u / q.shape[-1] ** 0.5)
+    lse_, ref_, pt_ = (x.detach().double().cpu() for x in (lse, ref, pt))
+    live = ~torch.isinf(ref_)
+    bound = torch.clamp(1e-3 + 1e-4 * ref_.abs(), min=2 * pt_err) + fold.double().cpu()
+    e = (lse_ - ref_).abs()
+    assert bool((e[live] <= bound[live]).all()), f"{c}: lse err {err:.3e} (pt {pt_err:.3e}, fold bound {bound.max():.3e})"
+
+
+@pytest.mark.parametrize("seed", range(160))
+def test_random_shape(seed):
+    from flash_attn import flash_attn_func, flash_attn_varlen_func
+
+    c = _case(seed)
+    torch.manual_seed(1000 + seed)
+    d, h, hk, dtype, causal = c["d"], c["h"], c["hk"], c["dtype"], c["causal"]
+    if "lens" not in c:
+        b, sq, sk = c["b"], c["sq"], c["sk"]
+        q = torch.randn(b, sq, h, d, device=DEV, dtype=dtype, requires_grad=True)
+        k, v = (torch.randn(b, sk, hk, d, device=DEV, dtype=dtype, requires_grad=True) for _ in range(2))
+        out, lse, _ = flash_attn_func(q, k, v, causal=causal, return_attn_probs=True)
+        g = torch.randn_like(out)
+        dq, dk, dv = torch.autograd.grad(out, (q, k, v), g)
+        rg = _ref_grads(q, k, v, g, causal)
+        for name, got, r_, p_ in zip(("out", "dq", "dk", "dv"), (out, dq, dk, dv), rg["ref"], rg["pt"]):
+            _bound(name, got, r_, p_, c)
+        _check_lse(lse, q, k, c)
+        return
+    lens = c["lens"]
+    cu = torch.tensor([0] + lens, dtype=torch.int64).cumsum(0).to(torch.int32).to(DEV)
+    total, mx = sum(lens), max(lens)
+    q = torch.randn(total, h, d, device=DEV, dtype=dtype, requires_grad=True)
+    k, v = (torch.randn(total, hk, d, device=DEV, dtype=dtype, requires_grad=True) for _ in range(2))
+    out = flash_attn_varlen_func(q, k, v, cu, cu, mx, mx, causal=causal)
+    g = torch.randn_like(out)
+    dq, dk, dv = torch.autograd.grad(out, (q, k, v), g)
+    # the whole packed tensors under the rule, as the reference's varlen test (test_flash_attn.py:774-783)
+    refs = {x: torch.zeros(total, h if x in ("out", "dq") else hk, d, device=DEV) for x in ("out", "dq", "dk", "dv")}
+    pts = {x: torch.zeros_like(t) for x, t in refs.items()}
+    for i, n in enumerate(lens):
+        if n == 0:
+            continue
+        a, e = int(cu[i]), int(cu[i + 1])
+        rg = _ref_grads(*(x.detach()[a:e].unsqueeze(0) for x in (q, k, v)), g[a:e].unsqueeze(0), causal)
+        for key, dst in (("ref", refs), ("pt", pts)):
+            for name, t in zip(("out", "dq", "dk", "dv"), rg[key]):
+                dst[name][a:e] = t[0].float()
+    for name, got in (("out", out), ("dq", dq), ("dk", dk), ("dv", dv)):
+        _bound(name, got, refs[name], pts[name], c)
