@@ -88,6 +88,28 @@ __device__ inline void dropout_block_bytes(char* buf, uint64_t seed, uint64_t of
   asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
 }
 
+// The same bytes without LDS: this lane's 16 dropout bytes of the wave's 32 x 32 block (rows row0 ..
+// row0+31, columns col0 .. col0+31, multiples of 32) straight into the S^T accumulator order,
+// rb[u] = bytes of keys col0 + 8u + 4hh + (0..3) of query row0 + r (what dropout_group_bytes reads back).
+// Lane (r, hh) needs, of 16-row block r / 16, the calls of lanes 4 (r % 8) + 2hh (keys 4hh + 8u + 0, 1)
+// and 4 (r % 8) + 2hh + 1 (keys + 2, 3); each of those calls also holds the same keys of row r ^ 8
+// (bytes 0-1 of each word: row r % 8, bytes 2-3: row r % 8 + 8).  So the lanes r and r ^ 8 split the
+// pair: the one with r & 8 == 0 runs the first call, its partner the second, and they swap words
+// across the 16-lane DPP row (row_ror:8 = lane ^ 8).  One call per lane, as in dropout_block_bytes.
+__device__ inline void dropout_lane_bytes(unsigned (&rb)[4], uint64_t seed, uint64_t off_bh, int row0,
+                                          int col0, int lane) {
+  const int r = lane & 31, hh = lane >> 5, up = (r >> 3) & 1;
+  const uint64_t sub = (uint64_t)(unsigned)(row0 / 16 + (r >> 4)) | ((uint64_t)(unsigned)(col0 / 32) << 32);
+  const u32x4_t w = philox(seed, sub, off_bh + (uint64_t)(4 * (r & 7) + 2 * hh + up));
+  // v_perm_b32 selectors over {own word: bytes 4-7, partner word: bytes 0-3}
+  const unsigned sel = up ? 0x07060302u : 0x01000504u;
+#pragma unroll
+  for (int u = 0; u < 4; ++u) {
+    const unsigned partner = (unsigned)__builtin_amdgcn_mov_dpp((int)w[u], 0x128, 0xf, 0xf, false);
+    rb[u] = __builtin_amdgcn_perm(w[u], partner, sel);
+  }
+}
+
 // The 4 bytes of accumulator group u (elements 4u .. 4u+3) of a 32x32 MFMA tile whose lane column
 // is `r` and whose row index of element g is (g & 3) + 8 (g >> 2) + 4 hh: bytes of [r][8u + 4hh ..].
 __device__ inline unsigned dropout_group_bytes(const char* buf, int r, int hh, int u) {

@@ -74,15 +74,13 @@ __global__ void __launch_bounds__(FwdTile<D>::NW * 64, FwdTile<D>::MINB) fwd_ker
   // every SIMD one wave opens its step with the softmax VALU while its partner opens with PV MFMAs
   // (MI355X_MICROARCH.md "Two waves per SIMD", item 9).  The late PV reads V(nb-1) while the DMA of
   // V(nb+3) is in flight, hence a 5-deep V ring next to the 4-deep K ring.
-  // (With dropout at d <= 64 the 5th V slot and the NW * NT KiB of random-byte scratch make the
-  // workgroup 88 KiB, one per CU.  Unstaggered with a 4-deep V ring it is 80 KiB, two per CU, but
-  // measured 7 % slower (d64 causal dropout forward, tools/ab.py: 2.205 vs 2.060 ms): kept staggered.)
+  // (Round 4, when dropout still staged its random bytes in LDS: unstaggered with a 4-deep V ring
+  // measured 7 % slower at d = 64 with dropout, tools/ab.py 2.205 vs 2.060 ms: kept staggered.)
   constexpr bool STAGGER = NW == 8;
   constexpr int VBUFS = STAGGER ? 5 : 4;
   constexpr int VBASE = kFwdBufs * TILE;
   constexpr int SCRATCH = VBASE + VBUFS * TILE;
-  constexpr int LDS_BYTES = SCRATCH + (DROPOUT ? NW * NT * 1024 : 0);
-  // [K ring][V ring], then (dropout) NT 1-KiB random-byte scratch blocks per wave
+  constexpr int LDS_BYTES = SCRATCH;   // [K ring][V ring]
   __shared__ __attribute__((aligned(16))) char smem[LDS_BYTES];
   auto kslot = [&](int nb) { return (nb % kFwdBufs) * TILE; };
   auto vslot = [&](int nb) { return VBASE + (nb % VBUFS) * TILE; };
@@ -278,29 +276,24 @@ __global__ void __launch_bounds__(FwdTile<D>::NW * 64, FwdTile<D>::MINB) fwd_ker
   // P = exp2(S c - m c) -> packed B operands; adds the partial row sum of this lane to l_run (the
   // sum is over the undropped P, as in the reference); with dropout the dropped elements of the
   // packed P are zero (reference flash_fwd_kernel.h:429-432; O is scaled by 1/keep_prob at the end)
-  char* const dscr = smem + SCRATCH + wave * NT * 1024;
   const uint64_t doff = s.philox_offset + (uint64_t)(bidb * s.h + head) * 32;
-  // dropout bytes of the tile at key n0 into the wave's scratch, generated ahead of the tile's
-  // softmax while no score tile of it is live (generated inside the softmax, the Philox temporaries
-  // made the d = 128 dropout instantiations spill ~70 registers); the refit path reuses them
-  auto gen_bytes = [&](int n0) {
+  // dropout bytes of the tile at key n0, in registers (dropout_lane_bytes: one Philox call per lane
+  // and 32-key subtile, the bytes of the lane's own scores swapped in from lane ^ 8 by DPP; no LDS
+  // scratch and no LDS drain per tile); the refit path reuses them
+  typedef unsigned DropBytes[NT][4];
+  auto gen_bytes = [&](DropBytes& db, int n0) {
     if constexpr (DROPOUT) {
 #pragma unroll
-      for (int t = 0; t < NT; ++t) dropout_block_bytes<false>(dscr + t * 1024, s.philox_seed, doff, wq0, n0 + 32 * t, lane);
-      __builtin_amdgcn_sched_barrier(0);
+      for (int t = 0; t < NT; ++t) dropout_lane_bytes(db[t], s.philox_seed, doff, wq0, n0 + 32 * t, lane);
     }
-    (void)n0;
+    (void)db; (void)n0;
   };
-  auto softmax_pack = [&](f32x16_t (&st)[NT], i16x8_t (&pf)[2 * NT], int n0) {
+  auto softmax_pack = [&](f32x16_t (&st)[NT], i16x8_t (&pf)[2 * NT], const DropBytes& db) {
     const float ms = (m_run == kNegInf) ? 0.f : m_run * c;
     float ls[4] = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
     for (int t = 0; t < NT; ++t) {
-      unsigned rb[4];
-      if constexpr (DROPOUT) {
-#pragma unroll
-        for (int u = 0; u < 4; ++u) rb[u] = dropout_group_bytes(dscr + t * 1024, r, hh, u);
-      }
+      const unsigned* rb = db[t];
 #pragma unroll
       for (int g = 0; g < 16; ++g) {
         const float pv = fast_exp2(fmaf(st[t][g], c, -ms));
@@ -316,16 +309,12 @@ __global__ void __launch_bounds__(FwdTile<D>::NW * 64, FwdTile<D>::MINB) fwd_ker
   // Fast-path softmax, no max pass: P = exp2(S c - m_run c) against the running max of earlier
   // tiles (finite here).  Returns this lane's partial row sum; the caller adds it to l_run only after
   // the overflow check (guard_ok), so a tile that trips the check is simply recomputed.
-  auto softmax_fast = [&](const f32x16_t (&st)[NT], i16x8_t (&pf)[2 * NT], int n0) {
+  auto softmax_fast = [&](const f32x16_t (&st)[NT], i16x8_t (&pf)[2 * NT], const DropBytes& db) {
     const float ms = m_run * c;
     float ls[4];
 #pragma unroll
     for (int t = 0; t < NT; ++t) {
-      unsigned rb[4];
-      if constexpr (DROPOUT) {
-#pragma unroll
-        for (int u = 0; u < 4; ++u) rb[u] = dropout_group_bytes(dscr + t * 1024, r, hh, u);
-      }
+      const unsigned* rb = db[t];
       f32x16_t pt;
 #pragma unroll
       for (int g = 0; g < 16; ++g) {
@@ -345,7 +334,7 @@ __global__ void __launch_bounds__(FwdTile<D>::NW * 64, FwdTile<D>::MINB) fwd_ker
   // Slow path (wave-uniform, rare): recompute S of tile nb (still resident in the K ring), move the
   // running max to the true max, rescale O / l_run, and redo P.  NaN sums (NaN inputs) also land
   // here and end as the reference's NaN / +inf LSE through the normal epilogue.
-  auto refit = [&](int nb, i16x8_t (&pf)[2 * NT]) {
+  auto refit = [&](int nb, i16x8_t (&pf)[2 * NT], const DropBytes& db) {
     asm volatile("; refit" ::: "memory");   // not speculated into the fast path (if-conversion)
     f32x16_t st[NT];
     qk(kslot(nb), st);
@@ -363,7 +352,7 @@ __global__ void __launch_bounds__(FwdTile<D>::NW * 64, FwdTile<D>::MINB) fwd_ker
 #pragma unroll
       for (int g = 0; g < 16; ++g) o[t][g] *= alpha;
     m_run = m_new;
-    return softmax_fast(st, pf, nb * BN);
+    return softmax_fast(st, pf, db);
   };
   // O^T[d][q] += V^T[d][key] P^T[key][q], one 32-wide d tile at a time
   auto pv = [&](int vt_off, const i16x8_t (&pf)[2 * NT]) {
@@ -397,12 +386,13 @@ __global__ void __launch_bounds__(FwdTile<D>::NW * 64, FwdTile<D>::MINB) fwd_ker
     auto body = [&](int nb, f32x16_t (&scur)[NT], f32x16_t (&snxt)[NT]) {
       if (nb + 3 < nblk) issue(nb + 3);
       i16x8_t pf[2 * NT];
-      gen_bytes(nb * BN);
-      float ls = softmax_fast(scur, pf, nb * BN);
+      DropBytes db;
+      gen_bytes(db, nb * BN);
+      float ls = softmax_fast(scur, pf, db);
       // tile nb+1 is resident (possibly past nblk: then its scores are simply discarded); its
       // MFMAs are independent of the softmax above, so the two interleave in this basic block
       qk(kslot(nb + 1), snxt);
-      if (!guard_ok(ls)) ls = refit(nb, pf);
+      if (!guard_ok(ls)) ls = refit(nb, pf, db);
       l_run += ls;
       __builtin_amdgcn_sched_barrier(0);   // bound the V-read hoisting (register pressure)
       pv(vslot(nb), pf);
@@ -416,10 +406,11 @@ __global__ void __launch_bounds__(FwdTile<D>::NW * 64, FwdTile<D>::MINB) fwd_ker
       if (nb + 3 < nblk) issue(nb + 3);
       if (nb > 0) pv(vslot(nb - 1), pfp);
       __builtin_amdgcn_sched_barrier(0);
-      gen_bytes(nb * BN);
-      float ls = softmax_fast(scur, pfp, nb * BN);
+      DropBytes db;
+      gen_bytes(db, nb * BN);
+      float ls = softmax_fast(scur, pfp, db);
       qk(kslot(nb + 1), snxt);
-      if (!guard_ok(ls)) ls = refit(nb, pfp);
+      if (!guard_ok(ls)) ls = refit(nb, pfp, db);
       l_run += ls;
       tile_sync(nb + 3 < nblk);
     };
@@ -450,7 +441,8 @@ __global__ void __launch_bounds__(FwdTile<D>::NW * 64, FwdTile<D>::MINB) fwd_ker
     if (a3 < nblk) issue_at(a3, pos + 3);
     const bool active = (wq0 < sq) && (!CAUSAL || n0 <= wq0 + 31);
     if (active) {
-      gen_bytes(n0);
+      DropBytes db;
+      gen_bytes(db, n0);
       f32x16_t st[NT];
       qk(kslot(pos), st);
 #pragma unroll
@@ -474,7 +466,7 @@ __global__ void __launch_bounds__(FwdTile<D>::NW * 64, FwdTile<D>::MINB) fwd_ker
       }
       rescale(rowmax(st));
       i16x8_t pf[2 * NT];
-      softmax_pack(st, pf, n0);
+      softmax_pack(st, pf, db);
       pv(vslot(pos), pf);
     }
     tile_sync(a3 < nblk);
