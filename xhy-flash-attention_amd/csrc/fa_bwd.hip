@@ -927,12 +927,19 @@ __global__ void __launch_bounds__(DqTile<D>::NW * 64, DqTile<D>::MINB) bwd_dq_ke
     const TileAddr tk(lb, kt), tv(lb, kt + TILE);
     // dropout bytes of the tile's NT 32x32 blocks, generated before the S / dP chains (the Philox
     // temporaries then never overlap the live score tiles: generated inside the dS loop they made
-    // the causal dropout instantiation spill ~140 registers)
-    char* const dscr = smem + BUFS * 2 * TILE + wave * NT * 1024;
+    // the causal dropout instantiation spill ~140 registers).  dropout_lane_bytes hands each lane
+    // its own 16 bytes (no cross-lane scatter); they wait in the lane's own 16-byte LDS slot, since
+    // held in registers across the chains they spill (114-145 VGPRs).  Each slot is read back, and
+    // the value used, before the next tile overwrites it.
+    u32x4_t* const dslot = (u32x4_t*)(smem + BUFS * 2 * TILE + wave * NT * 1024) + lane;
     if constexpr (DROPOUT) {
       const uint64_t doff = poff + (uint64_t)bhi * 32;
 #pragma unroll
-      for (int t = 0; t < NT; ++t) dropout_block_bytes<false>(dscr + t * 1024, pseed, doff, wq0, n0 + 32 * t, lane);
+      for (int t = 0; t < NT; ++t) {
+        unsigned w[4];
+        dropout_lane_bytes(w, pseed, doff, wq0, n0 + 32 * t, lane);
+        dslot[64 * t] = u32x4_t{w[0], w[1], w[2], w[3]};
+      }
     }
     f32x16_t st[NT], pt[NT];
     static_for<0, NT>([&](auto T) {
@@ -956,11 +963,8 @@ __global__ void __launch_bounds__(DqTile<D>::NW * 64, DqTile<D>::MINB) bwd_dq_ke
     });
 #pragma unroll
     for (int t = 0; t < NT; ++t) {
-      unsigned rb[4];
-      if constexpr (DROPOUT) {
-#pragma unroll
-        for (int u = 0; u < 4; ++u) rb[u] = dropout_group_bytes(dscr + t * 1024, r, hh, u);
-      }
+      u32x4_t rb = {0u, 0u, 0u, 0u};
+      if constexpr (DROPOUT) rb = dslot[64 * t];
 #pragma unroll
       for (int g = 0; g < 16; ++g) {
         float pv;
