@@ -491,9 +491,8 @@ __global__ void __launch_bounds__(DkdvTile<D>::NW * 64, 1) bwd_dkdv_kernel(const
       unsigned rb[4];
       if constexpr (DROPOUT) {
         const uint64_t doff = poff + (uint64_t)(bidb * s.h + h_begin + it_head) * 32;
-        dropout_block_bytes<true>(dscr, pseed, doff, q0 + 32 * qi, kw0, lane);
-#pragma unroll
-        for (int u = 0; u < 4; ++u) rb[u] = dropout_group_bytes(dscr, r, hh, u);
+        dropout_block_words(dscr, pseed, doff, q0 + 32 * qi, kw0, lane);
+        dropout_col_bytes(rb, dscr, lane);
       }
 #pragma unroll
       for (int u = 0; u < 4; ++u) {

@@ -110,6 +110,39 @@ __device__ inline void dropout_lane_bytes(unsigned (&rb)[4], uint64_t seed, uint
   }
 }
 
+// The transposed consumer (dK/dV: lane = key c, rows 8u + 4hh + j) needs two bytes of each of eight
+// calls, so the bytes still cross lanes through the wave's 1-KiB scratch, but word-wise: the lane of
+// call (row block R = lane / 32, L = lane % 32 = 4g + t) stores its word w (columns 8w + 2t, +1;
+// bytes: row g even / odd column, row g + 8 even / odd) at word ((4R + w) 4 + t) 8 + g -- four
+// conflict-free ds_write_b32 instead of sixteen byte stores -- and the consumer of column c reads the
+// words of g = 4hh .. 4hh + 3 of its (R, c / 8, c % 8 / 2) as one ds_read_b128 per row block, then
+// picks its bytes with v_perm.  Same drains as dropout_block_bytes (the scratch is reused per block).
+__device__ inline void dropout_block_words(char* buf, uint64_t seed, uint64_t off_bh, int row0, int col0,
+                                           int lane) {
+  const int R = lane >> 5, L = lane & 31, g = L >> 2, t = L & 3;
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  const uint64_t sub = (uint64_t)(unsigned)(row0 / 16 + R) | ((uint64_t)(unsigned)(col0 / 32) << 32);
+  const u32x4_t w = philox(seed, sub, off_bh + (uint64_t)L);
+#pragma unroll
+  for (int i = 0; i < 4; ++i) *(u32_alias*)(buf + 4 * (((4 * R + i) * 4 + t) * 8 + g)) = w[i];
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+}
+
+// rb[u] byte j = the byte of (row 8u + 4hh + j, column c = lane % 32) from dropout_block_words
+__device__ inline void dropout_col_bytes(unsigned (&rb)[4], const char* buf, int lane) {
+  const int c = lane & 31, hh = lane >> 5;
+  // bytes (c & 1) and 2 + (c & 1) of words j = 0, 1 (resp. 2, 3) side by side
+  const unsigned sel_pair = (c & 1) ? 0x07030501u : 0x06020400u;
+#pragma unroll
+  for (int R = 0; R < 2; ++R) {
+    const u32x4_t v = *(const u32x4_t*)(buf + 4 * (((4 * R + (c >> 3)) * 4 + ((c & 7) >> 1)) * 8 + 4 * hh));
+    const unsigned t01 = __builtin_amdgcn_perm(v[1], v[0], sel_pair);
+    const unsigned t23 = __builtin_amdgcn_perm(v[3], v[2], sel_pair);
+    rb[2 * R] = __builtin_amdgcn_perm(t23, t01, 0x05040100u);
+    rb[2 * R + 1] = __builtin_amdgcn_perm(t23, t01, 0x07060302u);
+  }
+}
+
 // The 4 bytes of accumulator group u (elements 4u .. 4u+3) of a 32x32 MFMA tile whose lane column
 // is `r` and whose row index of element g is (g & 3) + 8 (g >> 2) + 4 hh: bytes of [r][8u + 4hh ..].
 __device__ inline unsigned dropout_group_bytes(const char* buf, int r, int hh, int u) {
