@@ -91,6 +91,8 @@ def parse(argv=None):
                     help="untimed seconds of headline steps before either leg (clock / allocator ramp)")
     ap.add_argument("--workload", default="c3", choices=sorted(WORKLOADS))
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--dropout", type=float, default=0.0,
+                    help="dropout_p of every call (dev lines: the dropout training path; 0 = the BASELINE configs)")
     ap.add_argument("--cpu-threads", type=int, default=0,
                     help="CPU-baseline threads (0: the affinity set, capped by OMP_NUM_THREADS)")
     ap.add_argument("--pmc", default=os.path.join(ROOT, "profiles", "pmc.json"),
@@ -323,7 +325,7 @@ def load_pmc(path, workload, lib=None):
 # ------------------------------------------------------------------------------------------------
 # workloads
 # ------------------------------------------------------------------------------------------------
-def make_workload(name, dev, rank):
+def make_workload(name, dev, rank, dropout_p=0.0):
     """-> (fwd_only, fwd_bwd, f_fwd, config dict, dtype name, sdpa sample for the CPU baseline)."""
     import torch
 
@@ -341,16 +343,18 @@ def make_workload(name, dev, rank):
 
         def fwd_only():
             with torch.no_grad():
-                flash_attn_varlen_qkvpacked_func(qkv, cu, max_s, causal=causal)
+                flash_attn_varlen_qkvpacked_func(qkv, cu, max_s, dropout_p, causal=causal)
 
         def fwd_bwd():
-            out = flash_attn_varlen_qkvpacked_func(qkv, cu, max_s, causal=causal)
+            out = flash_attn_varlen_qkvpacked_func(qkv, cu, max_s, dropout_p, causal=causal)
             torch.autograd.grad(out, (qkv,), dout)
 
         f_fwd = varlen_flops_fwd(lens, h, d, causal)
         cfg = {"workload": "flash_attn_varlen_qkvpacked_func fwd+bwd (c4)", "total_tokens": s,
                "batch": len(lens), "max_seqlen": max_s, "seqlens": "U{512..4096}, seed 0 (SURVEY 8(d))",
                "nheads": h, "headdim": d, "causal": causal}
+        if dropout_p > 0:
+            cfg["dropout_p"] = dropout_p
         sample = ("varlen", lens[:2], h, d)
         return fwd_only, fwd_bwd, f_fwd, cfg, dt_name, sample
     q = torch.randn(b, s, h, d, device=dev, dtype=dtype, generator=g).requires_grad_()
@@ -360,16 +364,18 @@ def make_workload(name, dev, rank):
 
     def fwd_only():
         with torch.no_grad():
-            flash_attn_func(q, k, v, causal=causal)
+            flash_attn_func(q, k, v, dropout_p, causal=causal)
 
     def fwd_bwd():
-        out = flash_attn_func(q, k, v, causal=causal)
+        out = flash_attn_func(q, k, v, dropout_p, causal=causal)
         torch.autograd.grad(out, (q, k, v), dout)
 
     f_fwd = flops_fwd(b, s, h, d, causal)
     label = "forward only" if kind == "fwd" else "fwd+bwd"
     cfg = {"workload": f"flash_attn_func {label} ({name})", "batch_per_gpu": b, "seq_len": s,
            "nheads": h, "nheads_k": hk, "headdim": d, "causal": causal}
+    if dropout_p > 0:
+        cfg["dropout_p"] = dropout_p
     # CPU sample: one batch element; the 32k context is cut to 8k keys/queries (bounded time)
     sample = ("dense", 1, min(s, 8192), h, d)
     return fwd_only, fwd_bwd, f_fwd, cfg, dt_name, sample
@@ -425,7 +431,7 @@ def main():
         return
 
     dev = torch.device("cuda", local)
-    fwd_only, fwd_bwd, f_fwd, cfg, dt_name, sample = make_workload(args.workload, dev, rank)
+    fwd_only, fwd_bwd, f_fwd, cfg, dt_name, sample = make_workload(args.workload, dev, rank, args.dropout)
     kind = WORKLOADS[args.workload][7]
     causal = WORKLOADS[args.workload][6]
     f_step = f_fwd if kind == "fwd" else 3.5 * f_fwd
@@ -488,7 +494,7 @@ def main():
                     "alg_flops_per_launch": alg, "avg_launch_ms": round(kt[dom]["avg_ms"], 4)}
 
     cpu = None
-    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+    if rank == 0 and world == 1 and not args.no_cpu_baseline and args.dropout == 0:
         from oracle.cpu_baseline import cpu_model_name
         threads = cpu_threads(args.cpu_threads)
         dtype = torch.bfloat16 if dt_name == "bf16" else torch.float16
@@ -508,6 +514,9 @@ def main():
             "steps": args.steps,
             "warmup": args.warmup,
             "ms_per_step": round(ms_per_step, 4),
+            "value_estimator": ("wall clock of the forward-only leg: K back-to-back steps without per-step events, "
+                                "between barrier + synchronize" if kind == "fwd" else
+                                "wall clock of K steps between barrier + synchronize (events between steps)"),
             "ms_per_step_median": round(statistics.median(step_ms), 4) if step_ms else None,
             "ms_per_step_min": round(min(step_ms), 4) if step_ms else None,
             "higher_is_better": True,

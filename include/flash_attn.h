@@ -50,7 +50,10 @@
  *     with num_heads heads ("expanded", reference flash_api.cpp:628-635) and
  *     sums the groups itself;
  *   - num_splits is accepted and ignored: the MI355X backward uses no atomics,
- *     so dQ, dK and dV are bitwise deterministic for every value.
+ *     so dQ, dK and dV are bitwise deterministic for every value;
+ *   - return_softmax is honoured with or without dropout (reference
+ *     flash_attn.cu:641, 747); the probabilities come from the scores O and LSE
+ *     were computed from.
  *
  * MI355X extensions (no reference counterpart):
  *   flash_attn_bwd_gqa / flash_attn_varlen_bwd_gqa take the same arguments as
@@ -435,7 +438,11 @@ void flash_attn_timing_read(int kernel_id, double * total_ms, long * count);
 void flash_attn_set_knob(int id, int value);
 int flash_attn_get_knob(int id);
 /* 0 routes every forward to the HIP kernel, 1 (default) lets head dim 128 and 64 take the assembly
- * kernel (FLASH_ATTN_MI355X_FWD_ASM=0 sets 0). */
+ * kernel (FLASH_ATTN_MI355X_FWD_ASM=0 sets 0).  Neither this nor any knob changes a call's
+ * numerics contract: whether a call scores from Q' = bf16/f16(scale log2(e) Q) (head dim 64 / 128,
+ * no dropout; fp16 only with |scale log2(e)| <= 1) is decided by the call alone, the HIP forward
+ * scores from a materialised Q' then, and a backward may run under other settings than its
+ * forward. */
 void flash_attn_fwd_use_asm(int on);
 /* Backward dQ / dK-dV stream overlap: 0 (default) serial on the caller's stream, 1 dQ on a second
  * stream, 2 dQ on a lowest-priority stream, 3 dK/dV on a highest-priority stream

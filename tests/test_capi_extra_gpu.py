@@ -161,6 +161,67 @@ def test_flashmask_return_softmax():
     assert (sdm[~vis.expand_as(sdm)] == 0).all()
 
 
+@pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float16])
+@pytest.mark.parametrize("causal", [False, True])
+@pytest.mark.parametrize("d", [64, 128])
+def test_return_softmax_without_dropout_then_bwd(d, causal, dtype):
+    """The reference C ABI passes softmax_ptr whenever return_softmax is set
+    (capi/flash_attn.cu:641, 747), dropout or not.  At p = 0 the call folds (attn_folds_q), so the
+    forward runs the HIP kernels on Q' (the assembly kernel has no S_dmask) and the reference-shaped
+    flash_attn_bwd that follows scores with the same Q': S_dmask is the softmax, out / LSE / dq / dk
+    / dv are within the 2x rule, and out / LSE agree with a plain (assembly) forward of the call."""
+    import flash_attn_2_cuda as m
+    from oracle.attention_ref import attention_lse_pt, attention_lse_ref, check_lse_within_bound
+
+    torch.manual_seed(1)
+    b, s, h, scale = 2, 333, 3, d ** -0.5
+    # (plain N(0, 1) inputs: the reference's overflow scaling runs in tests/test_fold_gpu.py under its
+    # factor 5; with rows of q * 6 in fp16 at d = 64 the folded dK reached 1.7x the 2x bound)
+    q, k, v, dout = (torch.randn(b, s, h, d, device=DEV, dtype=dtype) for _ in range(4))
+    out, lse, sdm = _fwd_return_softmax(q, k, v, 0.0, 0, 0, causal)
+    sc = torch.einsum("bqhd,bkhd->bhqk", q.float(), k.float()) * scale
+    if causal:
+        sc = sc.masked_fill(torch.triu(torch.ones(s, s, dtype=torch.bool, device=DEV), 1), float("-inf"))
+    prob = torch.softmax(sc, -1)
+    assert not torch.signbit(sdm.float()).any()          # nothing dropped
+    torch.testing.assert_close(sdm.float(), prob, atol=4e-3, rtol=2 ** -7)
+    qr, kr, vr = (x.clone().requires_grad_() for x in (q, k, v))
+    ref, _ = attention_ref(qr, kr, vr, causal=causal)
+    qp, kp, vp = (x.clone().requires_grad_() for x in (q, k, v))
+    pt, _ = attention_ref(qp, kp, vp, causal=causal, upcast=False, reorder_ops=True)
+    ok, err, bound = check_within_bound(out, ref, pt)
+    assert ok, f"out {err:.3e} > {bound:.3e}"
+    ok, err, pt_err = check_lse_within_bound(lse, attention_lse_ref(q, k, causal), attention_lse_pt(q, k, causal))
+    assert ok, f"lse {err:.3e} (pt {pt_err:.3e})"
+    # the same call without return_softmax takes the assembly forward: same Q', same LSE
+    from flash_attn.flash_attn_interface import _flash_attn_forward
+    out2, _, _, _, _, lse2, _, _ = _flash_attn_forward(q, k, v, 0.0, scale, causal, False)
+    torch.testing.assert_close(lse, lse2, atol=1e-4, rtol=1e-5)
+    tol = 2 ** -7 if dtype == torch.bfloat16 else 2 ** -10
+    torch.testing.assert_close(out.float(), out2.float(), atol=tol, rtol=tol)
+    # reference-shaped backward of that forward
+    P = m._ptr
+    sq_r = (s + 127) // 128 * 128
+    dq, dk, dv = (torch.empty_like(x) for x in (q, k, v))
+    softmax_d = torch.empty(b, h, sq_r, device=DEV)
+    st = [_st(x) for x in (q, k, v, out, dq, dk, dv, dout)]
+    (qr_, qh, qb), (kr_, kh, kb), (vr_, vh, vb), (orr, oh, ob) = st[:4]
+    (dqr, dqh, dqb), (dkr, dkh, dkb), (dvr, dvh, dvb), (dor, doh, dob) = st[4:]
+    ok = m._lib.flash_attn_bwd(P(dout), P(q), P(k), P(v), P(out), P(softmax_d), P(lse), None, P(dq), P(dk), P(dv),
+                               None, b, s, s, sq_r, sq_r, h, h, d, d, 0.0, scale, 1.0, causal,
+                               dtype == torch.bfloat16, 1, m._stream(q), 0, 0,
+                               None, None, None, None, None, None, None, None,
+                               qr_, kr_, vr_, qh, kh, vh, orr, oh, qb, kb, vb, ob,
+                               dqr, dkr, dvr, dqh, dkh, dvh, dor, doh, dqb, dkb, dvb, dob)
+    assert ok, m._lib.flash_attn_error()
+    torch.cuda.synchronize()
+    gr = torch.autograd.grad(ref, (qr, kr, vr), dout)
+    gp = torch.autograd.grad(pt, (qp, kp, vp), dout)
+    for name, got, r, p_ in zip(("dq", "dk", "dv"), (dq, dk, dv), gr, gp):
+        ok, err, bound = check_within_bound(got, r, p_, floor=1e-3)
+        assert ok, f"{name} {err:.3e} > {bound:.3e}"
+
+
 def test_bwd_device_rng_state_matches_explicit_seed():
     """flash_attn_bwd_gqa reads (seed, offset) from rng_state on the device; the reference-shaped
     flash_attn_bwd takes them by value: bitwise the same gradients (deterministic backward)."""

@@ -11,9 +11,8 @@ import numpy as np
 import pytest
 import torch
 
-from knobs import hip_forward
-
-from oracle.attention_ref import check_within_bound
+from lse_record import lse_ratio, record
+from oracle.attention_ref import check_lse_within_bound, check_within_bound
 from oracle.flashmask_ref import document_lts, flashmask_keep
 
 pytestmark = pytest.mark.gpu
@@ -134,7 +133,16 @@ def test_flashmask_fwd_bwd(d, sq, h, hk, hm, mode, dtype):
     lse_ref = torch.logsumexp(s.masked_fill(~kp, float("-inf")), dim=-1)
     dead = ~kp.any(-1)
     assert torch.isinf(lse[dead]).all() and (lse[dead] > 0).all()
-    torch.testing.assert_close(lse[~dead], lse_ref[~dead], atol=2e-3, rtol=0)
+    # finite rows under the 2x rule against the PyTorch-precision LSE (scores in the input dtype, as
+    # oracle attention_lse_pt), never stricter than atol 2e-3: head dims 64 / 128 fold (Q', DESIGN.md
+    # deviation 8), masked calls included
+    s_pt = torch.einsum("bqhd,bkhd->bhqk", q, (k * scale).repeat_interleave(h // hk, dim=2)).float()
+    lse_pt = torch.logsumexp(s_pt.masked_fill(~kp, float("-inf")), dim=-1)
+    inf = torch.full_like(lse_ref, float("inf"))
+    lse_ref, lse_pt = torch.where(dead, inf, lse_ref), torch.where(dead, inf, lse_pt)
+    record("flashmask", (d, sq, h, hk, hm, mode, str(dtype)), *lse_ratio(lse, lse_ref, lse_pt, atol=2e-3))
+    ok, err, pt_err = check_lse_within_bound(lse, lse_ref, lse_pt, atol=2e-3, rtol=0.0)
+    assert ok, f"lse {err:.3e} (pt {pt_err:.3e})"
     if dead.any():
         assert (out.permute(0, 2, 1, 3)[dead] == 0).all()
     gr = torch.autograd.grad(ref, (qc, kc, vc), dout)
@@ -227,11 +235,11 @@ def test_flashmask_noop_bounds_equal_plain_attention(causal):
     bnd = dict(lts=lts) if causal else dict(lts=lts, ute=np.zeros((b, 1, s), np.int32))
     out, lse, dq, dk, dv = _capi(q, k, v, dout, d ** -0.5, causal, **bnd)
     qr, kr, vr = (x.clone().requires_grad_() for x in (q, k, v))
-    # (the HIP forward: the masked kernels' fp32 scores; the assembly forward holds Q as
-    # bf16(scale log2(e) Q), a rounding the masked path does not make)
-    with hip_forward():
-        o2 = flash_attn_func(qr, kr, vr, causal=causal)
-        g2 = torch.autograd.grad(o2, (qr, kr, vr), dout)
+    # the default path (assembly kernels): masked calls fold Q like unmasked ones (attn_folds_q), so
+    # the masked HIP kernels and the assembly kernels score from the same Q' (round 5 had to force
+    # the HIP forward here)
+    o2 = flash_attn_func(qr, kr, vr, causal=causal)
+    g2 = torch.autograd.grad(o2, (qr, kr, vr), dout)
     torch.testing.assert_close(out, o2, atol=2e-3, rtol=0)
     for a, bb in zip((dq, dk, dv), g2):
         torch.testing.assert_close(a, bb, atol=4e-3, rtol=0)

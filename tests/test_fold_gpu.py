@@ -1,0 +1,110 @@
+"""The Q fold belongs to the call, not to the kernel that ran it.
+
+A call with head dim 64 / 128, no dropout and no mask scores from Q' = bf16/f16(scale log2(e) Q)
+(attn_folds_q, fa_params.h): the assembly forward does, so the backward must recompute P from the
+same Q' or a row dominated by one key gets P != 1 against the forward's LSE.  Before round 6 the
+backward re-derived the forward's choice from the runtime switches; now the decision is a pure
+function of the call and a forward the assembly kernel does not take (the HIP kernels under
+``flash_attn_fwd_use_asm(0)``, split-KV, return_softmax) runs the HIP kernels on a materialised Q'.
+
+These tests run the forward under one setting and its backward under another -- every pairing of
+{assembly forward, HIP forward, no split-KV} with {default backward, HIP dK/dV + dQ, unfused
+preprocessing} -- on shapes where a rounding mismatch shows at once (one-key rows, the reference's
+overflow scaling ``q * 5, k * 3``, decode rows on the split-KV path), all under the reference's
+2x rule (``tests/test_flash_attn.py:835-878`` factor 5 for the scaled inputs)."""
+import contextlib
+
+import pytest
+import torch
+
+from knobs import BWD_ASM, DQ_ASM, FUSE_PRE, hip_forward, knob, no_splitkv
+from oracle.attention_ref import (attention_lse_pt, attention_lse_ref, attention_ref, check_lse_within_bound,
+                                  check_within_bound)
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda"
+
+
+@pytest.fixture(scope="module", autouse=True)
+def _need_gpu():
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    import flash_attn_2_cuda  # noqa: F401
+
+
+@contextlib.contextmanager
+def _hip_backward():
+    with knob(BWD_ASM, 0), knob(DQ_ASM, 0):
+        yield
+
+
+@contextlib.contextmanager
+def _unfused():
+    with knob(FUSE_PRE, 0):
+        yield
+
+
+FWD = {"asm": contextlib.nullcontext, "hip": hip_forward, "nosplit": no_splitkv}
+BWD = {"default": contextlib.nullcontext, "hip": _hip_backward, "unfused": _unfused}
+
+# (b, sq, sk, h, hk, d, causal, dtype, q_mul, kv_mul)
+SHAPES = [
+    (2, 1, 1, 5, 5, 64, False, torch.float16, 5.0, 3.0),      # one key per row: P must be exactly 1
+    (2, 17, 17, 5, 5, 64, True, torch.float16, 5.0, 3.0),     # the reference's overflow test shape
+    (2, 128, 128, 4, 2, 128, True, torch.bfloat16, 5.0, 3.0),
+    (2, 4, 2000, 4, 2, 128, False, torch.bfloat16, 1.0, 1.0),  # decode rows: the split-KV forward
+    (1, 300, 300, 4, 2, 128, True, torch.float16, 1.0, 1.0),
+]
+
+
+def _run(shape, fwd_ctx, bwd_ctx):
+    from flash_attn import flash_attn_func
+
+    b, sq, sk, h, hk, d, causal, dtype, qm, km = shape
+    torch.manual_seed(0)
+    q = (torch.randn(b, sq, h, d, device=DEV, dtype=dtype) * qm).requires_grad_()
+    k, v = [(torch.randn(b, sk, hk, d, device=DEV, dtype=dtype) * km).requires_grad_() for _ in range(2)]
+    g = torch.randn(b, sq, h, d, device=DEV, dtype=dtype)
+    with fwd_ctx():
+        out, lse, _ = flash_attn_func(q, k, v, causal=causal, return_attn_probs=True)
+    with bwd_ctx():
+        grads = torch.autograd.grad(out, (q, k, v), g)
+    return q, k, v, g, out, lse, grads
+
+
+@pytest.mark.parametrize("bwd", list(BWD))
+@pytest.mark.parametrize("fwd", list(FWD))
+@pytest.mark.parametrize("shape", SHAPES, ids=lambda s: "x".join(str(x) for x in s[:6]) + ("c" if s[6] else "")
+                         + str(s[7])[-4:])
+def test_forward_and_backward_under_different_switches(shape, fwd, bwd):
+    causal, scaled = shape[6], shape[8] != 1.0
+    q, k, v, g, out, lse, grads = _run(shape, FWD[fwd], BWD[bwd])
+    qr, kr, vr = (x.detach().clone().requires_grad_() for x in (q, k, v))
+    ref, _ = attention_ref(qr, kr, vr, causal=causal)
+    qp, kp, vp = (x.detach().clone().requires_grad_() for x in (q, k, v))
+    pt, _ = attention_ref(qp, kp, vp, causal=causal, upcast=False, reorder_ops=True)
+    factor = 5.0 if scaled else 2.0
+    ok, err, bound = check_within_bound(out, ref, pt, factor=factor)
+    assert ok, f"out {err:.3e} > {bound:.3e}"
+    ok, err, pt_err = check_lse_within_bound(lse, attention_lse_ref(q.detach(), k.detach(), causal),
+                                             attention_lse_pt(q.detach(), k.detach(), causal), factor=factor)
+    assert ok, f"lse {err:.3e} (pt {pt_err:.3e})"
+    gr = torch.autograd.grad(ref, (qr, kr, vr), g)
+    gp = torch.autograd.grad(pt, (qp, kp, vp), g)
+    for name, got, r, p in zip(("dq", "dk", "dv"), grads, gr, gp):
+        ok, err, bound = check_within_bound(got, r, p, factor=factor, floor=1e-3)
+        assert ok, f"{name} {err:.3e} > {bound:.3e}"
+
+
+@pytest.mark.parametrize("shape", SHAPES[:3], ids=["1key", "17c", "128c"])
+def test_fold_is_path_independent(shape):
+    """The HIP forward on Q' and the assembly forward score the same rounded Q: the same LSE to
+    fp32 summation order, and -- the backward being the same kernels -- gradients that agree to
+    within a few output ulps whichever forward produced O and LSE."""
+    _, _, _, _, out_a, lse_a, ga = _run(shape, FWD["asm"], BWD["default"])
+    _, _, _, _, out_h, lse_h, gh = _run(shape, FWD["hip"], BWD["default"])
+    live = torch.isfinite(lse_a)
+    assert torch.equal(live, torch.isfinite(lse_h))
+    torch.testing.assert_close(lse_a[live], lse_h[live], atol=1e-4, rtol=1e-5)
+    for x, y in zip((out_a,) + tuple(ga), (out_h,) + tuple(gh)):
+        torch.testing.assert_close(x.float(), y.float(), atol=2e-2 * max(1.0, float(y.abs().max())), rtol=2 ** -6)

@@ -7,7 +7,9 @@ import pytest
 import torch
 
 from knobs import hip_forward, no_splitkv
-from oracle.attention_ref import attention_ref, check_within_bound
+from lse_record import lse_ratio, record
+from oracle.attention_ref import (attention_lse_pt, attention_lse_ref, attention_ref, check_lse_within_bound,
+                                  check_within_bound)
 
 pytestmark = pytest.mark.gpu
 DEV = "cuda"
@@ -37,9 +39,11 @@ def test_splitkv_forward(sq, sk, h, hk, d, dtype):
     pt, _ = attention_ref(q, k, v, upcast=False, reorder_ops=True)
     ok, err, bound = check_within_bound(out, ref, pt)
     assert ok, (err, bound)
-    kr = k.float().repeat_interleave(h // hk, dim=2)
-    s = torch.einsum("bqhd,bkhd->bhqk", q.float(), kr) * d ** -0.5
-    torch.testing.assert_close(lse, torch.logsumexp(s, -1), atol=1e-3, rtol=0)
+    # LSE under the 2x rule against the PyTorch-precision LSE (d 64 / 128 fold: DESIGN.md deviation 8)
+    lse_ref, lse_pt = attention_lse_ref(q, k), attention_lse_pt(q, k)
+    record("splitkv", (sq, sk, h, hk, d, str(dtype)), *lse_ratio(lse, lse_ref, lse_pt))
+    ok, err, pt_err = check_lse_within_bound(lse, lse_ref, lse_pt)
+    assert ok, f"lse {err:.3e} (pt {pt_err:.3e})"
     with no_splitkv(), hip_forward():   # the unsplit HIP kernel: the split's own arithmetic
         out1, _, _, _, _, lse1, _, _ = _flash_attn_forward(q, k, v, 0.0, d ** -0.5, False, False)
     torch.testing.assert_close(lse, lse1, atol=2e-5, rtol=0)

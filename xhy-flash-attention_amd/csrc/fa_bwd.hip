@@ -227,39 +227,60 @@ __device__ unsigned long long g_fa_stamps[kStampWg * 8 * kStampIt * kStampPts];
 // MASKED (dense additive mask and/or FlashMask present): every slice takes the per-element path; the
 // unmasked instantiations carry no mask code (as in fwd_kernel).
 // ------------------------------------------------------------------------------------------------
-// Q' = bf16/f16(c Q) for the backward of a forward that scored with it (fwd_folds_q, launch_bwd):
-// the assembly forward rewrites its Q fragments as v_cvt_pk(v_mul_f32(q, c)) (gen_fwd.py
-// q_scale_ops) -- the same fp32 product and round-to-nearest-even pack here, so every score the
-// backward recomputes is bitwise the forward's.  HBM-bound elementwise pass, 16 bytes per thread
-// (rows and heads are 16-byte aligned: d % 8 == 0, bwd_pre_kernel's own assumption); output in the
-// compact layout (b or padded rows, seqlen_q, h, d), rows at the sequence offsets seq_geom uses.
+// Q' = bf16/f16(c Q) for a call that folds (attn_folds_q): the backward always, the forward when it
+// cannot take the assembly kernel.  The assembly forward rewrites its Q fragments as
+// v_cvt_pk(v_mul_f32(q, c)) (gen_fwd.py q_scale_ops) -- the same fp32 product and
+// round-to-nearest-even pack here, so every score a HIP kernel computes from Q' is bitwise the
+// assembly kernel's.  HBM-bound elementwise pass, 16 bytes per thread (rows and heads are 16-byte
+// aligned: d % 8 == 0, bwd_pre_kernel's own assumption); output in the compact layout (b or padded
+// rows, seqlen_q, h, d), rows at the sequence offsets seq_geom uses (QFoldArgs, fa_params.h).
 // ------------------------------------------------------------------------------------------------
 template <bool BF16>
-__global__ void __launch_bounds__(256) q_fold_kernel(const BwdParams p, u16* qf, float c) {
+__global__ void __launch_bounds__(256) q_fold_kernel(const QFoldArgs a) {
   using E = Elt<BF16>;
-  const AttnShape& s = p.s;
   const int bidb = blockIdx.y;
-  const SeqGeom g = seq_geom(p, bidb);
-  const int nch = s.d / 8;
+  int sq = a.seqlen_q;
+  int64_t q_off = (int64_t)bidb * a.q_batch;
+  const int64_t hd = (int64_t)a.h * a.d;
+  int64_t base = (int64_t)bidb * a.seqlen_q * hd;
+  if (a.cu_seqlens_q != nullptr) {   // (seq_geom's rule for the Q rows)
+    const int c0 = a.cu_seqlens_q[bidb];
+    sq = a.cu_seqlens_q[bidb + 1] - c0;
+    if (!a.padded) {
+      q_off = (int64_t)c0 * a.q_row;
+      base = (int64_t)c0 * hd;
+    }
+  }
+  const int nch = a.d / 8;
   const int64_t t = (int64_t)blockIdx.x * 256 + threadIdx.x;
   const int ch = (int)(t % nch);
   const int64_t rh = t / nch;
-  const int head = (int)(rh % s.h);
-  const int64_t row = rh / s.h;
-  if (row >= g.sq) return;
-  const u32x4_t x = *(const u32x4_t*)((const u16*)p.q + g.q_off + (int64_t)head * p.q_head + row * p.q_row + 8 * ch);
-  const int64_t hd = (int64_t)s.h * s.d;
-  const int64_t base = (s.cu_seqlens_q != nullptr && !s.varlen_padded_input)
-                           ? (int64_t)s.cu_seqlens_q[bidb] * hd
-                           : (int64_t)bidb * s.seqlen_q * hd;
+  const int head = (int)(rh % a.h);
+  const int64_t row = rh / a.h;
+  if (row >= sq) return;
+  const u32x4_t x = *(const u32x4_t*)((const u16*)a.q + q_off + (int64_t)head * a.q_head + row * a.q_row + 8 * ch);
   u32x4_t y;
 #pragma unroll
   for (int i = 0; i < 4; ++i) {
-    const float lo = E::to_f32((unsigned short)(x[i] & 0xffffu)) * c;
-    const float hi = E::to_f32((unsigned short)(x[i] >> 16)) * c;
+    const float lo = E::to_f32((unsigned short)(x[i] & 0xffffu)) * a.c;
+    const float hi = E::to_f32((unsigned short)(x[i] >> 16)) * a.c;
     y[i] = E::pack2(lo, hi);
   }
-  *(u32x4_t*)(qf + base + row * hd + (int64_t)head * s.d + 8 * ch) = y;
+  *(u32x4_t*)((u16*)a.qf + base + row * hd + (int64_t)head * a.d + 8 * ch) = y;
+}
+
+void launch_q_fold(const QFoldArgs& a, bool is_bf16, hipStream_t stream) {
+  const int64_t per_seq = (int64_t)a.seqlen_q * a.h * (a.d / 8);
+  if (a.b <= 0 || per_seq <= 0) return;
+  if (a.d % 8 != 0 || (per_seq + 255) / 256 > 0x7fffffff || a.b > 65535)
+    throw std::runtime_error("flash_attn: prescaled-Q grid too large");
+  const dim3 grid((unsigned)((per_seq + 255) / 256), (unsigned)a.b);
+  prof_begin(kTimeQFold, stream);
+  if (is_bf16)
+    hipLaunchKernelGGL((q_fold_kernel<true>), grid, dim3(256), 0, stream, a);
+  else
+    hipLaunchKernelGGL((q_fold_kernel<false>), grid, dim3(256), 0, stream, a);
+  prof_end(kTimeQFold, stream);
 }
 
 template <bool BF16, int D, bool CAUSAL, bool DROPOUT, bool MASKED>
@@ -932,6 +953,11 @@ __global__ void __launch_bounds__(DqTile<D>::NW * 64, DqTile<D>::MINB) bwd_dq_ke
     // the value used, before the next tile overwrites it.
     u32x4_t* const dslot = (u32x4_t*)(smem + BUFS * 2 * TILE + wave * NT * 1024) + lane;
     if constexpr (DROPOUT) {
+      // the previous tile's reads of the slots must have returned before the slots are rewritten: a
+      // wave's LDS store can overtake its own pending LDS load of the same address (fa_dropout.h),
+      // and nothing else orders them (the compiler may issue these stores before it waits on the
+      // previous tile's read)
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
       const uint64_t doff = poff + (uint64_t)bhi * 32;
 #pragma unroll
       for (int t = 0; t < NT; ++t) {
@@ -1239,34 +1265,30 @@ void launch_bwd(const BwdParams& p_in, bool is_bf16, hipStream_t stream) {
     p.dq_head_group = 0;
 #endif
   }
-  // The forward of this output scored with Q' = bf16/f16(c Q) (the assembly forward,
-  // fwd_folds_q): score the backward with the same Q' so that the recomputed P is the forward's --
-  // S' = Q' K^T is c S in the log2 domain (c -> 1), -LSE / scale -> -LSE log2(e) (scale -> ln 2),
-  // dK = ln2 dS^T Q', dQ = scale dS K (dq_scale).  Without this the backward's exact scores
-  // would disagree with the forward's LSE by the rounding of Q' (e.g. a one-key row's P != 1).
-  // Q' comes from the assembly dQ kernel when it runs first (fused preprocessing: it converts its
-  // own Q fragments and stores them for dK/dV), else from q_fold_kernel.
+  // A folding call (attn_folds_q -- a pure function of the call, so it is the forward's decision
+  // whatever knobs changed since): its forward scored with Q' = bf16/f16(c Q).  Score the backward
+  // with the same Q' so that the recomputed P is the forward's -- S' = Q' K^T is c S in the log2
+  // domain (c -> 1), -LSE / scale -> -LSE log2(e) (scale -> ln 2), dK = ln2 dS^T Q',
+  // dQ = scale dS K (dq_scale).  Without this the backward's exact scores would disagree with the
+  // forward's LSE by the rounding of Q' (e.g. a one-key row's P != 1).  Q' comes from the assembly
+  // dQ kernel when it runs first (fused preprocessing: it converts its own Q fragments and stores
+  // them for dK/dV), else from q_fold_kernel.
   p.dq_scale = p.s.scale;
   p.qfold = nullptr;
-  bool fold = false;
-  float fold_c = p.s.scale_log2;
-  {
-    FwdParams f;
-    std::memset(&f, 0, sizeof(f));
-    f.s = p.s;
-    f.q = p.q; f.k = p.k; f.v = p.v; f.o = const_cast<void*>(p.o);
-    f.q_batch = p.q_batch; f.q_row = p.q_row; f.q_head = p.q_head;
-    f.k_batch = p.k_batch; f.k_row = p.k_row; f.k_head = p.k_head;
-    f.v_batch = p.v_batch; f.v_row = p.v_row; f.v_head = p.v_head;
-    f.o_batch = p.o_batch; f.o_row = p.o_row; f.o_head = p.o_head;
-    int bm, bn;
-    fwd_block_size(p.s.d, &bm, &bn);
-    f.num_m_blocks = (p.s.seqlen_q + bm - 1) / bm;
-    fold = fwd_folds_q(f, is_bf16);
-  }
+  const bool fold = attn_folds_q(p.s, is_bf16);
+  const float fold_c = p.s.scale_log2;
   if (fold) {
+    p.s.mask_unscale *= fold_c;   // (dense mask: its term joins the log2-domain scores)
     p.s.scale = kLn2;
     p.s.scale_log2 = 1.0f;
+  }
+  // the strides the kernels see for Q' (compact, QFoldArgs): the assembly dK/dV kernel reads Q'
+  // there on both fold paths, so its 32-bit record limits are checked on these
+  BwdParams pq = p;
+  if (fold) {
+    pq.q_batch = (int64_t)p.s.seqlen_q * p.s.h * p.s.d;
+    pq.q_row = (int64_t)p.s.h * p.s.d;
+    pq.q_head = p.s.d;
   }
   // softmax_scale == 0 (uniform attention) would make -LSE / scale infinite: a tiny positive scale
   // gives the same P to fp32 precision (P deviates from uniform by 1e-30 |S|) and dQ, dK ~ 1e-30.
@@ -1276,7 +1298,7 @@ void launch_bwd(const BwdParams& p_in, bool is_bf16, hipStream_t stream) {
   // (2 x 32-row-rounded rows) always come from the allocator (the caller's buffer size is unknown)
   p.lsed = nullptr;
   p.lsed_ng = (p.s.seqlen_q + 31) / 32;
-  const bool asm_dkdv = bwd_asm_applicable(p);
+  const bool asm_dkdv = bwd_asm_applicable(pq);
   StreamScratch ws;
   p.lse_s = p.dq_accum;
   if (p.lse_s == nullptr || asm_dkdv) {
@@ -1292,8 +1314,9 @@ void launch_bwd(const BwdParams& p_in, bool is_bf16, hipStream_t stream) {
     }
   }
   // knob 8: the assembly dQ kernel computes D itself and writes softmax_d and the dK/dV scratch
+  // (with the fold the dQ kernel also stores Q' in the compact rows: their 256-row records must fit)
   p.fuse_pre = asm_dkdv && knob(kKnobFusePre) != 0 && p.s.d == 128 && !p.s.dropout && p.s.mask == nullptr &&
-               p.s.fm_lts == nullptr && dq_asm_applicable(p, true);
+               p.s.fm_lts == nullptr && dq_asm_applicable(p, true) && (!fold || dq_asm_applicable(pq, false));
   StreamScratch qfold;
   if (fold) {
     const int64_t hd = (int64_t)p.s.h * p.s.d;
@@ -1304,18 +1327,15 @@ void launch_bwd(const BwdParams& p_in, bool is_bf16, hipStream_t stream) {
       p.qfold = qfold.p;
       p.qfold_c = fold_c;
     } else {
-      const int64_t per_seq = (int64_t)p.s.seqlen_q * p.s.h * (p.s.d / 8);
-      if ((per_seq + 255) / 256 > 0x7fffffff || p.s.b > 65535)
-        throw std::runtime_error("flash_attn_bwd: prescaled-Q grid too large");
-      const dim3 grid((unsigned)((per_seq + 255) / 256), (unsigned)p.s.b);
-      prof_begin(kTimeQFold, stream);
-      if (is_bf16)
-        hipLaunchKernelGGL((q_fold_kernel<true>), grid, dim3(256), 0, stream, p, static_cast<u16*>(qfold.p), fold_c);
-      else
-        hipLaunchKernelGGL((q_fold_kernel<false>), grid, dim3(256), 0, stream, p, static_cast<u16*>(qfold.p), fold_c);
-      prof_end(kTimeQFold, stream);
+      QFoldArgs a;
+      a.q = p.q; a.qf = qfold.p;
+      a.q_batch = p.q_batch; a.q_row = p.q_row; a.q_head = p.q_head;
+      a.cu_seqlens_q = p.s.cu_seqlens_q; a.padded = p.s.varlen_padded_input;
+      a.b = p.s.b; a.seqlen_q = p.s.seqlen_q; a.h = p.s.h; a.d = p.s.d;
+      a.c = fold_c;
+      launch_q_fold(a, is_bf16, stream);
       p.q = qfold.p;
-      p.q_batch = (int64_t)p.s.seqlen_q * hd; p.q_row = hd; p.q_head = p.s.d;
+      p.q_batch = pq.q_batch; p.q_row = pq.q_row; p.q_head = pq.q_head;
     }
   }
   if (is_bf16) launch_bwd_t<true>(p, stream); else launch_bwd_t<false>(p, stream);

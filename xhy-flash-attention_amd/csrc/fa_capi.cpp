@@ -151,9 +151,10 @@ bool fwd_impl(const void* q, const void* k, const void* v, const int32_t* cu_q, 
               float unscale = 1.f) {
   FA_BEGIN
   check_common(b, h, hk, d, d_r, p_dropout, attn_mask, flashmask);
-  // reference mha_fwd: "return_softmax is only supported when p_dropout > 0.0" (flash_api.cpp:276-279)
-  if (return_softmax && !(p_dropout > 0.f))
-    throw std::runtime_error("return_softmax is only supported when p_dropout > 0.0");
+  // return_softmax is accepted with or without dropout, as the reference C ABI passes softmax_ptr
+  // whenever it is set (capi/flash_attn.cu:641, 747); the "p_dropout > 0" rule is the torch
+  // binding's (flash_api.cpp:276-279) and lives in flash_attn_2_cuda.py.  The probabilities come
+  // from the same scores as O and LSE (on a folding call: from Q', attn_folds_q).
   FA_CHECK(q && k && v && out && lse);
   fa::FwdParams p;
   std::memset(&p, 0, sizeof(p));

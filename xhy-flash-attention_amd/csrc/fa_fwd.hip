@@ -731,14 +731,16 @@ static void plan_split(FwdParams& p) {
   }
 }
 
-bool fwd_folds_q(const FwdParams& p_in, bool is_bf16) {
+// (fa_params.h: a pure function of the call.)  Head dim 64 / 128 without dropout -- the assembly
+// forward's domain, plus the dense mask and FlashMask, whose calls run the HIP kernels on Q' so that
+// a mask that hides nothing gives the unmasked call's result (the mask term enters the log2-domain
+// scores as mask * unscale * c); fp16 only with |c| <= 1, where c Q cannot overflow the 16-bit Q'.
+// Dropout calls (HIP kernels only) keep the exact Q: a fold would cost them a Q' pass for nothing.
+bool attn_folds_q(const AttnShape& s, bool is_bf16) {
 #ifdef FA_NO_QFOLD   // (A/B variants whose assembly forward is generated with FA_GEN_FOLD=0)
   return false;
 #endif
-  FwdParams p = p_in;
-  if (p.s.b <= 0 || p.s.h <= 0 || p.num_m_blocks <= 0 || p.s.dropout || (p.s.d != 128 && p.s.d != 64)) return false;
-  plan_split(p);
-  return fwd_asm_applicable(p, is_bf16);
+  return (s.d == 128 || s.d == 64) && !s.dropout && (is_bf16 || std::fabs(s.scale_log2) <= 1.0f);
 }
 
 void launch_fwd(const FwdParams& p_in, bool is_bf16, hipStream_t stream) {
@@ -752,7 +754,31 @@ void launch_fwd(const FwdParams& p_in, bool is_bf16, hipStream_t stream) {
   if (p.num_m_blocks <= 0) return;
   if ((int64_t)p.s.b * p.s.h * p.num_m_blocks > 0x7fffffff)
     throw std::runtime_error("flash_attn_fwd: batch * heads * query blocks too large for the grid");
-  StreamScratch ws;
+  StreamScratch ws, qf;
+  if (attn_folds_q(p.s, is_bf16)) {
+    FwdParams t = p;
+    plan_split(t);
+    if (!fwd_asm_applicable(t, is_bf16)) {
+      // A folding call the assembly kernel does not take (a knob, split-KV, return_softmax, record
+      // limits): the HIP kernels score from a materialised Q' with c = 1, scale = ln 2 -- the same
+      // scores, LSE and P (S_dmask included) the assembly forward and the backward use.
+      const int64_t hd = (int64_t)p.s.h * p.s.d;
+      if (!qf.alloc((size_t)p.s.b * p.s.seqlen_q * hd * 2, stream))
+        throw std::runtime_error("flash_attn_fwd: hipMallocAsync of the prescaled Q failed");
+      QFoldArgs a;
+      a.q = p.q; a.qf = qf.p;
+      a.q_batch = p.q_batch; a.q_row = p.q_row; a.q_head = p.q_head;
+      a.cu_seqlens_q = p.s.cu_seqlens_q; a.padded = p.s.varlen_padded_input;
+      a.b = p.s.b; a.seqlen_q = p.s.seqlen_q; a.h = p.s.h; a.d = p.s.d;
+      a.c = p.s.scale_log2;
+      launch_q_fold(a, is_bf16, stream);
+      p.q = qf.p;
+      p.q_batch = (int64_t)p.s.seqlen_q * hd; p.q_row = hd; p.q_head = p.s.d;
+      p.s.mask_unscale *= p.s.scale_log2;
+      p.s.scale = kLn2;
+      p.s.scale_log2 = 1.0f;
+    }
+  }
   plan_split(p);
   if (p.n_split > 0) {
     p.acc_d = (p.s.d + 31) / 32 * 32;

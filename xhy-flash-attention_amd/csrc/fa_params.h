@@ -110,8 +110,8 @@ struct BwdParams {
   float* lsed;
   int lsed_ng;
   bool fuse_pre;          // (knob 8) the assembly dQ kernel writes D, softmax_d and lsed; dQ before dK/dV
-  // dQ = dq_scale dS K.  launch_bwd sets it to the softmax scale, then -- when the forward of this
-  // output held Q as bf16/f16(c Q) (fwd_folds_q) -- scores the backward with that same rounded
+  // dQ = dq_scale dS K.  launch_bwd sets it to the softmax scale, then -- when the call folds
+  // (attn_folds_q: the forward held Q as bf16/f16(c Q)) -- scores the backward with that same rounded
   // Q' (q / q_* strides -> a prescaled copy), c -> 1 and scale -> ln 2 (dK = ln2 dS^T Q'), so the
   // recomputed P is the forward's P.
   float dq_scale;
@@ -149,15 +149,37 @@ struct RotaryParams {
   int64_t cs_row;
 };
 
+// Q' = bf16/f16(c Q) in the compact layout (b | padded rows, seqlen_q, h, d): rows at the sequence
+// offsets the kernels use (batch b at b seqlen_q h d; varlen at cu_seqlens_q[b] h d), so the
+// consumers address it with q_batch = seqlen_q h d, q_row = h d, q_head = d (fa_bwd.hip
+// q_fold_kernel; HBM-bound elementwise pass, 16 bytes per thread).
+struct QFoldArgs {
+  const void* q;
+  void* qf;
+  int64_t q_batch, q_row, q_head;   // elements
+  const int* cu_seqlens_q;
+  bool padded;                      // varlen_padded_input
+  int b, seqlen_q, h, d;
+  float c;
+};
+void launch_q_fold(const QFoldArgs& a, bool is_bf16, hipStream_t stream);
+
+// The Q fold.  A call "folds" when its scores are computed from Q' = bf16/f16(c Q), c = scale
+// log2(e), in the log2 domain (c -> 1, scale -> ln 2): the assembly forward holds Q that way
+// (gen_fwd.py FA_GEN_FOLD), and the backward must recompute P from the same Q' or a one-key row's
+// P would not be 1.  The decision is a PURE function of the call -- head dim, dtype, scale, dropout,
+// masks -- and never of a runtime knob, a stride or the kernel launch_fwd happens to pick: a forward
+// that folds but cannot take the assembly kernel (knobs, split-KV, return_softmax, 32-bit record
+// limits) runs the HIP kernels on a materialised Q' (launch_q_fold), so forward and backward agree
+// whatever switches are flipped between them.
+bool attn_folds_q(const AttnShape& s, bool is_bf16);                 // fa_fwd.hip
+
 // Host launchers (fa_fwd.hip / fa_bwd.hip).  Throw std::runtime_error on invalid configuration.
 void launch_fwd(const FwdParams& p, bool is_bf16, hipStream_t stream);
 // fa_fwd_asm.cpp: the assembly forward (d = 128 or 64, no dropout / mask / split-KV); false when it
 // does not apply
 bool launch_fwd_asm(const FwdParams& p, bool is_bf16, hipStream_t stream);
 bool fwd_asm_applicable(const FwdParams& p, bool is_bf16);           // fa_fwd_asm.cpp
-// true when launch_fwd runs this forward on the assembly kernel, which holds Q as bf16/f16(c Q),
-// c = scale log2(e) (gen_fwd.py FA_GEN_FOLD): its backward then scores with that rounded Q too
-bool fwd_folds_q(const FwdParams& p, bool is_bf16);                  // fa_fwd.hip
 void fwd_asm_enable(int on);
 void launch_bwd(const BwdParams& p, bool is_bf16, hipStream_t stream);
 void bwd_overlap_enable(int mode);                                  // fa_bwd.hip: dQ / dK-dV stream overlap mode (default 0: off)
