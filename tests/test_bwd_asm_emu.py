@@ -196,3 +196,38 @@ def test_generated_dq_kernels_assemble_shape():
         if x.startswith("buffer_load_dword") and x.endswith(" lds"):
             prev = lines[i - 1]
             assert not prev.startswith("s_add_u32 m0") and not prev.startswith("s_mov_b32 m0"), (i, prev)
+
+
+# ------------------------------------------------------------------------------------------------
+# the dK / dV kernel with two waves per SIMD (csrc/asm/gen_bwd2.py, knob 10): 8 waves by role, P
+# crossing from the P waves to the dS waves through LDS once per phase.  Same cases as above,
+# bitwise against the one-wave kernel, the waves run in both orders between barriers, and the
+# emulator's race checker on: no wave touches LDS bytes another wave writes (ds_write or in-flight
+# LDS-DMA) between the same two barriers.
+# ------------------------------------------------------------------------------------------------
+@pytest.fixture(scope="module")
+def asm2_text():
+    return emu_bwd.asm_text(2)
+
+
+@pytest.mark.timeout(900)
+@pytest.mark.parametrize("b,sq,sk,h,hk,causal,bf16,reduce,grid,order", [
+    (1, 64, 128, 1, 1, True, True, False, None, None),
+    (1, 200, 330, 2, 1, True, True, True, None, "reverse"),
+    (1, 257, 129, 1, 1, False, False, False, None, "reverse"),
+    (2, 160, 160, 2, 1, True, True, True, 3, None),      # persistent loop, several items per workgroup
+])
+def test_asm_dkdv_two_waves_in_emulator(asm_text, asm2_text, b, sq, sk, h, hk, causal, bf16, reduce, grid, order):
+    r1 = emu_bwd.run(b, sq, sk, h, hk, causal, bf16, reduce, seed=3, text=asm_text, verbose=False, grid=grid)
+    r2 = emu_bwd.run(b, sq, sk, h, hk, causal, bf16, reduce, seed=3, text=asm2_text, verbose=False, grid=grid,
+                     ver=2, order=order)
+    assert not emu_bwd.RACES, emu_bwd.RACES[:3]
+    assert (r1[2] == r2[2]).all() and (r1[4] == r2[4]).all()
+    assert max(r2[0], r2[1]) < 1e-2
+
+
+@pytest.mark.timeout(900)
+def test_asm_dkdv_two_waves_varlen_in_emulator(asm2_text):
+    ek, ev, *_ = emu_bwd.run(lens=[130, 0, 1, 257], h=2, hk=1, causal=True, text=asm2_text, verbose=False, ver=2)
+    assert not emu_bwd.RACES, emu_bwd.RACES[:3]
+    assert max(ek, ev) < 1e-2

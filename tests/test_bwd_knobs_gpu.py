@@ -112,3 +112,52 @@ def test_varlen_rounds_bitwise(causal, hk):
     for key, grads in res.items():
         for name, x, y in zip(("dq", "dk", "dv"), grads, base):
             assert torch.equal(x, y), (key, name, (x.float() - y.float()).abs().max().item())
+
+
+@pytest.mark.parametrize("case", [
+    dict(b=2, s=2048, h=16, hk=16, causal=True, dt=torch.bfloat16),        # persistent, several rounds
+    dict(b=1, s=1000, h=8, hk=2, causal=False, dt=torch.float16),          # GQA reduced, ragged
+    dict(b=3, s=77, h=4, hk=1, causal=True, dt=torch.bfloat16),            # one subtile pair, MQA
+    dict(b=1, s=4096 + 33, h=4, hk=4, causal=True, dt=torch.float16),      # long, ragged tail
+    dict(lens=[1, 300, 0, 1023, 64], h=8, hk=4, causal=True, dt=torch.bfloat16),   # varlen
+], ids=["c3class", "gqa_full", "mqa_short", "long_ragged", "varlen"])
+def test_two_waves_per_simd_bitwise(case):
+    """knob 10: the dK/dV kernel with two waves per SIMD (gen_bwd2.py: 8 waves specialised by role, P
+    crossing between them in LDS) against the one-wave kernel (gen_bwd.py): the same MFMA chains in
+    the same order, so dQ / dK / dV are bitwise equal; and under the 2x rule against the oracle."""
+    from flash_attn import flash_attn_func, flash_attn_varlen_func
+    from knobs import BWD_2W
+
+    torch.manual_seed(7)
+    dt, h, hk, causal = case["dt"], case["h"], case["hk"], case["causal"]
+    d = 128
+    if "lens" in case:
+        lens = case["lens"]
+        cu = torch.tensor([0] + lens, dtype=torch.int64).cumsum(0).to(torch.int32).to(DEV)
+        tot, mx = sum(lens), max(lens)
+        q = torch.randn(tot, h, d, device=DEV, dtype=dt, requires_grad=True)
+        k, v = (torch.randn(tot, hk, d, device=DEV, dtype=dt, requires_grad=True) for _ in range(2))
+        out = flash_attn_varlen_func(q, k, v, cu, cu, mx, mx, causal=causal)
+    else:
+        b, s = case["b"], case["s"]
+        q = torch.randn(b, s, h, d, device=DEV, dtype=dt, requires_grad=True)
+        k, v = (torch.randn(b, s, hk, d, device=DEV, dtype=dt, requires_grad=True) for _ in range(2))
+        out = flash_attn_func(q, k, v, causal=causal)
+    g = torch.randn_like(out)
+    res = []
+    for two in (0, 1):
+        with knob(BWD_2W, two):
+            res.append(torch.autograd.grad(out, (q, k, v), g, retain_graph=True))
+    for name, a, bb in zip(("dq", "dk", "dv"), *res):
+        assert torch.equal(a, bb), name
+    if "lens" in case:
+        return
+    qr, kr, vr = (x.detach().clone().requires_grad_() for x in (q, k, v))
+    ref, _ = attention_ref(qr, kr, vr, causal=causal)
+    gr = torch.autograd.grad(ref, (qr, kr, vr), g)
+    qp, kp, vp = (x.detach().clone().requires_grad_() for x in (q, k, v))
+    pt, _ = attention_ref(qp, kp, vp, causal=causal, upcast=False, reorder_ops=True)
+    gp = torch.autograd.grad(pt, (qp, kp, vp), g)
+    for name, got, r, p in zip(("dq", "dk", "dv"), res[1], gr, gp):
+        ok, err, bound = check_within_bound(got.float(), r.float(), p.float(), floor=1e-4)
+        assert ok, f"{name}: max|err| {err:.3e} > bound {bound:.3e}"

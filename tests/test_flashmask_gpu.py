@@ -240,9 +240,11 @@ def test_flashmask_noop_bounds_equal_plain_attention(causal):
     # the HIP forward here)
     o2 = flash_attn_func(qr, kr, vr, causal=causal)
     g2 = torch.autograd.grad(o2, (qr, kr, vr), dout)
-    torch.testing.assert_close(out, o2, atol=2e-3, rtol=0)
+    # (same Q', same math; the masked HIP kernels and the assembly kernels sum in different orders:
+    # a few elements one bf16 ulp apart, hence the relative term)
+    torch.testing.assert_close(out, o2, atol=2e-3, rtol=2 ** -7)
     for a, bb in zip((dq, dk, dv), g2):
-        torch.testing.assert_close(a, bb, atol=4e-3, rtol=0)
+        torch.testing.assert_close(a, bb, atol=4e-3, rtol=2 ** -7)
 
 
 @pytest.mark.parametrize("causal", [True, False])

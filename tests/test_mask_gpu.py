@@ -136,9 +136,11 @@ def test_dense_mask_zero_is_no_mask():
     # the HIP forward here)
     o2 = flash_attn_func(qr, kr, vr, causal=True)
     g2 = torch.autograd.grad(o2, (qr, kr, vr), dout)
-    torch.testing.assert_close(out, o2, atol=2e-3, rtol=0)
+    # (same Q', same math; the masked HIP kernels and the assembly kernels sum in different orders:
+    # a few elements one bf16 ulp apart, hence the relative term)
+    torch.testing.assert_close(out, o2, atol=2e-3, rtol=2 ** -7)
     for a, bb in zip((dq, dk, dv), g2):
-        torch.testing.assert_close(a, bb, atol=4e-3, rtol=0)
+        torch.testing.assert_close(a, bb, atol=4e-3, rtol=2 ** -7)
 
 
 def test_flashmask_and_bad_mask_dims_rejected():

@@ -141,6 +141,72 @@ class Emu:
         self.hooks = {}            # label -> fn(emu, wave) called when a wave reaches it
         self.trace = []
         self.label_at = {v: k for k, v in self.labels.items()}
+        self.races = None          # check_races(): list of cross-wave LDS conflicts within a barrier interval
+
+    # ---------------------------------------------------------------- LDS race checker
+    def check_races(self, benign=()):
+        """record LDS accesses per 16-byte granule and barrier interval: a wave reading (or writing)
+        bytes another wave wrote, or will overwrite, between the same two barriers, or bytes an
+        LDS-DMA of another wave still has in flight, is a race whatever order the hardware picks.
+        benign: (lo, hi) byte ranges to ignore (e.g. bytes every wave DMAs identically)."""
+        n = 163840 // 16
+        self.races = []
+        self.benign = [(lo // 16, (hi + 15) // 16) for lo, hi in benign]
+        self.epoch = 0
+        self.wr_ep = np.full(n, -1, np.int64)
+        self.wr_wv = np.full(n, -1, np.int64)
+        self.rd_ep = np.full(n, -1, np.int64)
+        self.rd_mask = np.zeros(n, np.int64)
+        self.pend = np.zeros(n, np.int64)       # bitmask of waves with an LDS-DMA in flight there
+
+    def _grs(self, addrs, nb):
+        g = set()
+        for a_ in addrs:
+            for x in range(int(a_) // 16, (int(a_) + nb - 1) // 16 + 1):
+                g.add(x)
+        return [x for x in sorted(g) if not any(lo <= x < hi for lo, hi in self.benign)]
+
+    def _race(self, w, kind, gr):
+        if len(self.races) < 50:
+            op = self.insts[w.pc - 1][3] if w.pc > 0 else "?"
+            self.races.append(f"epoch {self.epoch} wave {w.wid} {kind} at LDS {16 * gr}: {op}")
+
+    def _lds_read(self, w, addrs, nb):
+        if self.races is None:
+            return
+        bit = 1 << w.wid
+        for gr in self._grs(addrs, nb):
+            if self.pend[gr] & ~bit:
+                self._race(w, "read of another wave's in-flight DMA", gr)
+            if self.wr_ep[gr] == self.epoch and self.wr_wv[gr] != w.wid:
+                self._race(w, f"read after wave {self.wr_wv[gr]}'s write", gr)
+            if self.rd_ep[gr] != self.epoch:
+                self.rd_ep[gr], self.rd_mask[gr] = self.epoch, 0
+            self.rd_mask[gr] |= bit
+
+    def _lds_write(self, w, addrs, nb, dma=False):
+        if self.races is None:
+            return
+        bit = 1 << w.wid
+        for gr in self._grs(addrs, nb):
+            if self.rd_ep[gr] == self.epoch and self.rd_mask[gr] & ~bit:
+                self._race(w, "write of bytes another wave read" + (" (DMA)" if dma else ""), gr)
+            if not dma:
+                if self.wr_ep[gr] == self.epoch and self.wr_wv[gr] != w.wid:
+                    self._race(w, f"write after wave {self.wr_wv[gr]}'s write", gr)
+                if self.pend[gr] & ~bit:
+                    self._race(w, "write of another wave's in-flight DMA", gr)
+                self.wr_ep[gr], self.wr_wv[gr] = self.epoch, w.wid
+            else:
+                self.pend[gr] |= bit
+
+    def _dma_land(self, w, dst, nb):
+        if self.races is None:
+            return
+        bit = 1 << w.wid
+        for gr in self._grs([dst], nb):
+            self.pend[gr] &= ~bit
+            self.wr_ep[gr], self.wr_wv[gr] = self.epoch, w.wid
 
     # ---------------------------------------------------------------- operands
     def reg_index(self, tok):
@@ -215,7 +281,9 @@ class Emu:
         return self.heap.get(addr, n)
 
     # ---------------------------------------------------------------- execution
-    def run_wg(self, wg_id, kernarg_addr, nwaves=4):
+    def run_wg(self, wg_id, kernarg_addr, nwaves=4, order=None):
+        """order: the waves' order between two barriers (None: 0 first; "reverse": the last first --
+        a read of data another wave writes in the same barrier interval then sees the other version)"""
         lds = np.zeros(LDS_SIZE, dtype=np.uint8)
         waves = [Wave(i) for i in range(nwaves)]
         for w in waves:
@@ -223,9 +291,10 @@ class Emu:
             w.s[1] = kernarg_addr >> 32
             w.s[2] = wg_id
             w.r[0] = np.arange(64, dtype=np.uint32) + 64 * w.wid
+        seq = waves[::-1] if order == "reverse" else waves
         while True:
             progressed = False
-            for w in waves:
+            for w in seq:
                 while not w.done and not w.at_barrier:
                     self.step(w, lds)
                     progressed = True
@@ -235,6 +304,8 @@ class Emu:
             if all(w.at_barrier for w in live):
                 for w in live:
                     w.at_barrier = False
+                if self.races is not None:
+                    self.epoch += 1
                 continue
             if not progressed:
                 raise RuntimeError("deadlock")
@@ -271,6 +342,7 @@ class Emu:
                         e = w.vm.pop(0)
                         if e is not None:
                             lds[e[0]:e[0] + len(e[1])] = e[1]
+                            self._dma_land(w, e[0], len(e[1]))
             return
         if op == "s_nop" or op == "s_setprio":
             return
@@ -278,6 +350,7 @@ class Emu:
             for e in w.vm:
                 if e is not None:
                     lds[e[0]:e[0] + len(e[1])] = e[1]
+                    self._dma_land(w, e[0], len(e[1]))
             w.vm = []
             w.done = True
             return
@@ -313,6 +386,7 @@ class Emu:
             return
         if op == "ds_read_b128":
             addr = self.vsrc(w, a[1]).astype(np.int64) + mods.get("offset", 0)
+            self._lds_read(w, addr, 16)
             ri, n = self.regs(w, a[0])
             for lane in range(64):
                 d = lds[addr[lane]:addr[lane] + 16].view(np.uint32)
@@ -322,11 +396,13 @@ class Emu:
             addr = self.vsrc(w, a[0]).astype(np.int64) + mods.get("offset", 0)
             ri, n = self.regs(w, a[1])
             nb = 8 if op == "ds_write_b64" else 16
+            self._lds_write(w, addr, nb)
             for lane in range(64):
                 lds[addr[lane]:addr[lane] + nb] = w.r[ri:ri + nb // 4, lane].astype(np.uint32).view(np.uint8)
             return
         if op == "ds_read_b64_tr_b16":
             addr = self.vsrc(w, a[1]).astype(np.int64) + mods.get("offset", 0)
+            self._lds_read(w, addr, 8)
             ri, n = self.regs(w, a[0])
             loaded = np.stack([lds[addr[l]:addr[l] + 8].view(np.uint16) for l in range(64)])  # [64][4]
             out = np.zeros((64, 4), dtype=np.uint16)
@@ -558,6 +634,7 @@ class Emu:
                 # lands later (s_waitcnt vmcnt): a read before the wait sees the old LDS contents
                 dst = w.m0
                 w.vm.append((dst, np.ascontiguousarray(data).view(np.uint8).ravel().copy()))
+                self._lds_write(w, [dst], 64 * size, dma=True)
                 return
             else:
                 ri, _ = self.regs(w, a[0])

@@ -19,12 +19,18 @@ from isa import dkdv_item_decode  # noqa: E402
 from asm_emu import Emu, Heap, bf16_to_f32, f16_to_f32, f32_to_bf16, f32_to_f16  # noqa: E402
 
 GEN = os.path.join(ROOT, "xhy-flash-attention_amd", "csrc", "asm", "gen_bwd.py")
+GEN2 = os.path.join(ROOT, "xhy-flash-attention_amd", "csrc", "asm", "gen_bwd2.py")
 D = 128
 BKN = 128
+# (v2: the two-waves-per-SIMD kernel of gen_bwd2.py, 8 waves per workgroup; same arguments)
+KINDS = {1: (GEN, "fa_bwd_dkdv_asm", 4), 2: (GEN2, "fa_bwd2_dkdv_asm", 8)}
+# the -LSE / -D ring, which every wave DMAs with the same bytes (benign for the race checker)
+LRING = {1: (147456, 147456 + 4096), 2: (114688, 114688 + 4096)}
+RACES = []          # cross-wave LDS races the last run found (race checker on)
 
 
-def asm_text():
-    return subprocess.run([sys.executable, GEN], check=True, capture_output=True, text=True).stdout
+def asm_text(v=1):
+    return subprocess.run([sys.executable, KINDS[v][0]], check=True, capture_output=True, text=True).stdout
 
 
 def pack_args(**kw):
@@ -73,12 +79,12 @@ def reference(q, k, v, do, causal, scale):
 
 
 def run(b=1, sq=200, sk=200, h=2, hk=1, causal=True, bf16=True, reduce=True, seed=0, text=None, verbose=True,
-        grid=None, unit_c=False, lens=None, table=False):
+        grid=None, unit_c=False, lens=None, table=False, ver=1, order=None):
     """grid: workgroups of the persistent item loop (default: one per item); unit_c: the _c1 kernel
     (c = 1: scale = ln 2, the launch of a backward on the prescaled Q'); lens: varlen (unpadded,
     cu_seqlens_q = cu_seqlens_k from these lengths; b, sq, sk follow from them)"""
     if lens is not None:
-        return run_varlen(lens, h, hk, causal, bf16, reduce, seed, text, verbose, grid, table)
+        return run_varlen(lens, h, hk, causal, bf16, reduce, seed, text, verbose, grid, table, ver, order)
     rng = np.random.default_rng(seed)
     q = rng.standard_normal((b, sq, h, D)).astype(np.float32)
     k = rng.standard_normal((b, sk, hk, D)).astype(np.float32)
@@ -121,11 +127,15 @@ def run(b=1, sq=200, sk=200, h=2, hk=1, causal=True, bf16=True, reduce=True, see
               dv_head=D * 2, sq=sq, sk=sk, h=h, ng=ng, nh=g if red else 1, group=g,
               c=1.0 if unit_c else float(np.float32(scale * 1.4426950408889634)), scale=float(np.float32(scale)), flags=2 if red else 0)
     akarg = heap.put(np.frombuffer(pack_args(**kw), dtype=np.uint8))
-    text = text or asm_text()
-    name = f"fa_bwd_dkdv_asm_d128_{'bf16' if bf16 else 'f16'}_{'causal' if causal else 'full'}{'_c1' if unit_c else ''}"
+    text = text or asm_text(ver)
+    name = f"{KINDS[ver][1]}_d128_{'bf16' if bf16 else 'f16'}_{'causal' if causal else 'full'}{'_c1' if unit_c else ''}"
     emu = Emu(text, name, heap)
+    emu.check_races(benign=[LRING[ver]])
     for L in range(grid or n_items):
-        emu.run_wg(L, akarg)
+        emu.run_wg(L, akarg, nwaves=KINDS[ver][2], order=order)
+    RACES[:] = emu.races
+    if verbose and emu.races:
+        print("LDS races:", *emu.races[:10], sep="\n  ")
     dk = dec(heap.get(adk, b * sk * nh_out * D * 2).view(np.uint16)).reshape(b, sk, nh_out, D).astype(np.float64)
     dv = dec(heap.get(adv, b * sk * nh_out * D * 2).view(np.uint16)).reshape(b, sk, nh_out, D).astype(np.float64)
     ek = np.abs(dk - dk_ref).max() / max(np.abs(dk_ref).max(), 1e-9)
@@ -152,7 +162,7 @@ def varlen_items(lens, nh, gdiv, rows, nlev, reverse):
     return np.array([len(out) // 2, 0] + out, dtype=np.uint32)
 
 
-def run_varlen(lens, h, hk, causal, bf16, reduce, seed, text, verbose, grid, table=False):
+def run_varlen(lens, h, hk, causal, bf16, reduce, seed, text, verbose, grid, table=False, ver=1, order=None):
     """varlen launch (flags bit 0 clear: row offsets from cu_seqlens): packed (total, heads, D);
     table: the items from the device-built list (flags bit 2, the persistent varlen launch)"""
     rng = np.random.default_rng(seed)
@@ -207,11 +217,15 @@ def run_varlen(lens, h, hk, causal, bf16, reduce, seed, text, verbose, grid, tab
               c=float(np.float32(scale * 1.4426950408889634)), scale=float(np.float32(scale)),
               flags=(2 if red else 0) | (4 if table else 0))
     akarg = heap.put(np.frombuffer(pack_args(**kw), dtype=np.uint8))
-    text = text or asm_text()
-    name = f"fa_bwd_dkdv_asm_d128_{'bf16' if bf16 else 'f16'}_{'causal' if causal else 'full'}"
+    text = text or asm_text(ver)
+    name = f"{KINDS[ver][1]}_d128_{'bf16' if bf16 else 'f16'}_{'causal' if causal else 'full'}"
     emu = Emu(text, name, heap)
+    emu.check_races(benign=[LRING[ver]])
     for L in range(grid or n_items):
-        emu.run_wg(L, akarg)
+        emu.run_wg(L, akarg, nwaves=KINDS[ver][2], order=order)
+    RACES[:] = emu.races
+    if verbose and emu.races:
+        print("LDS races:", *emu.races[:10], sep="\n  ")
     dk = dec(heap.get(adk, nbytes).view(np.uint16)).reshape(total, nh_out, D).astype(np.float64)
     dv = dec(heap.get(adv, nbytes).view(np.uint16)).reshape(total, nh_out, D).astype(np.float64)
     ek = np.abs(dk - dk_ref).max() / max(np.abs(dk_ref).max(), 1e-9)
@@ -233,5 +247,10 @@ if __name__ == "__main__":
     ap.add_argument("--fp16", action="store_true")
     ap.add_argument("--noreduce", action="store_true")
     ap.add_argument("--seed", type=int, default=0)
+    ap.add_argument("--v2", action="store_true", help="the two-waves-per-SIMD kernel (gen_bwd2.py)")
+    ap.add_argument("--reverse", action="store_true", help="run the waves last-to-first between barriers")
+    ap.add_argument("--grid", type=int, default=None)
+    ap.add_argument("--c1", action="store_true")
     a = ap.parse_args()
-    run(a.b, a.sq, a.sk, a.h, a.hk, not a.full, not a.fp16, not a.noreduce, a.seed)
+    run(a.b, a.sq, a.sk, a.h, a.hk, not a.full, not a.fp16, not a.noreduce, a.seed, ver=2 if a.v2 else 1,
+        order="reverse" if a.reverse else None, grid=a.grid, unit_c=a.c1)

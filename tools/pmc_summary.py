@@ -18,7 +18,7 @@ def main(root):
                 for row in csv.DictReader(fh):
                     name = row.get("Kernel_Name", "")
                     short = name.split("(")[0].split("::")[-1].split("<")[0]
-                    if not short or "kernel" not in short:
+                    if not short or ("kernel" not in short and not short.startswith("fa_")):
                         continue
                     acc[short][row["Counter_Name"]].append(float(row["Counter_Value"]))
         print(f"== {os.path.basename(vdir)}")

@@ -33,6 +33,8 @@ extern "C" const unsigned char fa_bwd_asm_co[];
 extern "C" const unsigned long fa_bwd_asm_co_size;
 extern "C" const unsigned char fa_dq_asm_co[];
 extern "C" const unsigned long fa_dq_asm_co_size;
+extern "C" const unsigned char fa_bwd2_asm_co[];
+extern "C" const unsigned long fa_bwd2_asm_co_size;
 
 namespace fa {
 namespace {
@@ -86,8 +88,9 @@ static_assert(sizeof(DqAsmArgs) == 304 && offsetof(DqAsmArgs, dec) == 184 && off
 constexpr int kMaxDev = 64;
 constexpr int kBkn = 128;   // keys per workgroup
 struct DevModule {
-  hipModule_t mod = nullptr, mod_dq = nullptr;
+  hipModule_t mod = nullptr, mod_dq = nullptr, mod2 = nullptr;
   hipFunction_t fn[8] = {};      // dK/dV [bf16 causal, bf16 full, f16 causal, f16 full], then the same with c = 1
+  hipFunction_t fn2[8] = {};     // the same, two waves per SIMD (gen_bwd2.py, 512 threads)
   hipFunction_t fn_dq[4] = {};   // dQ, the same order
   int cus = 0;
 };
@@ -100,6 +103,10 @@ const char* kNames[8] = {"fa_bwd_dkdv_asm_d128_bf16_causal", "fa_bwd_dkdv_asm_d1
                          "fa_bwd_dkdv_asm_d128_f16_causal", "fa_bwd_dkdv_asm_d128_f16_full",
                          "fa_bwd_dkdv_asm_d128_bf16_causal_c1", "fa_bwd_dkdv_asm_d128_bf16_full_c1",
                          "fa_bwd_dkdv_asm_d128_f16_causal_c1", "fa_bwd_dkdv_asm_d128_f16_full_c1"};
+const char* kNames2[8] = {"fa_bwd2_dkdv_asm_d128_bf16_causal", "fa_bwd2_dkdv_asm_d128_bf16_full",
+                          "fa_bwd2_dkdv_asm_d128_f16_causal", "fa_bwd2_dkdv_asm_d128_f16_full",
+                          "fa_bwd2_dkdv_asm_d128_bf16_causal_c1", "fa_bwd2_dkdv_asm_d128_bf16_full_c1",
+                          "fa_bwd2_dkdv_asm_d128_f16_causal_c1", "fa_bwd2_dkdv_asm_d128_f16_full_c1"};
 const char* kDqNames[4] = {"fa_bwd_dq_asm_d128_bf16_causal", "fa_bwd_dq_asm_d128_bf16_full",
                            "fa_bwd_dq_asm_d128_f16_causal", "fa_bwd_dq_asm_d128_f16_full"};
 
@@ -115,6 +122,8 @@ DevModule& module_for(int dev) {
     for (int i = 0; i < 8; ++i) check(hipModuleGetFunction(&m.fn[i], m.mod, kNames[i]), kNames[i]);
     check(hipModuleLoadData(&m.mod_dq, fa_dq_asm_co), "hipModuleLoadData (dQ)");
     for (int i = 0; i < 4; ++i) check(hipModuleGetFunction(&m.fn_dq[i], m.mod_dq, kDqNames[i]), kDqNames[i]);
+    check(hipModuleLoadData(&m.mod2, fa_bwd2_asm_co), "hipModuleLoadData (dK/dV, two waves per SIMD)");
+    for (int i = 0; i < 8; ++i) check(hipModuleGetFunction(&m.fn2[i], m.mod2, kNames2[i]), kNames2[i]);
     check(hipDeviceGetAttribute(&m.cus, hipDeviceAttributeMultiprocessorCount, dev), "hipDeviceGetAttribute");
   }
   return m;
@@ -156,10 +165,16 @@ void launch_bwd_dkdv_asm(const BwdParams& p, bool is_bf16, hipStream_t stream) {
   check(hipGetDevice(&dev), "hipGetDevice");
   hipFunction_t fn;
   int cus = 0;
+  // knob 10 (default 0): the kernel with two waves per SIMD, specialised by role (gen_bwd2.py: 8
+  // waves, the P waves accumulate dV, the dS waves dK; P crosses in LDS) -- bitwise the same dK / dV,
+  // 7-8 % slower at C3 on two boxes; the P exchange costs ~11 % (ablation), its barriers ~2 %
+  // (profiles/r06/ab_bwd2_*_r06*.txt)
+  const bool two_waves = knob(kKnobBwd2W) != 0;
   {
     std::lock_guard<std::mutex> lk(g_mu);
     DevModule& m = module_for(dev);
-    fn = m.fn[(s.scale_log2 == 1.0f ? 4 : 0) + (is_bf16 ? 0 : 2) + (s.causal ? 0 : 1)];
+    const int v = (s.scale_log2 == 1.0f ? 4 : 0) + (is_bf16 ? 0 : 2) + (s.causal ? 0 : 1);
+    fn = two_waves ? m.fn2[v] : m.fn[v];
     cus = m.cus;
   }
   // persistent grid (knob 6, default on): one workgroup per CU (151 KiB of LDS allows one) walking the
@@ -211,7 +226,8 @@ void launch_bwd_dkdv_asm(const BwdParams& p, bool is_bf16, hipStream_t stream) {
   a.grid = (int32_t)grid;
   size_t sz = sizeof(a);
   void* cfg[] = {HIP_LAUNCH_PARAM_BUFFER_POINTER, &a, HIP_LAUNCH_PARAM_BUFFER_SIZE, &sz, HIP_LAUNCH_PARAM_END};
-  check(hipModuleLaunchKernel(fn, (unsigned)grid, 1, 1, 256, 1, 1, 0, stream, nullptr, cfg), "hipModuleLaunchKernel");
+  check(hipModuleLaunchKernel(fn, (unsigned)grid, 1, 1, two_waves ? 512 : 256, 1, 1, 0, stream, nullptr, cfg),
+        "hipModuleLaunchKernel");
 }
 
 // fused: the kernel also reads O (the fused preprocessing, knob 8): its strides and 256-row records

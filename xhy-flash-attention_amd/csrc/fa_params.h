@@ -220,7 +220,10 @@ enum Knob { kKnobNoSplitKv = 0 /* FLASH_ATTN_MI355X_NO_SPLITKV: 1 = never split 
             kKnobVarlenRounds = 9 /* FLASH_ATTN_MI355X_VARLEN_ROUNDS: items per workgroup of the assembly
                                      dK/dV kernel on varlen calls (default 2, snake-paired
                                      rounds; 1 = one workgroup per item, the dispatcher balancing) */,
-            kNumKnobs = 10 };
+            kKnobBwd2W = 10 /* FLASH_ATTN_MI355X_BWD_2W: 1 = the assembly dK/dV kernel with two waves per SIMD
+                               (gen_bwd2.py, 8 waves by role; bitwise the same results, 7-8 % slower at C3,
+                               DESIGN.md round 6); 0 (default) = one wave per SIMD (gen_bwd.py) */,
+            kNumKnobs = 11 };
 int knob(int id);
 void set_knob(int id, int value);
 
