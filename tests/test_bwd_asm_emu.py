@@ -231,3 +231,35 @@ def test_asm_dkdv_two_waves_varlen_in_emulator(asm2_text):
     ek, ev, *_ = emu_bwd.run(lens=[130, 0, 1, 257], h=2, hk=1, causal=True, text=asm2_text, verbose=False, ver=2)
     assert not emu_bwd.RACES, emu_bwd.RACES[:3]
     assert max(ek, ev) < 1e-2
+
+
+# ------------------------------------------------------------------------------------------------
+# head dim 64 (csrc/asm/gen_bwd64.py): 4 waves x 64 keys (two 32-key groups a wave sharing every A
+# fragment), 256-key blocks, 2-piece subtile DMA; against the float64 restatement, race checker on
+# ------------------------------------------------------------------------------------------------
+@pytest.fixture(scope="module")
+def asm64_text():
+    return emu_bwd.asm_text(64)
+
+
+@pytest.mark.timeout(900)
+@pytest.mark.parametrize("b,sq,sk,h,hk,causal,bf16,reduce,grid,unit_c", [
+    (1, 64, 256, 1, 1, True, True, False, None, False),     # one step: first + last + masked
+    (1, 300, 300, 2, 1, True, True, True, None, False),     # GQA reduce across a head boundary
+    (1, 40, 600, 1, 1, False, True, False, None, False),    # three key blocks, the last ragged
+    (1, 333, 257, 4, 2, False, False, True, None, True),    # fp16, c = 1 (the folded backward)
+    (2, 300, 700, 2, 1, True, True, True, 3, False),        # persistent loop
+    (1, 600, 40, 2, 2, True, True, False, None, False),     # keys fewer than a group
+])
+def test_asm_dkdv_d64_in_emulator(asm64_text, b, sq, sk, h, hk, causal, bf16, reduce, grid, unit_c):
+    ek, ev, *_ = emu_bwd.run(b, sq, sk, h, hk, causal, bf16, reduce, seed=1, text=asm64_text, verbose=False,
+                             grid=grid, unit_c=unit_c, ver=64)
+    assert not emu_bwd.RACES, emu_bwd.RACES[:3]
+    assert max(ek, ev) < (1e-2 if bf16 else 2e-3), (ek, ev)
+
+
+@pytest.mark.timeout(900)
+def test_asm_dkdv_d64_varlen_in_emulator(asm64_text):
+    ek, ev, *_ = emu_bwd.run(lens=[130, 0, 1, 557], h=2, hk=1, causal=True, text=asm64_text, verbose=False, ver=64)
+    assert not emu_bwd.RACES, emu_bwd.RACES[:3]
+    assert max(ek, ev) < 1e-2

@@ -20,12 +20,14 @@ from asm_emu import Emu, Heap, bf16_to_f32, f16_to_f32, f32_to_bf16, f32_to_f16 
 
 GEN = os.path.join(ROOT, "xhy-flash-attention_amd", "csrc", "asm", "gen_bwd.py")
 GEN2 = os.path.join(ROOT, "xhy-flash-attention_amd", "csrc", "asm", "gen_bwd2.py")
+GEN64 = os.path.join(ROOT, "xhy-flash-attention_amd", "csrc", "asm", "gen_bwd64.py")
 D = 128
 BKN = 128
 # (v2: the two-waves-per-SIMD kernel of gen_bwd2.py, 8 waves per workgroup; same arguments)
-KINDS = {1: (GEN, "fa_bwd_dkdv_asm", 4), 2: (GEN2, "fa_bwd2_dkdv_asm", 8)}
+KINDS = {1: (GEN, "fa_bwd_dkdv_asm", 4), 2: (GEN2, "fa_bwd2_dkdv_asm", 8), 64: (GEN64, "fa_bwd_dkdv_asm", 4)}
+DIMS = {1: (128, 128), 2: (128, 128), 64: (64, 256)}     # (head dim, keys per workgroup)
 # the -LSE / -D ring, which every wave DMAs with the same bytes (benign for the race checker)
-LRING = {1: (147456, 147456 + 4096), 2: (114688, 114688 + 4096)}
+LRING = {1: (147456, 147456 + 4096), 2: (114688, 114688 + 4096), 64: (73728, 73728 + 4096)}
 RACES = []          # cross-wave LDS races the last run found (race checker on)
 
 
@@ -85,6 +87,7 @@ def run(b=1, sq=200, sk=200, h=2, hk=1, causal=True, bf16=True, reduce=True, see
     cu_seqlens_q = cu_seqlens_k from these lengths; b, sq, sk follow from them)"""
     if lens is not None:
         return run_varlen(lens, h, hk, causal, bf16, reduce, seed, text, verbose, grid, table, ver, order)
+    D, BKN = DIMS[ver]
     rng = np.random.default_rng(seed)
     q = rng.standard_normal((b, sq, h, D)).astype(np.float32)
     k = rng.standard_normal((b, sk, hk, D)).astype(np.float32)
@@ -128,7 +131,7 @@ def run(b=1, sq=200, sk=200, h=2, hk=1, causal=True, bf16=True, reduce=True, see
               c=1.0 if unit_c else float(np.float32(scale * 1.4426950408889634)), scale=float(np.float32(scale)), flags=2 if red else 0)
     akarg = heap.put(np.frombuffer(pack_args(**kw), dtype=np.uint8))
     text = text or asm_text(ver)
-    name = f"{KINDS[ver][1]}_d128_{'bf16' if bf16 else 'f16'}_{'causal' if causal else 'full'}{'_c1' if unit_c else ''}"
+    name = f"{KINDS[ver][1]}_d{D}_{'bf16' if bf16 else 'f16'}_{'causal' if causal else 'full'}{'_c1' if unit_c else ''}"
     emu = Emu(text, name, heap)
     emu.check_races(benign=[LRING[ver]])
     for L in range(grid or n_items):
@@ -165,6 +168,7 @@ def varlen_items(lens, nh, gdiv, rows, nlev, reverse):
 def run_varlen(lens, h, hk, causal, bf16, reduce, seed, text, verbose, grid, table=False, ver=1, order=None):
     """varlen launch (flags bit 0 clear: row offsets from cu_seqlens): packed (total, heads, D);
     table: the items from the device-built list (flags bit 2, the persistent varlen launch)"""
+    D, BKN = DIMS[ver]
     rng = np.random.default_rng(seed)
     b, total, mx = len(lens), sum(lens), max(lens)
     cu = np.concatenate([[0], np.cumsum(lens)]).astype(np.int32)
@@ -218,7 +222,7 @@ def run_varlen(lens, h, hk, causal, bf16, reduce, seed, text, verbose, grid, tab
               flags=(2 if red else 0) | (4 if table else 0))
     akarg = heap.put(np.frombuffer(pack_args(**kw), dtype=np.uint8))
     text = text or asm_text(ver)
-    name = f"{KINDS[ver][1]}_d128_{'bf16' if bf16 else 'f16'}_{'causal' if causal else 'full'}"
+    name = f"{KINDS[ver][1]}_d{D}_{'bf16' if bf16 else 'f16'}_{'causal' if causal else 'full'}"
     emu = Emu(text, name, heap)
     emu.check_races(benign=[LRING[ver]])
     for L in range(grid or n_items):
@@ -248,9 +252,10 @@ if __name__ == "__main__":
     ap.add_argument("--noreduce", action="store_true")
     ap.add_argument("--seed", type=int, default=0)
     ap.add_argument("--v2", action="store_true", help="the two-waves-per-SIMD kernel (gen_bwd2.py)")
+    ap.add_argument("--d64", action="store_true", help="the head-dim-64 kernel (gen_bwd64.py)")
     ap.add_argument("--reverse", action="store_true", help="run the waves last-to-first between barriers")
     ap.add_argument("--grid", type=int, default=None)
     ap.add_argument("--c1", action="store_true")
     a = ap.parse_args()
-    run(a.b, a.sq, a.sk, a.h, a.hk, not a.full, not a.fp16, not a.noreduce, a.seed, ver=2 if a.v2 else 1,
+    run(a.b, a.sq, a.sk, a.h, a.hk, not a.full, not a.fp16, not a.noreduce, a.seed, ver=2 if a.v2 else (64 if a.d64 else 1),
         order="reverse" if a.reverse else None, grid=a.grid, unit_c=a.c1)

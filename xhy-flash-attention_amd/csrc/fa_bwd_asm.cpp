@@ -4,7 +4,10 @@
 //
 // The kernel covers the headline backward: head dim 128, bf16 / fp16, causal or not, fixed length
 // or varlen, MHA / GQA (reduced in-kernel over the group, or expanded per query head), no dropout /
-// mask / FlashMask.  It replaces bwd_dkdv_kernel for those calls; bwd_pre_kernel then writes the
+// mask / FlashMask.  Head dim 64 has its own dK / dV kernels (round 6, gen_bwd64.py: 4 waves x 64
+// keys, each A fragment feeding both 32-key groups' MFMAs, 256-key blocks; C2-class / d64 dK/dV
+// -33 to -41 % against bwd_dkdv_kernel, profiles/r06/ab_d64_*_r06g.txt); its dQ stays on the HIP
+// kernel.  It replaces bwd_dkdv_kernel for those calls; bwd_pre_kernel then writes the
 // per-row chain starts it streams (-LSE / scale and -D, 32 rows per 256-byte group: the "lsed"
 // scratch), and the dQ kernel is unchanged.  Everything else -- and this path when it is switched
 // off (FLASH_ATTN_MI355X_BWD_ASM=0 or knob 3) -- runs bwd_dkdv_kernel (fa_bwd.hip).
@@ -35,6 +38,8 @@ extern "C" const unsigned char fa_dq_asm_co[];
 extern "C" const unsigned long fa_dq_asm_co_size;
 extern "C" const unsigned char fa_bwd2_asm_co[];
 extern "C" const unsigned long fa_bwd2_asm_co_size;
+extern "C" const unsigned char fa_bwd64_asm_co[];
+extern "C" const unsigned long fa_bwd64_asm_co_size;
 
 namespace fa {
 namespace {
@@ -86,9 +91,12 @@ static_assert(sizeof(DqAsmArgs) == 304 && offsetof(DqAsmArgs, dec) == 184 && off
               offsetof(DqAsmArgs, qf) == 272, "DqAsmArgs layout");
 
 constexpr int kMaxDev = 64;
-constexpr int kBkn = 128;   // keys per workgroup
+constexpr int kBkn = 128;   // keys per workgroup (head dim 128)
+constexpr int kBkn64 = 256; // head dim 64: 4 waves x 64 keys (gen_bwd64.py)
+int bkn_of(int d) { return d == 64 ? kBkn64 : kBkn; }
 struct DevModule {
-  hipModule_t mod = nullptr, mod_dq = nullptr, mod2 = nullptr;
+  hipModule_t mod = nullptr, mod_dq = nullptr, mod2 = nullptr, mod64 = nullptr;
+  hipFunction_t fn64[8] = {};    // head dim 64, the order of fn
   hipFunction_t fn[8] = {};      // dK/dV [bf16 causal, bf16 full, f16 causal, f16 full], then the same with c = 1
   hipFunction_t fn2[8] = {};     // the same, two waves per SIMD (gen_bwd2.py, 512 threads)
   hipFunction_t fn_dq[4] = {};   // dQ, the same order
@@ -107,6 +115,10 @@ const char* kNames2[8] = {"fa_bwd2_dkdv_asm_d128_bf16_causal", "fa_bwd2_dkdv_asm
                           "fa_bwd2_dkdv_asm_d128_f16_causal", "fa_bwd2_dkdv_asm_d128_f16_full",
                           "fa_bwd2_dkdv_asm_d128_bf16_causal_c1", "fa_bwd2_dkdv_asm_d128_bf16_full_c1",
                           "fa_bwd2_dkdv_asm_d128_f16_causal_c1", "fa_bwd2_dkdv_asm_d128_f16_full_c1"};
+const char* kNames64[8] = {"fa_bwd_dkdv_asm_d64_bf16_causal", "fa_bwd_dkdv_asm_d64_bf16_full",
+                           "fa_bwd_dkdv_asm_d64_f16_causal", "fa_bwd_dkdv_asm_d64_f16_full",
+                           "fa_bwd_dkdv_asm_d64_bf16_causal_c1", "fa_bwd_dkdv_asm_d64_bf16_full_c1",
+                           "fa_bwd_dkdv_asm_d64_f16_causal_c1", "fa_bwd_dkdv_asm_d64_f16_full_c1"};
 const char* kDqNames[4] = {"fa_bwd_dq_asm_d128_bf16_causal", "fa_bwd_dq_asm_d128_bf16_full",
                            "fa_bwd_dq_asm_d128_f16_causal", "fa_bwd_dq_asm_d128_f16_full"};
 
@@ -124,6 +136,8 @@ DevModule& module_for(int dev) {
     for (int i = 0; i < 4; ++i) check(hipModuleGetFunction(&m.fn_dq[i], m.mod_dq, kDqNames[i]), kDqNames[i]);
     check(hipModuleLoadData(&m.mod2, fa_bwd2_asm_co), "hipModuleLoadData (dK/dV, two waves per SIMD)");
     for (int i = 0; i < 8; ++i) check(hipModuleGetFunction(&m.fn2[i], m.mod2, kNames2[i]), kNames2[i]);
+    check(hipModuleLoadData(&m.mod64, fa_bwd64_asm_co), "hipModuleLoadData (dK/dV, head dim 64)");
+    for (int i = 0; i < 8; ++i) check(hipModuleGetFunction(&m.fn64[i], m.mod64, kNames64[i]), kNames64[i]);
     check(hipDeviceGetAttribute(&m.cus, hipDeviceAttributeMultiprocessorCount, dev), "hipDeviceGetAttribute");
   }
   return m;
@@ -138,16 +152,17 @@ void* g_stamps = nullptr;   // flash_attn_debug_bwd_stamps
 bool bwd_asm_applicable(const BwdParams& p) {
   const AttnShape& s = p.s;
   if (knob(kKnobBwdAsm) == 0) return false;
-  if (s.d != 128 || s.dropout || s.mask != nullptr || s.fm_lts != nullptr) return false;
+  if ((s.d != 128 && s.d != 64) || s.dropout || s.mask != nullptr || s.fm_lts != nullptr) return false;
   if (s.hk <= 0 || s.h % s.hk != 0 || s.b > 65535 || s.h > 65535) return false;
-  const int nblk = (s.seqlen_k + kBkn - 1) / kBkn;
+  const int bkn = bkn_of(s.d);
+  const int nblk = (s.seqlen_k + bkn - 1) / bkn;
   if (nblk > 65535 || (long long)s.b * s.h * nblk > 0x7fffffffll) return false;
   if ((32ll * ((s.seqlen_q + 31) / 32) + 15) / 16 > 65535) return false;   // bwd_pre_kernel's grid
   for (int64_t x : {p.q_row, p.k_row, p.v_row, p.do_row, p.dk_row, p.dv_row,
                     p.q_head, p.k_head, p.v_head, p.do_head, p.dk_head, p.dv_head})
     if (!fits32(2 * x)) return false;
   // records of one (sequence, head) and the 32-row cursor steps stay below 2^31 bytes
-  const int64_t sq = s.seqlen_q + 64, sk = s.seqlen_k + kBkn;
+  const int64_t sq = s.seqlen_q + 64, sk = s.seqlen_k + bkn;
   for (int64_t x : {sq * 2 * p.q_row, sq * 2 * p.do_row, sk * 2 * p.k_row, sk * 2 * p.v_row, sk * 2 * p.dk_row,
                     sk * 2 * p.dv_row})
     if (!fits32(x)) return false;
@@ -158,7 +173,8 @@ void launch_bwd_dkdv_asm(const BwdParams& p, bool is_bf16, hipStream_t stream) {
   const AttnShape& s = p.s;
   if (p.lsed == nullptr) throw std::runtime_error("flash_attn_bwd (asm dK/dV): no LSE / D scratch");
   const int nh_grid = p.gqa_reduce ? s.hk : s.h;
-  const int nblk = (s.seqlen_k + kBkn - 1) / kBkn;
+  const int bkn = bkn_of(s.d);
+  const int nblk = (s.seqlen_k + bkn - 1) / bkn;
   const long long nwg = (long long)s.b * nh_grid * nblk;
   if (nwg <= 0) return;
   int dev = 0;
@@ -169,12 +185,12 @@ void launch_bwd_dkdv_asm(const BwdParams& p, bool is_bf16, hipStream_t stream) {
   // waves, the P waves accumulate dV, the dS waves dK; P crosses in LDS) -- bitwise the same dK / dV,
   // 7-8 % slower at C3 on two boxes; the P exchange costs ~11 % (ablation), its barriers ~2 %
   // (profiles/r06/ab_bwd2_*_r06*.txt)
-  const bool two_waves = knob(kKnobBwd2W) != 0;
+  const bool two_waves = s.d == 128 && knob(kKnobBwd2W) != 0;
   {
     std::lock_guard<std::mutex> lk(g_mu);
     DevModule& m = module_for(dev);
     const int v = (s.scale_log2 == 1.0f ? 4 : 0) + (is_bf16 ? 0 : 2) + (s.causal ? 0 : 1);
-    fn = two_waves ? m.fn2[v] : m.fn[v];
+    fn = s.d == 64 ? m.fn64[v] : two_waves ? m.fn2[v] : m.fn[v];
     cus = m.cus;
   }
   // persistent grid (knob 6, default on): one workgroup per CU (151 KiB of LDS allows one) walking the
@@ -191,7 +207,7 @@ void launch_bwd_dkdv_asm(const BwdParams& p, bool is_bf16, hipStream_t stream) {
   long long grid = (persist && cus > 0 && nwg > cus) ? cus : nwg;
   StreamScratch vbuf;          // device-built varlen work list (stream-ordered allocation)
   uint32_t* vtab = dev_list ? build_varlen_items(vbuf, s.cu_seqlens_k, s.b, nh_grid, p.gqa_reduce ? 1 : s.h / s.hk,
-                                                 kBkn, nblk, true, nwg, stream)
+                                                 bkn, nblk, true, nwg, stream)
                             : nullptr;
   // varlen, one workgroup per item: R items per workgroup instead (knob 9, default 2) in snake-paired
   // rounds (item w, then the mirror of w, ...), the dispatcher still balancing the workgroups; G a
