@@ -1,6 +1,6 @@
 #!/usr/bin/env python3
-"""Generates fa_fwd_asm.s: the gfx950 FlashAttention-2 forward for head dim 128, written as a
-hand-scheduled assembly kernel (one wave per SIMD).
+"""Generates fa_fwd_asm.s: the gfx950 FlashAttention-2 forward for head dims 128 and 64 (kernels
+fa_fwd_asm_d128_* and fa_fwd_asm_d64_*), written as hand-scheduled assembly (one wave per SIMD).
 
     python3 gen_fwd.py > fa_fwd_asm.s
 
@@ -185,6 +185,7 @@ OPT_MFZERO = os.environ.get("FA_GEN_MFZERO") == "1"          # zero O with 2 NP 
 OPT_EPI2 = os.environ.get("FA_GEN_EPI2") == "1"              # epilogue: groups interleaved stage by stage
 OPT_LAST2 = os.environ.get("FA_GEN_LAST2") == "1"            # last step: PV(a) under softmax(b), then PV(b)
 OPT_NOGUARD = os.environ.get("FA_GEN_NOGUARD") == "1"        # ablation (wrong on a refit): no guard branch
+OPT_SM_ABL = os.environ.get("FA_GEN_SM_ABL", "").split(",")  # ablation (wrong results): nosum / noexp / nocvt
 OPT_T0OV = os.environ.get("FA_GEN_T0OV") == "1"              # tile 0: QK(a), then QK(b) || max / softmax(a)
 # guard: compare as soon as the partial sum is complete, branch on vcc later (round 4 default: the
 # compare + s_cmp + branch in one place stalled the wave, 1.3 % at C3; FA_GEN_GUARD1=1 restores it)
@@ -353,17 +354,20 @@ class K:
             elif fold_add:
                 ops.append(Inst(f"v_add_f32_e32 v{reg}, v{V_NEGMC[j]}, v{reg}", VALU, rd=vr(reg) + vr(V_NEGMC[j]),
                                 wr=vr(reg), key=k + kk + 1))
-            ops.append(Inst(f"v_exp_f32_e32 v{reg}, v{reg}", TRANS, rd=vr(reg), wr=vr(reg), key=k + kk + 2))
-            if e == 1:    # (p1 + p0: the first two terms in one add, no copy of p0)
+            if "noexp" not in OPT_SM_ABL:
+                ops.append(Inst(f"v_exp_f32_e32 v{reg}, v{reg}", TRANS, rd=vr(reg), wr=vr(reg), key=k + kk + 2))
+            if e > 1 and "nosum" in OPT_SM_ABL:
+                pass
+            elif e == 1:    # (p1 + p0: the first two terms in one add, no copy of p0)
                 a = Inst(f"v_add_f32_e32 v{V_PS[j]}, v{reg}, v{reg - 1}", VALU, rd=vr(reg) + vr(reg - 1),
                          wr=vr(V_PS[j]), key=k + kk + 3)
             elif e > 1:
                 a = Inst(f"v_add_f32_e32 v{V_PS[j]}, v{reg}, v{V_PS[j]}", VALU, rd=vr(reg) + vr(V_PS[j]),
                          wr=vr(V_PS[j]), key=k + kk + 3)
-            if e > 0:
+            if e == 1 or (e > 1 and "nosum" not in OPT_SM_ABL):
                 last_sum = a
                 ops.append(a)
-            if e % 2 == 1:
+            if e % 2 == 1 and "nocvt" not in OPT_SM_ABL:
                 kkf = 2 * st + (g >> 3)
                 w = (g & 7) >> 1
                 ops.append(self.cvt(preg + 4 * kkf + w, reg - 1, reg, key=k + kk + 3))
