@@ -44,6 +44,19 @@ def test_asm_forward_in_emulator(asm_text, b, sq, sk, h, hk, causal, bf16, big, 
 
 
 @pytest.mark.timeout(600)
+@pytest.mark.parametrize("seqs,h,hk,causal,bf16,d", [
+    ([300, 37, 290], 2, 1, True, True, 64),       # ragged sequences, one item per workgroup
+    ([300, 0, 100], 4, 2, False, True, 128),      # an empty sequence, GQA, non-causal
+    ([260, 1], 1, 1, True, False, 128),           # fp16, a one-token sequence
+])
+def test_asm_forward_varlen_in_emulator(asm_text, seqs, h, hk, causal, bf16, d):
+    """varlen item starts: cu_seqlens loaded for Q, O and K / V in one scalar round trip"""
+    eo, el = emu_fwd.run_varlen(seqs, h=h, hk=hk, causal=causal, bf16=bf16, text=asm_text, verbose=False, d=d)
+    assert eo <= (1.6e-2 if bf16 else 2e-3), eo
+    assert el <= 1e-5, el
+
+
+@pytest.mark.timeout(600)
 @pytest.mark.parametrize("b,sq,sk,h,hk,causal,bf16,grid", [
     (1, 600, 600, 2, 1, True, True, 1),      # one workgroup walks all 6 items: warm starts (>= 4 tiles)
     (1, 600, 600, 2, 1, True, True, 4),      # snake rounds: items 0-3, then 7, 6 / 5, 4 reversed

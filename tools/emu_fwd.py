@@ -114,6 +114,62 @@ def run(b=1, sq=300, sk=300, h=2, hk=1, causal=True, bf16=True, seed=0, big=None
     return eo, el, o, o_ref, lse, lse_ref
 
 
+def run_varlen(seqs_q, seqs_k=None, h=2, hk=1, causal=True, bf16=True, seed=0, text=None, verbose=True, d=128):
+    """varlen: packed (total, h, d) Q / K / V and cu_seqlens (one workgroup per item, as the
+    launcher runs varlen calls whose K/V stream is grouped per XCD); compares every sequence with
+    the float64 reference on the kernel's folded scores"""
+    seqs_k = seqs_k or seqs_q
+    D, b = d, len(seqs_q)
+    rng = np.random.default_rng(seed)
+    tq, tk = sum(seqs_q), sum(seqs_k)
+    q = rng.standard_normal((tq, h, D)).astype(np.float32)
+    k = rng.standard_normal((tk, hk, D)).astype(np.float32)
+    v = rng.standard_normal((tk, hk, D)).astype(np.float32)
+    enc, dec = (f32_to_bf16, bf16_to_f32) if bf16 else (f32_to_f16, f16_to_f32)
+    q16, k16, v16 = (enc(x).astype(np.uint16) for x in (q, k, v))
+    qf, kf, vf = (dec(x).astype(np.float64) for x in (q16, k16, v16))
+    scale = D ** -0.5
+    msq, msk = max(seqs_q), max(seqs_k)
+    heap = Heap(64 << 20)
+    aq, ak, av = heap.put(q16), heap.put(k16), heap.put(v16)
+    ao = heap.alloc(tq * h * D * 2)
+    heap.get(ao, tq * h * D * 2)[:] = 0xAB   # poison
+    alse = heap.alloc(b * h * msq * 4)
+    cuq = np.array([0] + list(np.cumsum(seqs_q)), dtype=np.int32)
+    cuk = np.array([0] + list(np.cumsum(seqs_k)), dtype=np.int32)
+    acq, ack = heap.put(cuq), heap.put(cuk)
+    nmb = (msq + BM - 1) // BM
+    n_items = b * h * nmb
+    kw = dict(q=aq, k=ak, v=av, o=ao, lse=alse, sched=0, cuq=acq, cuk=ack, rng=0, seed=0, off=0,
+              q_batch=0, k_batch=0, v_batch=0, o_batch=0,
+              q_row=h * D * 2, kv_row=hk * D * 2, o_row=h * D * 2, q_head=D * 2, k_head=D * 2, v_head=D * 2,
+              o_head=D * 2, sq=msq, sk=msk, lse_pitch=msq, h=h, c=float(np.float32(scale * 1.4426950408889634)),
+              flags=0, n_items=n_items, grid=n_items, dec=fwd_item_decode(b * h, h, h // hk, nmb, 0))
+    akarg = heap.put(np.frombuffer(pack_args(**kw), dtype=np.uint8))
+    text = text or asm_text()
+    name = f"fa_fwd_asm_d{D}_{'bf16' if bf16 else 'f16'}_{'causal' if causal else 'full'}"
+    emu = Emu(text, name, heap)
+    for L in range(n_items):
+        emu.run_wg(L, akarg)
+    o = dec(heap.get(ao, tq * h * D * 2).view(np.uint16)).reshape(tq, h, D).astype(np.float64)
+    lse = heap.get(alse, b * h * msq * 4).view(np.float32).reshape(b, h, msq).astype(np.float64)
+    c = np.float32(scale * 1.4426950408889634)
+    qc = dec(enc(qf.astype(np.float32) * c).astype(np.uint16)).astype(np.float64) * (np.log(2.0) / scale)
+    eo = el = 0.0
+    for i in range(b):
+        lq, lk = seqs_q[i], seqs_k[i]
+        if lq == 0 or lk == 0:
+            continue
+        o_ref, lse_ref = reference(qc[None, cuq[i]:cuq[i + 1]], kf[None, cuk[i]:cuk[i + 1]],
+                                   vf[None, cuk[i]:cuk[i + 1]], causal, scale)
+        eo = max(eo, np.abs(o[cuq[i]:cuq[i + 1]] - o_ref[0]).max())
+        el = max(el, np.abs(lse[i, :, :lq] - lse_ref[0]).max())
+    if verbose:
+        print(f"varlen seqs_q={seqs_q} seqs_k={seqs_k} h={h} hk={hk} causal={causal} bf16={bf16} d={D}: "
+              f"max|dO| {eo:.3e} max|dLSE| {el:.3e}  ({emu.count} instructions)")
+    return eo, el
+
+
 if __name__ == "__main__":
     ap = argparse.ArgumentParser()
     ap.add_argument("--b", type=int, default=1)
@@ -128,5 +184,9 @@ if __name__ == "__main__":
     ap.add_argument("--grid", type=int, default=None)
     ap.add_argument("--d", type=int, default=128)
     ap.add_argument("--hp", type=int, default=0)
+    ap.add_argument("--varlen", type=str, default=None, help="comma-separated sequence lengths")
     a = ap.parse_args()
+    if a.varlen:
+        run_varlen([int(x) for x in a.varlen.split(",")], h=a.h, hk=a.hk, causal=not a.full, bf16=not a.fp16, d=a.d)
+        sys.exit(0)
     run(a.b, a.sq, a.sk, a.h, a.hk, not a.full, not a.fp16, a.seed, a.big, grid=a.grid, d=a.d, hp=a.hp)

@@ -27,7 +27,7 @@ import torch  # noqa: E402
 
 import flash_attn_2_cuda as m  # noqa: E402
 from ab import load  # noqa: E402
-from bench import WORKLOADS  # noqa: E402
+from bench import WORKLOADS, c4_seqlens  # noqa: E402
 
 
 def main():
@@ -44,11 +44,27 @@ def main():
     m._lib = lib
     b, s, h, hk, d, dt, causal, _ = WORKLOADS[args.workload]
     dtype = torch.bfloat16 if dt == "bf16" else torch.float16
-    q = torch.randn(b, s, h, d, device="cuda", dtype=dtype)
-    k = torch.randn(b, s, hk, d, device="cuda", dtype=dtype)
-    v = torch.randn(b, s, hk, d, device="cuda", dtype=dtype)
     scale = d ** -0.5
-    nwave = 256 * 4 * 4   # >= grid x 4 waves (persistent grid = CUs)
+    if b is None:   # c4: varlen over the SURVEY 8(d) sequence lengths, packed qkv views
+        lens = c4_seqlens(total=s)
+        cu = torch.tensor([0] + torch.tensor(lens).cumsum(0).tolist(), dtype=torch.int32, device="cuda")
+        q, k, v = torch.randn(s, 3, h, d, device="cuda", dtype=dtype).unbind(1)
+        ms_ = max(lens)
+
+        def call():
+            m.varlen_fwd(q, k, v, None, cu, cu, ms_, ms_, 0.0, scale, False, causal, False, None)
+    else:
+        q = torch.randn(b, s, h, d, device="cuda", dtype=dtype)
+        k = torch.randn(b, s, hk, d, device="cuda", dtype=dtype)
+        v = torch.randn(b, s, hk, d, device="cuda", dtype=dtype)
+
+        def call():
+            m.fwd(q, k, v, None, 0.0, scale, causal, False, None)
+    # one 128-byte record per wave of the grid: the persistent grid has one workgroup per CU, but a
+    # varlen launch without the device list runs one workgroup per item -- size for the larger (an
+    # item covers >= 32 query rows of one head), or the stamp stores run past the buffer
+    rows_q = s if b is None else b * s
+    nwave = max(256 * 4 * 4, 4 * h * (rows_q // 32 + (0 if b is None else b) + 256))
     buf = torch.zeros(nwave * 32, dtype=torch.int32, device="cuda")
     rows = []
     for smp in range(args.samples):
@@ -59,7 +75,7 @@ def main():
         ev0.record()
         while time.time() < t_end:
             for _ in range(10):
-                m.fwd(q, k, v, None, 0.0, scale, causal, False, None)
+                call()
             n += 10
             torch.cuda.synchronize()
         ev1.record()
@@ -67,7 +83,7 @@ def main():
         ms = ev0.elapsed_time(ev1) / n
         buf.zero_()
         lib.flash_attn_debug_fwd_stamps(ctypes.c_void_p(buf.data_ptr()))
-        m.fwd(q, k, v, None, 0.0, scale, causal, False, None)
+        call()
         torch.cuda.synchronize()
         lib.flash_attn_debug_fwd_stamps(ctypes.c_void_p(0))
         a = buf.cpu().numpy().view(np.uint32).reshape(nwave, 32).astype(np.int64)
@@ -86,8 +102,8 @@ def main():
                    cycles_per_tile_med=float(np.median(cpt)), cycles_per_tile_min=float(cpt.min()),
                    us_per_tile_med=float(np.median((r1 - r0) / 100.0 / np.maximum(tiles, 1))),
                    tiles_med=float(np.median(tiles)), items_med=float(np.median(items)), span_us=float(span_us),
-                   ideal_cycles_per_tile=2048)
-        row["mfma_busy_cycles"] = 2048 / row["cycles_per_tile_med"]
+                   ideal_cycles_per_tile=16 * d)
+        row["mfma_busy_cycles"] = 16 * d / row["cycles_per_tile_med"]
         steps = a[:, 19]
         if steps.max() > 0:   # FA_GEN_STAMP=2: per-step compute / wait / barrier cycles
             for i, nm in ((16, "compute"), (17, "vmwait"), (18, "barrier")):

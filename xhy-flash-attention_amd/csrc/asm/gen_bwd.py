@@ -647,15 +647,23 @@ class K:
                     I(f"s_mul_i32 s{T0}, s{a32}, s{b64 + 1}", SALU, rd=sr(a32) + sr(b64 + 1), wr=sr(T0)),
                     I(f"s_add_u32 s{dst[1]}, s{dst[1]}, s{T0}", SALU, rd=sr(dst[1]) + sr(T0), wr=sr(dst[1]))]
 
-        for cu, bstride, rstride, off, seq in ((Pcq, Bq, Rq, QOFF, SQ), (Pcq, Bdo, Rdo, DOOFF, None),
-                                                (Pck, Bk, Rk, KOFF, SK), (Pck, Bv, Rv, VOFF, None),
-                                                (Pck, Bdk, Rdk, DKOFF, None), (Pck, Bdv, Rdv, DVOFF, None)):
-            lf, ld = self.lab("fixed"), self.lab("done")
+        # varlen: the cu_seqlens loads of every part are issued together and waited for once (one
+        # scalar-memory round trip per item start instead of one per part)
+        parts = ((Pcq, Bq, Rq, QOFF, SQ), (Pcq, Bdo, Rdo, DOOFF, None),
+                 (Pck, Bk, Rk, KOFF, SK), (Pck, Bv, Rv, VOFF, None),
+                 (Pck, Bdk, Rdk, DKOFF, None), (Pck, Bdv, Rdv, DVOFF, None))
+        ins += [I(f"s_lshl_b32 s{T1}, s{BIDB}, 2", SALU, rd=sr(BIDB), wr=sr(T1))]
+        for cu, bstride, rstride, off, seq in parts:
+            lf = self.lab("nold")
             ins += [I(f"s_cmp_eq_u64 s[{cu}:{cu + 1}], 0", SALU, rd=sr(cu, 2), wr=[("scc", 0)]),
                     I(f"s_cbranch_scc1 {lf}", BRANCH),
-                    I(f"s_lshl_b32 s{T1}, s{BIDB}, 2", SALU, rd=sr(BIDB), wr=sr(T1)),
                     I(f"s_load_dwordx2 s[{off[0]}:{off[1]}], s[{cu}:{cu + 1}], s{T1}", SMEM, rd=sr(cu, 2) + sr(T1), wr=sr(off[0], 2)),
-                    I("s_waitcnt lgkmcnt(0)", WAIT)]
+                    label(lf)]
+        ins += [I("s_waitcnt lgkmcnt(0)", WAIT)]
+        for cu, bstride, rstride, off, seq in parts:
+            lf, ld = self.lab("fixed"), self.lab("done")
+            ins += [I(f"s_cmp_eq_u64 s[{cu}:{cu + 1}], 0", SALU, rd=sr(cu, 2), wr=[("scc", 0)]),
+                    I(f"s_cbranch_scc1 {lf}", BRANCH)]
             if seq is not None:
                 ins += [I(f"s_sub_u32 s{seq}, s{off[1]}, s{off[0]}", SALU, rd=sr(off[0], 2), wr=sr(seq))]
             ins += [I(f"s_bitcmp1_b32 s{FLG}, 0", SALU, rd=sr(FLG), wr=[("scc", 0)]),

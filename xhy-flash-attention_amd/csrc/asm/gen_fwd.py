@@ -1145,13 +1145,20 @@ class K:
         if not nxt:
             parts.append((A["Pcq"], A["Bo"], A["Ro"], OOFF, None))
         parts.append((A["Pck"], A["Bk"], A["Rkv"], KOFF, SK))
+        # varlen: the cu_seqlens loads of every part are issued together and waited for once (one
+        # scalar-memory round trip per item start instead of one per part)
+        ins += [I(f"s_lshl_b32 s{T1}, s{BIDB}, 2", SALU, rd=sr(BIDB), wr=sr(T1))]
+        for cu, bstride, rstride, off, seq in parts:
+            lf = self.lab("nold")
+            ins += [I(f"s_cmp_eq_u64 s[{cu}:{cu + 1}], 0", SALU, rd=sr(cu, 2), wr=[("scc", 0)]),
+                    I(f"s_cbranch_scc1 {lf}", BRANCH),
+                    I(f"s_load_dwordx2 s[{off[0]}:{off[1]}], s[{cu}:{cu + 1}], s{T1}", SMEM, rd=sr(cu, 2) + sr(T1), wr=sr(off[0], 2)),
+                    label(lf)]
+        ins += [I("s_waitcnt lgkmcnt(0)", WAIT)]
         for cu, bstride, rstride, off, seq in parts:
             lf, ld = self.lab("fixed"), self.lab("vdone")
             ins += [I(f"s_cmp_eq_u64 s[{cu}:{cu + 1}], 0", SALU, rd=sr(cu, 2), wr=[("scc", 0)]),
-                    I(f"s_cbranch_scc1 {lf}", BRANCH),
-                    I(f"s_lshl_b32 s{T1}, s{BIDB}, 2", SALU, rd=sr(BIDB), wr=sr(T1)),
-                    I(f"s_load_dwordx2 s[{off[0]}:{off[1]}], s[{cu}:{cu + 1}], s{T1}", SMEM, rd=sr(cu, 2) + sr(T1), wr=sr(off[0], 2)),
-                    I("s_waitcnt lgkmcnt(0)", WAIT)]
+                    I(f"s_cbranch_scc1 {lf}", BRANCH)]
             if seq is not None:
                 ins += [I(f"s_sub_u32 s{seq}, s{off[1]}, s{off[0]}", SALU, rd=sr(off[0], 2), wr=sr(seq))]
             ins += [I(f"s_bitcmp1_b32 s{A['FL']}, 0", SALU, rd=sr(A["FL"]), wr=[("scc", 0)]),
