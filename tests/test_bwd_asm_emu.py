@@ -263,3 +263,36 @@ def test_asm_dkdv_d64_varlen_in_emulator(asm64_text):
     ek, ev, *_ = emu_bwd.run(lens=[130, 0, 1, 557], h=2, hk=1, causal=True, text=asm64_text, verbose=False, ver=64)
     assert not emu_bwd.RACES, emu_bwd.RACES[:3]
     assert max(ek, ev) < 1e-2
+
+
+# ------------------------------------------------------------------------------------------------
+# head dim 64 dQ (csrc/asm/gen_dq64.py: gen_dq.py's kernel at d = 64, one K and one V DMA piece a
+# wave per subtile), against the float64 dQ of tools/emu_dq.py
+# ------------------------------------------------------------------------------------------------
+@pytest.fixture(scope="module")
+def dq64_text():
+    import emu_dq
+    return emu_dq.asm_text(64)
+
+
+@pytest.mark.timeout(900)
+@pytest.mark.parametrize("b,sq,sk,h,hk,causal,bf16,grid,fused,qfold", [
+    (1, 64, 64, 1, 1, True, True, None, False, False),         # one step: first + last + masked
+    (1, 330, 200, 2, 1, True, True, None, False, False),       # GQA, sq > sk
+    (2, 130, 77, 2, 1, False, True, None, False, False),       # full attention, ragged
+    (1, 96, 300, 3, 1, True, False, None, True, False),        # fp16, fused D (v_dot2 over 16 registers)
+    (1, 330, 200, 2, 1, True, True, None, True, True),         # the Q fold (Q' stored bitwise)
+    (1, 600, 600, 2, 1, True, True, 2, True, True),            # persistent loop, fold state per item
+])
+def test_asm_dq_d64_in_emulator(dq64_text, b, sq, sk, h, hk, causal, bf16, grid, fused, qfold):
+    import emu_dq
+    e, *_ = emu_dq.run(b, sq, sk, h, hk, causal, bf16, seed=5, text=dq64_text, verbose=False, grid=grid,
+                       fused=fused, qfold=qfold, d=64)
+    assert e <= (1e-2 if bf16 else 2e-3), e
+
+
+def test_generated_dq64_kernels_assemble_shape():
+    text = subprocess.run([sys.executable, os.path.join(ROOT, "xhy-flash-attention_amd", "csrc", "asm", "gen_dq64.py")],
+                          check=True, capture_output=True, text=True).stdout
+    assert text.count(".amdhsa_kernel fa_bwd_dq_asm_d64_") == 4
+    assert ".amdhsa_group_segment_fixed_size 73728" in text

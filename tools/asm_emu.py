@@ -19,6 +19,7 @@ Lane layouts modelled (the ones the HIP kernels rely on, fa_common.h):
     whose [offset, offset + size) leaves [0, num_records) reads 0 / is dropped; `lds` loads write
     16 bytes per lane at M0 + 16 lane.
 """
+import os
 import re
 import struct
 
@@ -117,9 +118,17 @@ def parse_kernel(text, name):
     return insts, labels
 
 
+# FA_EMU_POISON=1: registers start as fp32 NaN and LDS as 0xff bytes (bf16 / f16 NaN) instead of
+# zero -- a kernel that reads a register or LDS byte it never wrote then shows NaN in its outputs, as
+# it may on the GPU, where that state is whatever the previous wave left
+POISON = os.environ.get("FA_EMU_POISON") == "1"
+
+
 class Wave:
     def __init__(self, wid, nregs=512):
         self.r = np.zeros((nregs, 64), dtype=np.uint32)   # v0..v255, a0..a255 at 256..511
+        if POISON:
+            self.r[:] = 0x7fc00000
         self.s = np.zeros(128, dtype=np.uint32)
         self.vcc = np.zeros(64, dtype=bool)
         self.scc = False
@@ -284,7 +293,7 @@ class Emu:
     def run_wg(self, wg_id, kernarg_addr, nwaves=4, order=None):
         """order: the waves' order between two barriers (None: 0 first; "reverse": the last first --
         a read of data another wave writes in the same barrier interval then sees the other version)"""
-        lds = np.zeros(LDS_SIZE, dtype=np.uint8)
+        lds = np.full(LDS_SIZE, 0xff if POISON else 0, dtype=np.uint8)
         waves = [Wave(i) for i in range(nwaves)]
         for w in waves:
             w.s[0] = kernarg_addr & 0xFFFFFFFF

@@ -20,12 +20,12 @@ sys.path.insert(0, os.path.join(ROOT, "xhy-flash-attention_amd", "csrc", "asm"))
 from isa import fwd_item_decode  # noqa: E402
 
 GEN = os.path.join(ROOT, "xhy-flash-attention_amd", "csrc", "asm", "gen_dq.py")
-D = 128
+GEN64 = os.path.join(ROOT, "xhy-flash-attention_amd", "csrc", "asm", "gen_dq64.py")
 BM = 256
 
 
-def asm_text():
-    return subprocess.run([sys.executable, GEN], check=True, capture_output=True, text=True).stdout
+def asm_text(d=128):
+    return subprocess.run([sys.executable, GEN64 if d == 64 else GEN], check=True, capture_output=True, text=True).stdout
 
 
 def pack_args(**kw):
@@ -71,14 +71,16 @@ def reference_dq(q, k, v, do, causal, scale, o=None):
 
 
 def run(b=1, sq=300, sk=300, h=2, hk=1, causal=True, bf16=True, seed=0, text=None, verbose=True, hp=0, grid=None,
-        fused=False, wgs=None, qfold=False):
+        fused=False, wgs=None, qfold=False, d=128):
     """hp: heads per XCD group of the work order (0: head-fastest); grid: workgroups of the
     persistent item loop (default: one per item); fused: the kernel computes D = rowsum(dO o O) itself
     (flags bit 1, bwd_pre fused): the D input is garbage, softmax_d and the dK/dV scratch
     [-LSE / scale | -D] are checked against float64 (the error returned is the max of the three);
     qfold (with fused): the Q fold (flags bit 2) -- the kernel rewrites Q as bf16/f16(c Q), stores it
     (checked bitwise against the forward's rounding) and runs with c = 1, scale ln 2 on the chain
-    starts, dQ scaled by the softmax scale, against a float64 reference on that Q'"""
+    starts, dQ scaled by the softmax scale, against a float64 reference on that Q'; d: head dim
+    (128: gen_dq.py, 64: gen_dq64.py)"""
+    D = d
     rng = np.random.default_rng(seed)
     q = rng.standard_normal((b, sq, h, D)).astype(np.float32)
     k = rng.standard_normal((b, sk, hk, D)).astype(np.float32)
@@ -133,8 +135,8 @@ def run(b=1, sq=300, sk=300, h=2, hk=1, causal=True, bf16=True, seed=0, text=Non
         kw.update(qf=aqf, qf_batch=sq * h * D * 2, qf_row=h * D * 2, qf_head=D * 2, qc=float(qc32), c=1.0,
                   flags=2 | 4)
     akarg = heap.put(np.frombuffer(pack_args(**kw), dtype=np.uint8))
-    text = text or asm_text()
-    name = f"fa_bwd_dq_asm_d128_{'bf16' if bf16 else 'f16'}_{'causal' if causal else 'full'}"
+    text = text or asm_text(D)
+    name = f"fa_bwd_dq_asm_d{D}_{'bf16' if bf16 else 'f16'}_{'causal' if causal else 'full'}"
     emu = Emu(text, name, heap)
     for L in range(grid or n_items) if wgs is None else wgs:
         emu.run_wg(L, akarg)
@@ -178,5 +180,7 @@ if __name__ == "__main__":
     ap.add_argument("--fp16", action="store_true")
     ap.add_argument("--seed", type=int, default=0)
     ap.add_argument("--fused", action="store_true", help="the kernel computes D (bwd_pre fused)")
+    ap.add_argument("--qfold", action="store_true", help="with --fused: the Q fold")
+    ap.add_argument("--d", type=int, default=128)
     a = ap.parse_args()
-    run(a.b, a.sq, a.sk, a.h, a.hk, not a.full, not a.fp16, a.seed, fused=a.fused)
+    run(a.b, a.sq, a.sk, a.h, a.hk, not a.full, not a.fp16, a.seed, fused=a.fused or a.qfold, qfold=a.qfold, d=a.d)

@@ -53,9 +53,10 @@ NS = 9
 RING = NS * SLOT        # 147456
 LDS_BYTES = RING
 KQ = 6                  # K / V subtile s is DMA'd in step (s - KQ) / 2
+PIECES = 4              # 1-KiB LDS-DMA pieces a wave issues per subtile (K halves 0 / 1, V halves 0 / 1)
 # the end of step n-1 waits for the rows of subtiles <= 2n+3 (step n reads them, its last phase
 # prefetching the first fragments of 2n+3); younger than K/V(2n+3) (issued in step n-2): the 8 of step n-1
-VMCNT_STEP = 8
+VMCNT_STEP = 2 * PIECES
 
 OPT_WIN = int(os.environ.get("FA_GDQ_WIN", "16"))
 # (a read more than 16 MFMAs ahead would overwrite the ring slot (16 fragments) an earlier MFMA
@@ -139,7 +140,7 @@ class K:
         self.bf16 = bf16
         self.causal = causal
         self.ty = "bf16" if bf16 else "f16"
-        self.name = f"fa_bwd_dq_asm_d{D}_{self.ty}_{'causal' if causal else 'full'}"
+        self.name = f"fa_bwd_dq_asm_d{D}_{self.ty}_{'causal' if causal else 'full'}"   # (D: 128, or 64 via gen_dq64.py)
         self.uid = 0
 
     def lab(self, s):
@@ -157,12 +158,14 @@ class K:
         return Inst(t, MFMA, rd=rd, wr=d, rd_c=[] if first else d)
 
     def phase_frags(self, sdp, dq):
-        """the A fragments of a phase in MFMA order: (kind, index)"""
+        """the A fragments of a phase in MFMA order: (kind, index) -- KS k-steps of S^T and of dP^T,
+        2 NP (d-tile, key half) fragments of dQ^T: 8 each at d = 128, 4 at d = 64"""
+        assert KS == 2 * NP
         if sdp and dq:
-            return [(t, i) for i in range(8) for t in ("S", "dQ", "dP")]
+            return [(t, i) for i in range(KS) for t in ("S", "dQ", "dP")]
         if sdp:
-            return [(t, i) for i in range(8) for t in ("S", "dP")]
-        return [("dQ", i) for i in range(8)]
+            return [(t, i) for i in range(KS) for t in ("S", "dP")]
+        return [("dQ", i) for i in range(KS)]
 
     def phase_mfmas(self, par, sdp, dq):
         """MFMA list (two per fragment: q-blocks a, b) and the fragment list; par = parity of the VALU
@@ -236,8 +239,11 @@ class K:
         t = S_TMP
         I = Inst
         ops = [I(f"s_add_u32 s{t}, s{S_SDMA}, s{S_W2K}", SALU, rd=sr(S_SDMA) + sr(S_W2K), wr=sr(t) + [("scc", 0)], key=key)]
-        for jx, (voff, desc, add) in enumerate(((V_KV0, S_KD, 0), (V_KV1, S_KD, 1024), (V_KV0, S_VD, KT),
-                                                (V_KV1, S_VD, KT + 1024))):
+        # d = 128: the wave's 64-byte panel of both 16-row halves of K and of V; d = 64 (two panels):
+        # one piece of K and one of V (panel w & 1, rows 16 (w >> 1): S_W2K and V_KV0 say which)
+        pieces = (((V_KV0, S_KD, 0), (V_KV1, S_KD, 1024), (V_KV0, S_VD, KT), (V_KV1, S_VD, KT + 1024))
+                  if PIECES == 4 else ((V_KV0, S_KD, 0), (V_KV0, S_VD, KT)))
+        for jx, (voff, desc, add) in enumerate(pieces):
             e = None if eg is None else eg + 2 * jx
             ops.append(I(f"s_add_u32 m0, s{t}, {add}", SALU, rd=sr(t), wr=[("m0", 0), ("scc", 0)], key=key, earliest=e))
             ops.append(I(f"buffer_load_dwordx4 v{voff}, s[{desc}:{desc + 3}], 0 offen lds", DMA,
@@ -584,13 +590,21 @@ class K:
                 I(f"v_add_u32_e32 v{x + 5}, 2, v{hh}", VALU, rd=vr(hh), wr=vr(x + 5)),
                 I(f"v_xor_b32_e32 v{x + 5}, v{x + 3}, v{x + 5}", VALU, rd=vr(x + 3) + vr(x + 5), wr=vr(x + 5)),
                 I(f"v_lshl_add_u32 v{V_TB1}, v{x + 5}, 4, v{x + 4}", VALU, rd=vr(x + 5) + vr(x + 4), wr=vr(V_TB1))]
-        # DMA voffsets: wave w, half f: row = 16 f + lane / 4, col = 64 w + 16 ((lane & 3) ^ ((lane >> 4) & 3))
-        ins += [I(f"v_lshrrev_b32_e32 v{x}, 2, v{V_LANE}", VALU, rd=vr(V_LANE), wr=vr(x)),
+        # DMA voffsets: wave w, half f: row = 16 f + lane / 4, col = 64 w + 16 ((lane & 3) ^ ((lane >> 4) & 3));
+        # d = 64: row = 16 (w >> 1) + lane / 4, col = 64 (w & 1) + 16 (...)
+        ins += [I(f"v_lshrrev_b32_e32 v{x}, 2, v{V_LANE}", VALU, rd=vr(V_LANE), wr=vr(x))]
+        if PIECES == 2:
+            ins += [I(f"s_lshr_b32 s{T[0]}, s{S_WAVE}, 1", SALU, rd=sr(S_WAVE), wr=sr(T[0])),
+                    I(f"s_lshl_b32 s{T[0]}, s{T[0]}, 4", SALU, rd=sr(T[0]), wr=sr(T[0])),
+                    I(f"v_add_u32_e32 v{x}, s{T[0]}, v{x}", VALU, rd=sr(T[0]) + vr(x), wr=vr(x))]
+        ins += [
                 I(f"v_bfe_u32 v{x + 1}, v{V_LANE}, 4, 2", VALU, rd=vr(V_LANE), wr=vr(x + 1)),
                 I(f"v_and_b32_e32 v{x + 2}, 3, v{V_LANE}", VALU, rd=vr(V_LANE), wr=vr(x + 2)),
                 I(f"v_xor_b32_e32 v{x + 1}, v{x + 1}, v{x + 2}", VALU, rd=vr(x + 1, 2), wr=vr(x + 1)),
                 I(f"v_lshlrev_b32_e32 v{x + 1}, 4, v{x + 1}", VALU, rd=vr(x + 1), wr=vr(x + 1)),
-                I(f"s_lshl_b32 s{T[0]}, s{S_WAVE}, 6", SALU, rd=sr(S_WAVE), wr=sr(T[0])),
+                (I(f"s_lshl_b32 s{T[0]}, s{S_WAVE}, 6", SALU, rd=sr(S_WAVE), wr=sr(T[0])) if PIECES == 4 else
+                 I(f"s_and_b32 s{T[0]}, s{S_WAVE}, 1", SALU, rd=sr(S_WAVE), wr=sr(T[0]))),
+                ] + ([] if PIECES == 4 else [I(f"s_lshl_b32 s{T[0]}, s{T[0]}, 6", SALU, rd=sr(T[0]), wr=sr(T[0]))]) + [
                 I(f"v_add_u32_e32 v{x + 1}, s{T[0]}, v{x + 1}", VALU, rd=sr(T[0]) + vr(x + 1), wr=vr(x + 1)),
                 I(f"v_mul_lo_u32 v{V_KV0}, v{x}, s{Rkv}", VALU, rd=vr(x) + sr(Rkv), wr=vr(V_KV0)),
                 I(f"v_add_u32_e32 v{V_KV0}, v{V_KV0}, v{x + 1}", VALU, rd=vr(V_KV0) + vr(x + 1), wr=vr(V_KV0)),
@@ -598,7 +612,15 @@ class K:
                 I(f"v_add_u32_e32 v{V_KV1}, s{T[0]}, v{V_KV0}", VALU, rd=sr(T[0]) + vr(V_KV0), wr=vr(V_KV1)),
                 I(f"v_mov_b32_e32 v{V_NINF}, 0xff800000", VALU, wr=vr(V_NINF))]
         # ---- loop state ----
-        ins += [I(f"s_lshl_b32 s{S_W2K}, s{S_WAVE}, 11", SALU, rd=sr(S_WAVE), wr=sr(S_W2K)),
+        if PIECES == 4:     # this wave's LDS panel: 2048 w
+            ins += [I(f"s_lshl_b32 s{S_W2K}, s{S_WAVE}, 11", SALU, rd=sr(S_WAVE), wr=sr(S_W2K))]
+        else:               # d = 64: panel w & 1, rows 16 (w >> 1) -> 2048 (w & 1) + 1024 (w >> 1)
+            ins += [I(f"s_and_b32 s{T[0]}, s{S_WAVE}, 1", SALU, rd=sr(S_WAVE), wr=sr(T[0])),
+                    I(f"s_lshl_b32 s{T[0]}, s{T[0]}, 11", SALU, rd=sr(T[0]), wr=sr(T[0])),
+                    I(f"s_lshr_b32 s{T[1]}, s{S_WAVE}, 1", SALU, rd=sr(S_WAVE), wr=sr(T[1])),
+                    I(f"s_lshl_b32 s{T[1]}, s{T[1]}, 10", SALU, rd=sr(T[1]), wr=sr(T[1])),
+                    I(f"s_add_u32 s{S_W2K}, s{T[0]}, s{T[1]}", SALU, rd=sr(T[0]) + sr(T[1]), wr=sr(S_W2K))]
+        ins += [
                 I(f"s_mov_b32 s{S_SDMA}, 0", SALU, wr=sr(S_SDMA)),
                 I(f"s_mov_b32 s{S_NLAST}, s{T[8]}", SALU, rd=sr(T[8]), wr=sr(S_NLAST)),
                 I(f"s_mov_b32 s{S_MASK0}, s{T[3]}", SALU, rd=sr(T[3]), wr=sr(S_MASK0)),
@@ -633,7 +655,7 @@ class K:
         for j in range(2):
             acc = V_D[j]
             ins.append(I(f"v_mov_b32_e32 v{acc}, 0", VALU, wr=vr(acc)))
-            for i in range(32):
+            for i in range(4 * KS):
                 ins.append(I(f"{dot} v{acc}, v{64 + 32 * j + i}, v{32 * j + i}, v{acc}", VALU,
                              rd=vr(64 + 32 * j + i) + vr(32 * j + i) + vr(acc), wr=vr(acc)))
             # the other lane half holds the row's other 64 columns (a v_dot result read by another
@@ -797,8 +819,8 @@ class K:
         pro = head + self.prologue()
         for _ in range(KQ):
             pro += self.dma_subtile()
-        # K / V(0) and (1) landed (phase -1 reads 0, its tail prefetches 1): 16 younger DMAs
-        pro += [Inst("s_waitcnt vmcnt(16)", WAIT), Inst("s_barrier", BARRIER)]
+        # K / V(0) and (1) landed (phase -1 reads 0, its tail prefetches 1): 16 younger DMAs (d = 64: 8)
+        pro += [Inst(f"s_waitcnt vmcnt({(KQ - 2) * PIECES})", WAIT), Inst("s_barrier", BARRIER)]
         pro += self.fused_d()
         # no keys: epilogue (dQ = 0), after the fused D (softmax_d and the scratch are still written)
         pro += [Inst(f"s_cmp_lt_i32 s{S_NLAST}, 0", SALU, rd=sr(S_NLAST), wr=[("scc", 0)]),

@@ -1147,7 +1147,7 @@ static void run_bwd(const BwdParams& p, hipStream_t stream) {
   auto dq = [&](hipStream_t st) {
     dim3 grid(p.s.b * p.s.h * ((p.s.seqlen_q + DqTile<D>::BM - 1) / DqTile<D>::BM));
     prof_begin(kTimeBwdDq, st);
-    if (D == 128 && !DROPOUT && !masked && dq_asm_applicable(p, p.fuse_pre)) {   // the assembly dQ kernel (fa_bwd_asm.cpp)
+    if ((D == 128 || D == 64) && !DROPOUT && !masked && dq_asm_applicable(p, p.fuse_pre)) {   // the assembly dQ kernel (fa_bwd_asm.cpp)
       BwdParams pa = p;   // (persistent: heads grouped per XCD as in the forward, knob 7)
       if (p.s.cu_seqlens_q == nullptr)
         pa.dq_head_group = xcd_head_group((long long)p.s.b * p.s.h, (p.s.seqlen_q + 255) / 256,
@@ -1315,7 +1315,7 @@ void launch_bwd(const BwdParams& p_in, bool is_bf16, hipStream_t stream) {
   }
   // knob 8: the assembly dQ kernel computes D itself and writes softmax_d and the dK/dV scratch
   // (with the fold the dQ kernel also stores Q' in the compact rows: their 256-row records must fit)
-  p.fuse_pre = asm_dkdv && knob(kKnobFusePre) != 0 && p.s.d == 128 && !p.s.dropout && p.s.mask == nullptr &&
+  p.fuse_pre = asm_dkdv && knob(kKnobFusePre) != 0 && (p.s.d == 128 || p.s.d == 64) && !p.s.dropout && p.s.mask == nullptr &&
                p.s.fm_lts == nullptr && dq_asm_applicable(p, true) && (!fold || dq_asm_applicable(pq, false));
   StreamScratch qfold;
   if (fold) {

@@ -6,8 +6,9 @@
 // or varlen, MHA / GQA (reduced in-kernel over the group, or expanded per query head), no dropout /
 // mask / FlashMask.  Head dim 64 has its own dK / dV kernels (round 6, gen_bwd64.py: 4 waves x 64
 // keys, each A fragment feeding both 32-key groups' MFMAs, 256-key blocks; C2-class / d64 dK/dV
-// -33 to -41 % against bwd_dkdv_kernel, profiles/r06/ab_d64_*_r06g.txt); its dQ stays on the HIP
-// kernel.  It replaces bwd_dkdv_kernel for those calls; bwd_pre_kernel then writes the
+// -33 to -41 % against bwd_dkdv_kernel, profiles/r06/ab_d64_*_r06g.txt), and so does dQ (gen_dq64.py:
+// gen_dq.py's kernel at d = 64, 24 MFMAs a phase, one K and one V DMA piece a wave per subtile).
+// It replaces bwd_dkdv_kernel for those calls; bwd_pre_kernel then writes the
 // per-row chain starts it streams (-LSE / scale and -D, 32 rows per 256-byte group: the "lsed"
 // scratch), and the dQ kernel is unchanged.  Everything else -- and this path when it is switched
 // off (FLASH_ATTN_MI355X_BWD_ASM=0 or knob 3) -- runs bwd_dkdv_kernel (fa_bwd.hip).
@@ -36,6 +37,8 @@ extern "C" const unsigned char fa_bwd_asm_co[];
 extern "C" const unsigned long fa_bwd_asm_co_size;
 extern "C" const unsigned char fa_dq_asm_co[];
 extern "C" const unsigned long fa_dq_asm_co_size;
+extern "C" const unsigned char fa_dq64_asm_co[];
+extern "C" const unsigned long fa_dq64_asm_co_size;
 extern "C" const unsigned char fa_bwd2_asm_co[];
 extern "C" const unsigned long fa_bwd2_asm_co_size;
 extern "C" const unsigned char fa_bwd64_asm_co[];
@@ -95,11 +98,12 @@ constexpr int kBkn = 128;   // keys per workgroup (head dim 128)
 constexpr int kBkn64 = 256; // head dim 64: 4 waves x 64 keys (gen_bwd64.py)
 int bkn_of(int d) { return d == 64 ? kBkn64 : kBkn; }
 struct DevModule {
-  hipModule_t mod = nullptr, mod_dq = nullptr, mod2 = nullptr, mod64 = nullptr;
+  hipModule_t mod = nullptr, mod_dq = nullptr, mod2 = nullptr, mod64 = nullptr, mod_dq64 = nullptr;
   hipFunction_t fn64[8] = {};    // head dim 64, the order of fn
   hipFunction_t fn[8] = {};      // dK/dV [bf16 causal, bf16 full, f16 causal, f16 full], then the same with c = 1
   hipFunction_t fn2[8] = {};     // the same, two waves per SIMD (gen_bwd2.py, 512 threads)
   hipFunction_t fn_dq[4] = {};   // dQ, the same order
+  hipFunction_t fn_dq64[4] = {}; // dQ, head dim 64 (gen_dq64.py)
   int cus = 0;
 };
 std::mutex g_mu;
@@ -121,6 +125,8 @@ const char* kNames64[8] = {"fa_bwd_dkdv_asm_d64_bf16_causal", "fa_bwd_dkdv_asm_d
                            "fa_bwd_dkdv_asm_d64_f16_causal_c1", "fa_bwd_dkdv_asm_d64_f16_full_c1"};
 const char* kDqNames[4] = {"fa_bwd_dq_asm_d128_bf16_causal", "fa_bwd_dq_asm_d128_bf16_full",
                            "fa_bwd_dq_asm_d128_f16_causal", "fa_bwd_dq_asm_d128_f16_full"};
+const char* kDq64Names[4] = {"fa_bwd_dq_asm_d64_bf16_causal", "fa_bwd_dq_asm_d64_bf16_full",
+                             "fa_bwd_dq_asm_d64_f16_causal", "fa_bwd_dq_asm_d64_f16_full"};
 
 void check(hipError_t e, const char* what) {
   if (e != hipSuccess) throw std::runtime_error(std::string("flash_attn_bwd (asm dK/dV): ") + what + ": " + hipGetErrorString(e));
@@ -134,6 +140,8 @@ DevModule& module_for(int dev) {
     for (int i = 0; i < 8; ++i) check(hipModuleGetFunction(&m.fn[i], m.mod, kNames[i]), kNames[i]);
     check(hipModuleLoadData(&m.mod_dq, fa_dq_asm_co), "hipModuleLoadData (dQ)");
     for (int i = 0; i < 4; ++i) check(hipModuleGetFunction(&m.fn_dq[i], m.mod_dq, kDqNames[i]), kDqNames[i]);
+    check(hipModuleLoadData(&m.mod_dq64, fa_dq64_asm_co), "hipModuleLoadData (dQ, head dim 64)");
+    for (int i = 0; i < 4; ++i) check(hipModuleGetFunction(&m.fn_dq64[i], m.mod_dq64, kDq64Names[i]), kDq64Names[i]);
     check(hipModuleLoadData(&m.mod2, fa_bwd2_asm_co), "hipModuleLoadData (dK/dV, two waves per SIMD)");
     for (int i = 0; i < 8; ++i) check(hipModuleGetFunction(&m.fn2[i], m.mod2, kNames2[i]), kNames2[i]);
     check(hipModuleLoadData(&m.mod64, fa_bwd64_asm_co), "hipModuleLoadData (dK/dV, head dim 64)");
@@ -251,7 +259,7 @@ void launch_bwd_dkdv_asm(const BwdParams& p, bool is_bf16, hipStream_t stream) {
 bool dq_asm_applicable(const BwdParams& p, bool fused) {
   const AttnShape& s = p.s;
   if (knob(kKnobDqAsm) == 0) return false;
-  if (s.d != 128 || s.dropout || s.mask != nullptr || s.fm_lts != nullptr) return false;
+  if ((s.d != 128 && s.d != 64) || s.dropout || s.mask != nullptr || s.fm_lts != nullptr) return false;
   if (s.hk <= 0 || s.h % s.hk != 0 || s.b > 65535 || s.h > 65535) return false;
   if (p.k_row != p.v_row || p.k_batch != p.v_batch) return false;   // K / V share the DMA offsets
   const int nmb = (s.seqlen_q + 255) / 256;
@@ -277,7 +285,7 @@ void launch_bwd_dq_asm(const BwdParams& p, bool is_bf16, hipStream_t stream) {
   {
     std::lock_guard<std::mutex> lk(g_mu);
     DevModule& m = module_for(dev);
-    fn = m.fn_dq[(is_bf16 ? 0 : 2) + (s.causal ? 0 : 1)];
+    fn = (s.d == 64 ? m.fn_dq64 : m.fn_dq)[(is_bf16 ? 0 : 2) + (s.causal ? 0 : 1)];
     cus = m.cus;
   }
   // persistent grid (knob 6): one workgroup per CU walking the item list in snake order (fixed
