@@ -13,6 +13,7 @@ import os
 import subprocess
 import sys
 
+import numpy as np
 import pytest
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
@@ -296,3 +297,16 @@ def test_generated_dq64_kernels_assemble_shape():
                           check=True, capture_output=True, text=True).stdout
     assert text.count(".amdhsa_kernel fa_bwd_dq_asm_d64_") == 4
     assert ".amdhsa_group_segment_fixed_size 73728" in text
+
+
+@pytest.mark.timeout(900)
+@pytest.mark.parametrize("d,sq,sk,causal", [(64, 1, 1, False), (128, 17, 17, False), (64, 130, 77, True)])
+def test_asm_dq_fp16_large_scores(d, sq, sk, causal):
+    """fp16, |LSE| large (Q x 5, K / V x 3): the keys past seqlen_k in the last step (zero K / V)
+    must get P = 0, or P dS overflows the fp16 dS pack and 0 x inf puts NaN into dQ (found on the GPU
+    by test_flash_attn_bwd_overflow at d = 64)"""
+    import emu_dq
+    _, dq, ref = emu_dq.run(2, sq, sk, 2, 2, causal, False, seed=1, verbose=False, d=d, qmul=5, kmul=3,
+                            text=emu_dq.asm_text(d))
+    assert np.isfinite(dq).all()
+    assert np.abs(dq - ref).max() <= 2e-3 * max(1.0, np.abs(ref).max())

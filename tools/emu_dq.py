@@ -71,7 +71,7 @@ def reference_dq(q, k, v, do, causal, scale, o=None):
 
 
 def run(b=1, sq=300, sk=300, h=2, hk=1, causal=True, bf16=True, seed=0, text=None, verbose=True, hp=0, grid=None,
-        fused=False, wgs=None, qfold=False, d=128):
+        fused=False, wgs=None, qfold=False, d=128, qmul=1.0, kmul=1.0):
     """hp: heads per XCD group of the work order (0: head-fastest); grid: workgroups of the
     persistent item loop (default: one per item); fused: the kernel computes D = rowsum(dO o O) itself
     (flags bit 1, bwd_pre fused): the D input is garbage, softmax_d and the dK/dV scratch
@@ -79,12 +79,13 @@ def run(b=1, sq=300, sk=300, h=2, hk=1, causal=True, bf16=True, seed=0, text=Non
     qfold (with fused): the Q fold (flags bit 2) -- the kernel rewrites Q as bf16/f16(c Q), stores it
     (checked bitwise against the forward's rounding) and runs with c = 1, scale ln 2 on the chain
     starts, dQ scaled by the softmax scale, against a float64 reference on that Q'; d: head dim
-    (128: gen_dq.py, 64: gen_dq64.py)"""
+    (128: gen_dq.py, 64: gen_dq64.py); qmul / kmul scale Q and K / V (large |LSE|: the fp16 overflow
+    cases)"""
     D = d
     rng = np.random.default_rng(seed)
-    q = rng.standard_normal((b, sq, h, D)).astype(np.float32)
-    k = rng.standard_normal((b, sk, hk, D)).astype(np.float32)
-    v = rng.standard_normal((b, sk, hk, D)).astype(np.float32)
+    q = rng.standard_normal((b, sq, h, D)).astype(np.float32) * np.float32(qmul)
+    k = rng.standard_normal((b, sk, hk, D)).astype(np.float32) * np.float32(kmul)
+    v = rng.standard_normal((b, sk, hk, D)).astype(np.float32) * np.float32(kmul)
     do = rng.standard_normal((b, sq, h, D)).astype(np.float32)
     enc, dec = (f32_to_bf16, bf16_to_f32) if bf16 else (f32_to_f16, f16_to_f32)
     q16, k16, v16, do16 = (enc(x).astype(np.uint16) for x in (q, k, v, do))

@@ -103,7 +103,7 @@ V_KB0, V_KB1, V_VB0, V_VB1 = 228, 229, 230, 231
 V_KV0, V_KV1 = 232, 233        # DMA voffsets (K and V share them: k_row == v_row), halves 0 / 1
 V_NLC = (234, 235)             # -log2e LSE per q-block
 V_D = (236, 237)               # D per q-block
-V_LIM = (238, 239)             # causal mask limit base per q-block: q - 4 hh
+V_LIM = (238, 239)             # mask limit base per q-block: the row's last key - 4 hh
 V_LM = 240
 V_NINF = 241
 V_LANE = 242
@@ -451,11 +451,16 @@ class K:
         ins += [I(f"s_add_u32 s{T[0]}, s{NEND}, {2 * SUB - 1}", SALU, rd=sr(NEND), wr=sr(T[0])),
                 I(f"s_lshr_b32 s{T[0]}, s{T[0]}, 6", SALU, rd=sr(T[0]), wr=sr(T[0])),          # steps
                 I(f"s_sub_i32 s{T[8]}, s{T[0]}, 1", SALU, rd=sr(T[0]), wr=sr(T[8]))]           # last step
-        # first masked step (causal): the first subtile with keys past the block's first row: m0 / 64
+        # first masked step: causal, the first with keys past the block's first row (m0 / 64); and the
+        # step holding key seqlen_k, whose keys past it read zero K / V but would still get P > 0
+        # (exp2(-LSE log2 e)): with fp16 dS packs a P dS past 65504 turns into inf and 0 x inf into NaN
+        # in dQ^T += K^T dS^T, so the masked step zeroes them (sk / 64 > the last step when sk % 64 == 0)
         if self.causal:
             ins += [I(f"s_lshr_b32 s{T[3]}, s{M0R}, 6", SALU, rd=sr(M0R), wr=sr(T[3]))]
         else:
             ins += [I(f"s_mov_b32 s{T[3]}, 0x7fffffff", SALU, wr=sr(T[3]))]
+        ins += [I(f"s_lshr_b32 s{T[2]}, s{SK}, 6", SALU, rd=sr(SK), wr=sr(T[2])),
+                I(f"s_min_u32 s{T[3]}, s{T[3]}, s{T[2]}", SALU, rd=sr(T[3]) + sr(T[2]), wr=sr(T[3]))]
         # ---- per-lane values: rows, LSE / D, offsets ----
         r_, hh = V_TMP, V_TMP + 1
         x = V_TMP + 2
@@ -477,6 +482,7 @@ class K:
                     I(f"s_lshl_b32 s{dd + 2}, s{NROW}, 2", SALU, rd=sr(NROW), wr=sr(dd + 2)),
                     I(f"s_mov_b32 s{dd + 3}, 0x20000", SALU, wr=sr(dd + 3))]
         # rows of the wave: 64 w + 32 j + r
+        ins += [I(f"s_sub_i32 s{T[2]}, s{SK}, 1", SALU, rd=sr(SK), wr=sr(T[2]))]        # the last key
         for j in range(2):
             ins += [I(f"v_lshl_add_u32 v{x}, v1, 6, v{r_}", VALU, rd=vr(1) + vr(r_), wr=vr(x)),
                     I(f"v_add_u32_e32 v{x}, {32 * j}, v{x}", VALU, rd=vr(x), wr=vr(x)),
@@ -490,8 +496,11 @@ class K:
                     I(f"v_lshl_add_u32 v{V_QOFF[j]}, v{hh}, 4, v{V_QOFF[j]}", VALU, rd=vr(hh) + vr(V_QOFF[j]), wr=vr(V_QOFF[j])),
                     I(f"v_mul_lo_u32 v{V_OOFF[j]}, v{x}, s{Rdo}", VALU, rd=vr(x) + sr(Rdo), wr=vr(V_OOFF[j])),
                     I(f"v_lshl_add_u32 v{V_OOFF[j]}, v{hh}, 4, v{V_OOFF[j]}", VALU, rd=vr(hh) + vr(V_OOFF[j]), wr=vr(V_OOFF[j])),
-                    # causal mask limit base: q - 4 hh (q = m0 + row)
-                    I(f"v_add_u32_e32 v{V_LIM[j]}, s{M0R}, v{x}", VALU, rd=sr(M0R) + vr(x), wr=vr(V_LIM[j])),
+                    # mask limit base: the row's last key - 4 hh: min(q, sk - 1) causal (q = m0 + row), sk - 1 not
+                    (I(f"v_add_u32_e32 v{V_LIM[j]}, s{M0R}, v{x}", VALU, rd=sr(M0R) + vr(x), wr=vr(V_LIM[j])) if self.causal
+                     else I(f"v_mov_b32_e32 v{V_LIM[j]}, s{T[2]}", VALU, rd=sr(T[2]), wr=vr(V_LIM[j]))),
+                    ] + ([I(f"v_min_i32_e32 v{V_LIM[j]}, s{T[2]}, v{V_LIM[j]}", VALU, rd=sr(T[2]) + vr(V_LIM[j]), wr=vr(V_LIM[j]))]
+                         if self.causal else []) + [
                     I(f"v_lshlrev_b32_e32 v{x + 2}, 2, v{hh}", VALU, rd=vr(hh), wr=vr(x + 2)),
                     I(f"v_sub_u32_e32 v{V_LIM[j]}, v{V_LIM[j]}, v{x + 2}", VALU, rd=vr(V_LIM[j]) + vr(x + 2), wr=vr(V_LIM[j]))]
         # Q / dO fragments into AGPRs: lane holds row[16 ks + 8 hh .. +7]
@@ -835,7 +844,7 @@ class K:
         emit(self.q_fold_setup() + self.phase_m1(True), pre=[nop(15)])
         code.append(label(l_after))
         L = {}
-        variants = [(f, l, m) for f in (True, False) for l in (True, False) for m in ((True, False) if self.causal else (False,))]
+        variants = [(f, l, m) for f in (True, False) for l in (True, False) for m in (True, False)]
         for v in variants:
             L[v] = self.lab("step_" + ("".join(c for c, on in zip("FLM", v) if on) or "R"))
         l_tail = self.lab("tail")
@@ -845,20 +854,16 @@ class K:
         # entry: the first step (masked when causal and m0 == 0)
         code.append(label(l_first))
         code += [Inst(f"s_cmp_eq_u32 s{S_NLAST}, 0", SALU), Inst(f"s_cbranch_scc1 {l_first}_last", BRANCH)]
-        if self.causal:
-            code += [Inst(f"s_cmp_eq_u32 s{S_MASK0}, 0", SALU), Inst(f"s_cbranch_scc1 {L[(True, False, True)]}", BRANCH)]
+        code += [Inst(f"s_cmp_eq_u32 s{S_MASK0}, 0", SALU), Inst(f"s_cbranch_scc1 {L[(True, False, True)]}", BRANCH)]
         code += [Inst(f"s_branch {L[(True, False, False)]}", BRANCH), label(f"{l_first}_last")]
-        if self.causal:
-            code += [Inst(f"s_cmp_eq_u32 s{S_MASK0}, 0", SALU), Inst(f"s_cbranch_scc1 {L[(True, True, True)]}", BRANCH)]
+        code += [Inst(f"s_cmp_eq_u32 s{S_MASK0}, 0", SALU), Inst(f"s_cbranch_scc1 {L[(True, True, True)]}", BRANCH)]
         code += [Inst(f"s_branch {L[(True, True, False)]}", BRANCH)]
         # dispatch: done? last? masked (S_N >= S_MASK0)?
         code += [label(l_disp), Inst(f"s_cmp_gt_u32 s{S_N}, s{S_NLAST}", SALU), Inst(f"s_cbranch_scc1 {l_tail}", BRANCH),
                  Inst(f"s_cmp_lt_u32 s{S_N}, s{S_NLAST}", SALU), Inst(f"s_cbranch_scc1 {l_notlast}", BRANCH)]
-        if self.causal:
-            code += [Inst(f"s_cmp_ge_u32 s{S_N}, s{S_MASK0}", SALU), Inst(f"s_cbranch_scc1 {L[(False, True, True)]}", BRANCH)]
+        code += [Inst(f"s_cmp_ge_u32 s{S_N}, s{S_MASK0}", SALU), Inst(f"s_cbranch_scc1 {L[(False, True, True)]}", BRANCH)]
         code += [Inst(f"s_branch {L[(False, True, False)]}", BRANCH), label(l_notlast)]
-        if self.causal:
-            code += [Inst(f"s_cmp_ge_u32 s{S_N}, s{S_MASK0}", SALU), Inst(f"s_cbranch_scc1 {L[(False, False, True)]}", BRANCH)]
+        code += [Inst(f"s_cmp_ge_u32 s{S_N}, s{S_MASK0}", SALU), Inst(f"s_cbranch_scc1 {L[(False, False, True)]}", BRANCH)]
         code += [Inst(f"s_branch {L[(False, False, False)]}", BRANCH)]
         pad = [nop(15)]
         for v in variants:
