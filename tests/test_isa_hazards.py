@@ -196,7 +196,7 @@ def test_shipped_assembly_kernels_hazard_free():
     assert len([n for n in names if n.startswith("fa_bwd_dkdv_asm_d128")]) == 8, names   # (+ the c = 1 kernels)
     assert len([n for n in names if n.startswith("fa_bwd_dkdv_asm_d64")]) == 8, names    # head dim 64
     assert len([n for n in names if n.startswith("fa_bwd_dq_asm_d128")]) == 4, names
-    assert len([n for n in names if n.startswith("fa_bwd_dq_asm_d64")]) == 4, names      # head dim 64
+    assert len([n for n in names if n.startswith("fa_bwd_dq_asm_d64")]) == 8, names      # head dim 64 (+ c = 1)
     assert len([n for n in names if n.startswith("fa_bwd2_dkdv_asm_")]) == 8, names  # two waves per SIMD
     for n, (count, bad) in res.items():
         assert count > 1000, (n, count)

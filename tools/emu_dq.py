@@ -137,7 +137,8 @@ def run(b=1, sq=300, sk=300, h=2, hk=1, causal=True, bf16=True, seed=0, text=Non
                   flags=2 | 4)
     akarg = heap.put(np.frombuffer(pack_args(**kw), dtype=np.uint8))
     text = text or asm_text(D)
-    name = f"fa_bwd_dq_asm_d{D}_{'bf16' if bf16 else 'f16'}_{'causal' if causal else 'full'}"
+    name = (f"fa_bwd_dq_asm_d{D}_{'bf16' if bf16 else 'f16'}_{'causal' if causal else 'full'}"
+            f"{'_c1' if D == 64 and kw['c'] == 1.0 else ''}")     # (d = 64: the c = 1 kernels, fa_bwd_asm.cpp)
     emu = Emu(text, name, heap)
     for L in range(grid or n_items) if wgs is None else wgs:
         emu.run_wg(L, akarg)

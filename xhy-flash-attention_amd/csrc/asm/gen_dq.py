@@ -92,10 +92,34 @@ def DSP(par, j):
 
 
 RG = 160
+# CHAIN_S / CHAIN_D: the S^T / dP^T chains start from per-row constant blocks instead of zero --
+# S' = S^T - LSE log2 e / c and dP' = dP^T - D -- so a score needs no v_fma before its exp (P =
+# exp2(c S'), exp2(S') on the c = 1 kernels) and no v_sub before its dS multiply (dS = P dP').  d = 64
+# (gen_dq64.py): both, the blocks in v[160:223] and the A-fragment ring in the AGPRs d = 64 leaves free
+# (a[32:63], a[96:127]); d = 128: CHAIN_D with the ring cut to 8 slots (v[160:191]), -D in v[192:223]
+CHAIN_S = False
+# (d = 128 A/B, profiles/r06/ab_c{3,5}_dqcd_r06k.txt: dQ -0.9 % at C3, -0.8 % at C5; FA_GDQ_CHAIN_D=0 is the
+# 16-slot ring without it)
+CHAIN_D = os.environ.get("FA_GDQ_CHAIN_D", "1") == "1"
+RING_FILE = "v"
+RING_SLOTS = 8 if CHAIN_D else 16
 
 
 def ring(f):
-    return RG + 4 * (f % 16)
+    if RING_FILE == "a":
+        s = f % 16
+        return (32 if s < 8 else 96) + 4 * (s % 8)
+    return RG + 4 * (f % RING_SLOTS)
+
+
+def NLCB(j):
+    """(CHAIN_S) 16 copies of the q-block's -LSE log2 e / c: the S^T chain start"""
+    return 160 + 16 * j
+
+
+def NDB(j):
+    """(CHAIN_D) 16 copies of the q-block's -D: the dP^T chain start"""
+    return 192 + 16 * j
 
 
 V_RB0, V_RB1, V_TB0, V_TB1 = 224, 225, 226, 227
@@ -136,11 +160,16 @@ NITEMS_OFF = 224  # n_items, grid (persistent item loop)
 
 
 class K:
-    def __init__(self, bf16, causal):
+    def __init__(self, bf16, causal, unit_c=False):
+        """unit_c (CHAIN_S only): for launches with c = 1 (the folded backward): P = exp2(S') with no
+        multiply"""
         self.bf16 = bf16
         self.causal = causal
+        self.unit_c = unit_c
+        assert CHAIN_S or not unit_c
         self.ty = "bf16" if bf16 else "f16"
-        self.name = f"fa_bwd_dq_asm_d{D}_{self.ty}_{'causal' if causal else 'full'}"   # (D: 128, or 64 via gen_dq64.py)
+        self.name = (f"fa_bwd_dq_asm_d{D}_{self.ty}_{'causal' if causal else 'full'}"   # (D: 128, or 64 via gen_dq64.py)
+                     f"{'_c1' if unit_c else ''}")
         self.uid = 0
 
     def lab(self, s):
@@ -148,14 +177,18 @@ class K:
         return f".L{self.name}_{s}_{self.uid}"
 
     # ------------------------------------------------------------------ MFMAs of a phase
-    def mf(self, dst, a, b, first=False):
+    def mf(self, dst, a, b, first=False, c_src=None):
+        """c_src: (file, register) of the chain's start block (its first MFMA reads C from there)"""
         dk, dr = dst
         regs = {"v": vr, "a": ar}
-        c = "0" if first else rtxt(dk, dr, 16)
-        t = (f"v_mfma_f32_32x32x16_{self.ty} {rtxt(dk, dr, 16)}, {rtxt(a[0], a[1], 4)}, {rtxt(b[0], b[1], 4)}, {c}")
         d = regs[dk](dr, 16)
-        rd = regs[a[0]](a[1], 4) + regs[b[0]](b[1], 4) + ([] if first else d)
-        return Inst(t, MFMA, rd=rd, wr=d, rd_c=[] if first else d)
+        if c_src is not None:
+            c, cr = rtxt(c_src[0], c_src[1], 16), regs[c_src[0]](c_src[1], 16)
+        else:
+            c, cr = ("0", []) if first else (rtxt(dk, dr, 16), d)
+        t = (f"v_mfma_f32_32x32x16_{self.ty} {rtxt(dk, dr, 16)}, {rtxt(a[0], a[1], 4)}, {rtxt(b[0], b[1], 4)}, {c}")
+        rd = regs[a[0]](a[1], 4) + regs[b[0]](b[1], 4) + cr
+        return Inst(t, MFMA, rd=rd, wr=d, rd_c=cr)
 
     def phase_frags(self, sdp, dq):
         """the A fragments of a phase in MFMA order: (kind, index) -- KS k-steps of S^T and of dP^T,
@@ -176,12 +209,14 @@ class K:
         for f, (t, i) in enumerate(frags):
             for j in range(2):
                 if t == "S":
-                    out.append(self.mf(("v", SB(nb, j)), ("v", ring(f)), ("a", QF(j, i)), first=(i == 0)))
+                    out.append(self.mf(("v", SB(nb, j)), (RING_FILE, ring(f)), ("a", QF(j, i)), first=(i == 0),
+                                       c_src=("v", NLCB(j)) if CHAIN_S and i == 0 else None))
                 elif t == "dP":
-                    out.append(self.mf(("v", DPB(nb, j)), ("v", ring(f)), ("a", OF(j, i)), first=(i == 0)))
+                    out.append(self.mf(("v", DPB(nb, j)), (RING_FILE, ring(f)), ("a", OF(j, i)), first=(i == 0),
+                                       c_src=("v", NDB(j)) if CHAIN_D and i == 0 else None))
                 else:
                     dt, kk = i // 2, i % 2
-                    out.append(self.mf(("a", DQ(j, dt)), ("v", ring(f)), ("v", DSP(nb, j) + 4 * kk)))
+                    out.append(self.mf(("a", DQ(j, dt)), (RING_FILE, ring(f)), ("v", DSP(nb, j) + 4 * kk)))
         return out, frags
 
     def frag_reads(self, f, t, i, **kw):
@@ -189,14 +224,15 @@ class K:
         if t in ("S", "dP"):
             base = V_KB0 if i % 2 == 0 else V_KB1
             off = (i // 2) * 2048 + (KT if t == "dP" else 0)
-            return [Inst(f"ds_read_b128 {rtxt('v', dst, 4)}, v{base} offset:{off}", LDS, rd=vr(base), wr=vr(dst, 4), **kw)]
+            wr = (ar if RING_FILE == "a" else vr)(dst, 4)
+            return [Inst(f"ds_read_b128 {rtxt(RING_FILE, dst, 4)}, v{base} offset:{off}", LDS, rd=vr(base), wr=wr, **kw)]
         dt, kk = i // 2, i % 2
         out = []
         for h in range(2):
             base = V_VB0 if h == 0 else V_VB1
             off = dt * 2048 + kk * 1024 + h * 512
-            out.append(Inst(f"ds_read_b64_tr_b16 {rtxt('v', dst + 2 * h, 2)}, v{base} offset:{off}", LDS,
-                            rd=vr(base), wr=vr(dst + 2 * h, 2), **kw))
+            out.append(Inst(f"ds_read_b64_tr_b16 {rtxt(RING_FILE, dst + 2 * h, 2)}, v{base} offset:{off}", LDS,
+                            rd=vr(base), wr=(ar if RING_FILE == "a" else vr)(dst + 2 * h, 2), **kw))
         return out
 
     def cvt(self, dst, s0, s1, **kw):
@@ -218,16 +254,21 @@ class K:
                 if n0_add:
                     ops.append(Inst(f"v_subrev_u32 v{V_LM}, {n0_add}, v{V_LM}", VALU, rd=vr(V_LM), wr=vr(V_LM), key=k0))
             for g in range(16):
-                ops.append(Inst(f"v_fma_f32 v{S + g}, v{S + g}, s{S_C}, v{V_NLC[j]}", VALU,
-                                rd=vr(S + g) + sr(S_C) + vr(V_NLC[j]), wr=vr(S + g), key=k0 + 4 * g))
+                if not CHAIN_S:
+                    ops.append(Inst(f"v_fma_f32 v{S + g}, v{S + g}, s{S_C}, v{V_NLC[j]}", VALU,
+                                    rd=vr(S + g) + sr(S_C) + vr(V_NLC[j]), wr=vr(S + g), key=k0 + 4 * g))
+                elif not self.unit_c:      # S' = S^T - LSE log2 e / c: c S' is the log2-domain score
+                    ops.append(Inst(f"v_mul_f32_e32 v{S + g}, s{S_C}, v{S + g}", VALU, rd=vr(S + g) + sr(S_C),
+                                    wr=vr(S + g), key=k0 + 4 * g))
                 if masked:
                     const = (g & 3) + 8 * (g >> 2)
                     ops.append(Inst(f"v_cmp_gt_i32_e32 vcc, {const}, v{V_LM}", VALU, rd=vr(V_LM), wr=[("vcc", 0)], key=k0 + 4 * g))
                     ops.append(Inst(f"v_cndmask_b32_e32 v{S + g}, v{S + g}, v{V_NINF}, vcc", VALU,
                                     rd=vr(S + g) + vr(V_NINF) + [("vcc", 0)], wr=vr(S + g), key=k0 + 4 * g))
                 ops.append(Inst(f"v_exp_f32_e32 v{S + g}, v{S + g}", TRANS, rd=vr(S + g), wr=vr(S + g), key=k0 + 4 * g + 1))
-                ops.append(Inst(f"v_sub_f32_e32 v{DP + g}, v{DP + g}, v{V_D[j]}", VALU, rd=vr(DP + g) + vr(V_D[j]),
-                                wr=vr(DP + g), key=k0 + 4 * g + 2))
+                if not CHAIN_D:            # (CHAIN_D: dP' = dP^T - D already)
+                    ops.append(Inst(f"v_sub_f32_e32 v{DP + g}, v{DP + g}, v{V_D[j]}", VALU, rd=vr(DP + g) + vr(V_D[j]),
+                                    wr=vr(DP + g), key=k0 + 4 * g + 2))
                 ops.append(Inst(f"v_mul_f32_e32 v{DP + g}, v{S + g}, v{DP + g}", VALU, rd=vr(S + g) + vr(DP + g),
                                 wr=vr(DP + g), key=k0 + 4 * g + 3))
                 if g % 2 == 1:
@@ -272,7 +313,8 @@ class K:
         for f, (t, i) in enumerate(frags):
             if f < 3:
                 continue        # prefetched by the predecessor
-            eg = 2 * (f - 16) + 1 if f >= 16 else (2 * (f - OPT_WIN) + 1 if f >= OPT_WIN else None)
+            win = min(OPT_WIN, RING_SLOTS)
+            eg = 2 * (f - win) + 1 if f >= win else None
             fill += self.frag_reads(f, t, i, key=-100 + f, earliest=eg, deadline=max(2 * f - OPT_LEAD, 0))
         if valu:
             fill += self.valu_ops(par, masked, n0_add)
@@ -288,7 +330,7 @@ class K:
             nfr = self.phase_frags(next_kind in ("full", "sdp"), next_kind in ("full", "dq"))
             for f in range(3):
                 t, i = nfr[f]
-                users = [k for k in range(len(frags)) if k % 16 == f % 16]
+                users = [k for k in range(len(frags)) if k % RING_SLOTS == f % RING_SLOTS]
                 eg = 2 * max(users) + 1 if users else None
                 fill += self.frag_reads(f, t, i, key=600 + f, earliest=eg)
         if tail_ops:
@@ -312,7 +354,8 @@ class K:
         for f, (t, i) in enumerate(frags):
             if f < 3:
                 continue
-            fill += self.frag_reads(f, t, i, key=-100 + f, deadline=max(2 * f - OPT_LEAD, 0))
+            fill += self.frag_reads(f, t, i, key=-100 + f, deadline=max(2 * f - OPT_LEAD, 0),
+                                    earliest=2 * (f - RING_SLOTS) + 1 if f >= RING_SLOTS else None)
         return schedule(mf, fill)
 
     # ------------------------------------------------------------------ prologue
@@ -773,6 +816,30 @@ class K:
         # -LSE log2 e (LSE = +inf -> -inf: P = 0); the loads landed with the prologue's wait
         ph = [Inst(f"v_mul_f32_e32 v{V_NLC[j]}, 0xbfb8aa3b, v{V_NLC[j]}", VALU, rd=vr(V_NLC[j]), wr=vr(V_NLC[j]), key=-500)
               for j in range(2)]
+        if CHAIN_S or CHAIN_D:
+            # the chain-start blocks: 16 copies of -LSE log2 e / c and of -D per q-block (a row's 16
+            # accumulator elements are 16 keys of that row); c = 1 on the _c1 kernels.  The first MFMAs
+            # read them: all in gap -1 (deadline 0; the scheduler orders fillers against MFMAs only so)
+            ph = [x for x in ph]
+            for x in ph:
+                x.dl = 0
+            t = V_TMP + 8
+            if CHAIN_S and not self.unit_c:
+                ph.append(Inst(f"v_rcp_f32_e32 v{t}, s{S_C}", TRANS, rd=sr(S_C), wr=vr(t), key=-500))
+            for j in range(2):
+                if CHAIN_S:
+                    src = V_NLC[j]
+                    if not self.unit_c:
+                        ph.append(Inst(f"v_mul_f32_e32 v{V_TMP + 6 + j}, v{t}, v{V_NLC[j]}", VALU, rd=vr(t) + vr(V_NLC[j]),
+                                       wr=vr(V_TMP + 6 + j), key=-499))
+                        src = V_TMP + 6 + j
+                    ph += [Inst(f"v_mov_b32_e32 v{NLCB(j) + e}, v{src}", VALU, rd=vr(src), wr=vr(NLCB(j) + e), key=-498)
+                           for e in range(16)]
+                if CHAIN_D:
+                    ph += [Inst(f"v_sub_f32_e32 v{NDB(j) + e}, 0, v{V_D[j]}", VALU, rd=vr(V_D[j]), wr=vr(NDB(j) + e), key=-498)
+                           for e in range(16)]
+            for x in ph:
+                x.dl = 0
         ph += [Inst(f"s_mov_b32 s{S_SROW}, 0", SALU, wr=sr(S_SROW)),
                Inst(f"s_mov_b32 s{S_STR}, {RING - 2 * SLOT}", SALU, wr=sr(S_STR)),
                Inst(f"v_add_u32_e32 v{V_KB0}, 0, v{V_RB0}", VALU, rd=vr(V_RB0), wr=vr(V_KB0)),
@@ -780,7 +847,8 @@ class K:
         mf, frags = self.phase_mfmas(1, True, False)
         fill = []
         for f, (t, i) in enumerate(frags):
-            fill += self.frag_reads(f, t, i, key=-100 + f, deadline=max(2 * f - OPT_LEAD, 0))
+            fill += self.frag_reads(f, t, i, key=-100 + f, deadline=max(2 * f - OPT_LEAD, 0),
+                                    earliest=2 * (f - RING_SLOTS) + 1 if f >= RING_SLOTS else None)
         if fold:
             fill += self.q_fold_fill()
         fill += self.slot_advance(S_SROW, key=400) + self.slot_advance(S_STR, key=400)
@@ -791,7 +859,8 @@ class K:
         nfr = self.phase_frags(True, False)
         for f in range(3):
             t, i = nfr[f]
-            fill += self.frag_reads(f, t, i, key=600 + f, earliest=2 * f + 1)
+            users = [k for k in range(len(frags)) if k % RING_SLOTS == f % RING_SLOTS]
+            fill += self.frag_reads(f, t, i, key=600 + f, earliest=2 * max(users) + 1)
         sch = schedule(mf, ph + fill)
         # (the fold's 16 Q' stores are younger than the K / V DMAs this wait is about)
         sch += [Inst(f"s_waitcnt vmcnt({VMCNT_STEP + (2 * KS if fold else 0)}) lgkmcnt(0)", WAIT), Inst("s_barrier", BARRIER)]

@@ -14,8 +14,11 @@ flash_bwd_launch_template.h:194-235).  What changes at d = 64:
   * a K (or V) subtile of 32 keys is 4 KiB: the two 64-byte panels of gen_dq.py's LDS layout; each wave
     DMAs one 1-KiB piece of K and one of V per subtile (panel w & 1, rows 16 (w >> 1)), so the ring's
     9 slots take 72 KiB and a step issues 4 pieces a wave (VMCNT_STEP 4);
-  * registers keep gen_dq.py's map (dQ^T a[64 j + 16 dt], Q a[128 + 32 j + 4 ks], dO a[192 + ...]),
-    the upper halves of each block unused.
+  * registers keep gen_dq.py's map (dQ^T a[64 j + 16 dt], Q a[128 + 32 j + 4 ks], dO a[192 + ...]);
+    the A-fragment ring moves into the AGPRs that leaves free (a[32:63], a[96:127]), and its VGPRs
+    v[160:223] hold per-row chain starts (gen_dq.py CHAIN_S / CHAIN_D): S^T starts from -LSE log2 e / c and dP^T
+    from -D, so the softmax VALU per score is exp (+ one multiply unless c = 1: the _c1 kernels, the
+    folded backward) and dS = P dP' -- 64 fewer VALU ops a phase than gen_dq.py's v_fma + v_sub.
 """
 import os
 import sys
@@ -32,11 +35,14 @@ G.RING = G.NS * G.SLOT              # 72 KiB
 G.LDS_BYTES = G.RING
 G.PIECES = 2
 G.VMCNT_STEP = 2 * G.PIECES
+G.CHAIN_S = G.CHAIN_D = True
+G.RING_SLOTS = 16
+G.RING_FILE = "a"
 assert G.RING % 4096 == 0
 
 
 def main():
-    kernels = [G.K(bf, ca) for bf in (True, False) for ca in (True, False)]
+    kernels = [G.K(bf, ca, u) for u in (False, True) for bf in (True, False) for ca in (True, False)]
     out = ['\t.amdgcn_target "amdgcn-amd-amdhsa--gfx950"', "\t.amdhsa_code_object_version 5", "\t.text"]
     for k in kernels:
         out.append(k.render())

@@ -103,7 +103,7 @@ struct DevModule {
   hipFunction_t fn[8] = {};      // dK/dV [bf16 causal, bf16 full, f16 causal, f16 full], then the same with c = 1
   hipFunction_t fn2[8] = {};     // the same, two waves per SIMD (gen_bwd2.py, 512 threads)
   hipFunction_t fn_dq[4] = {};   // dQ, the same order
-  hipFunction_t fn_dq64[4] = {}; // dQ, head dim 64 (gen_dq64.py)
+  hipFunction_t fn_dq64[8] = {}; // dQ, head dim 64 (gen_dq64.py): the order of fn (c = 1 kernels last)
   int cus = 0;
 };
 std::mutex g_mu;
@@ -125,8 +125,10 @@ const char* kNames64[8] = {"fa_bwd_dkdv_asm_d64_bf16_causal", "fa_bwd_dkdv_asm_d
                            "fa_bwd_dkdv_asm_d64_f16_causal_c1", "fa_bwd_dkdv_asm_d64_f16_full_c1"};
 const char* kDqNames[4] = {"fa_bwd_dq_asm_d128_bf16_causal", "fa_bwd_dq_asm_d128_bf16_full",
                            "fa_bwd_dq_asm_d128_f16_causal", "fa_bwd_dq_asm_d128_f16_full"};
-const char* kDq64Names[4] = {"fa_bwd_dq_asm_d64_bf16_causal", "fa_bwd_dq_asm_d64_bf16_full",
-                             "fa_bwd_dq_asm_d64_f16_causal", "fa_bwd_dq_asm_d64_f16_full"};
+const char* kDq64Names[8] = {"fa_bwd_dq_asm_d64_bf16_causal", "fa_bwd_dq_asm_d64_bf16_full",
+                             "fa_bwd_dq_asm_d64_f16_causal", "fa_bwd_dq_asm_d64_f16_full",
+                             "fa_bwd_dq_asm_d64_bf16_causal_c1", "fa_bwd_dq_asm_d64_bf16_full_c1",
+                             "fa_bwd_dq_asm_d64_f16_causal_c1", "fa_bwd_dq_asm_d64_f16_full_c1"};
 
 void check(hipError_t e, const char* what) {
   if (e != hipSuccess) throw std::runtime_error(std::string("flash_attn_bwd (asm dK/dV): ") + what + ": " + hipGetErrorString(e));
@@ -141,7 +143,7 @@ DevModule& module_for(int dev) {
     check(hipModuleLoadData(&m.mod_dq, fa_dq_asm_co), "hipModuleLoadData (dQ)");
     for (int i = 0; i < 4; ++i) check(hipModuleGetFunction(&m.fn_dq[i], m.mod_dq, kDqNames[i]), kDqNames[i]);
     check(hipModuleLoadData(&m.mod_dq64, fa_dq64_asm_co), "hipModuleLoadData (dQ, head dim 64)");
-    for (int i = 0; i < 4; ++i) check(hipModuleGetFunction(&m.fn_dq64[i], m.mod_dq64, kDq64Names[i]), kDq64Names[i]);
+    for (int i = 0; i < 8; ++i) check(hipModuleGetFunction(&m.fn_dq64[i], m.mod_dq64, kDq64Names[i]), kDq64Names[i]);
     check(hipModuleLoadData(&m.mod2, fa_bwd2_asm_co), "hipModuleLoadData (dK/dV, two waves per SIMD)");
     for (int i = 0; i < 8; ++i) check(hipModuleGetFunction(&m.fn2[i], m.mod2, kNames2[i]), kNames2[i]);
     check(hipModuleLoadData(&m.mod64, fa_bwd64_asm_co), "hipModuleLoadData (dK/dV, head dim 64)");
@@ -285,7 +287,8 @@ void launch_bwd_dq_asm(const BwdParams& p, bool is_bf16, hipStream_t stream) {
   {
     std::lock_guard<std::mutex> lk(g_mu);
     DevModule& m = module_for(dev);
-    fn = (s.d == 64 ? m.fn_dq64 : m.fn_dq)[(is_bf16 ? 0 : 2) + (s.causal ? 0 : 1)];
+    const int v = (is_bf16 ? 0 : 2) + (s.causal ? 0 : 1);
+    fn = s.d == 64 ? m.fn_dq64[v + (s.scale_log2 == 1.0f ? 4 : 0)] : m.fn_dq[v];
     cus = m.cus;
   }
   // persistent grid (knob 6): one workgroup per CU walking the item list in snake order (fixed
