@@ -435,8 +435,10 @@ void flash_attn_timing_read(int kernel_id, double * total_ms, long * count);
  * (FLASH_ATTN_MI355X_VARLEN_ROUNDS, default 2, in snake-paired rounds; 1: one workgroup per item).
  * Knob 6 = 2 also runs varlen dK/dV persistent, from a device-built work list.  10 the assembly
  * dK/dV kernel with two waves per SIMD, specialised by role (FLASH_ATTN_MI355X_BWD_2W, default 0 =
- * the one-wave-per-SIMD kernel; 1 gives bitwise the same results, measured 7-8 % slower).  Each is read from its environment
- * variable once, at first use. */
+ * the one-wave-per-SIMD kernel; 1 gives bitwise the same results, measured 7-8 % slower).  11 items
+ * per workgroup of the assembly forward on varlen calls that are not persistent
+ * (FLASH_ATTN_MI355X_FWD_VARLEN_ROUNDS, snake-paired rounds; 1 = one workgroup per item).  Each is
+ * read from its environment variable once, at first use. */
 void flash_attn_set_knob(int id, int value);
 int flash_attn_get_knob(int id);
 /* 0 routes every forward to the HIP kernel, 1 (default) lets head dim 128 and 64 take the assembly

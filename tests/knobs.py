@@ -5,7 +5,7 @@ import contextlib
 import ctypes
 
 NO_SPLITKV, NO_XCD_GROUP, XCD_GROUP_MIN_MIB, BWD_ASM, DQ_ASM, FWD_PERSIST, BWD_PERSIST, ASM_XCD_GROUP_MIN_MIB, FUSE_PRE, \
-    VARLEN_ROUNDS, BWD_2W = 0, 1, 2, 3, 4, 5, 6, 7, 8, 9, 10
+    VARLEN_ROUNDS, BWD_2W, FWD_VARLEN_ROUNDS = 0, 1, 2, 3, 4, 5, 6, 7, 8, 9, 10, 11
 
 
 def _lib():

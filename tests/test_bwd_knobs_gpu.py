@@ -3,7 +3,8 @@
 reference compute_dot_do_o, flash_bwd_kernel.h:112-188) and the persistent item loops (knob 6) each
 run under the reference's 2x rule (tests/test_flash_attn.py:630-639) in both settings, so the fused
 D path keeps oracle coverage whatever the defaults are.  A C3-class fixed-length case and a varlen
-case with ragged sequences; d = 128 (the assembly backward's domain)."""
+case with ragged sequences; d = 128 and 64 (the assembly backward's domain: gen_bwd / gen_dq and,
+since round 6, gen_bwd64 / gen_dq64)."""
 import pytest
 import torch
 
@@ -26,16 +27,17 @@ def _bound(name, got, ref, pt):
     assert ok, f"{name}: max|err| {err:.3e} > bound {bound:.3e}"
 
 
+@pytest.mark.parametrize("d", [128, 64])
 @pytest.mark.parametrize("persist", [0, 1])
 @pytest.mark.parametrize("fuse", [0, 1])
 @pytest.mark.parametrize("causal", [True, False])
-def test_fixed_length_2x_rule(fuse, persist, causal):
-    """C3-class (bf16, d 128, 2 x 2048 x 16 heads: 256 dK/dV items, more than the CUs, so the
+def test_fixed_length_2x_rule(fuse, persist, causal, d):
+    """C3-class (bf16, 2 x 2048 x 16 heads: 256 dK/dV items at d 128, more than the CUs, so the
     persistent loops run several rounds)"""
     from flash_attn import flash_attn_func
 
     torch.manual_seed(0)
-    b, s, h, d = 2, 2048, 16, 128
+    b, s, h = 2, 2048, 16
     q, k, v = (torch.randn(b, s, h, d, device=DEV, dtype=torch.bfloat16, requires_grad=True) for _ in range(3))
     out = flash_attn_func(q, k, v, causal=causal)
     g = torch.randn_like(out)
@@ -52,14 +54,15 @@ def test_fixed_length_2x_rule(fuse, persist, causal):
         _bound(name, got, r, p)
 
 
+@pytest.mark.parametrize("d", [128, 64])
 @pytest.mark.parametrize("fuse", [0, 1])
 @pytest.mark.parametrize("causal", [True, False])
-def test_varlen_2x_rule(fuse, causal):
+def test_varlen_2x_rule(fuse, causal, d):
     from flash_attn import flash_attn_varlen_func
 
     torch.manual_seed(1)
     lens = [1, 300, 1500, 0, 777, 64, 255, 256, 257]
-    h, d = 4, 128
+    h = 4
     cu = torch.tensor([0] + lens, dtype=torch.int64).cumsum(0).to(torch.int32).to(DEV)
     total = sum(lens)
     q, k, v = (torch.randn(total, h, d, device=DEV, dtype=torch.bfloat16, requires_grad=True) for _ in range(3))
@@ -161,3 +164,29 @@ def test_two_waves_per_simd_bitwise(case):
     for name, got, r, p in zip(("dq", "dk", "dv"), res[1], gr, gp):
         ok, err, bound = check_within_bound(got.float(), r.float(), p.float(), floor=1e-4)
         assert ok, f"{name}: max|err| {err:.3e} > bound {bound:.3e}"
+
+
+@pytest.mark.parametrize("d", [128, 64])
+@pytest.mark.parametrize("causal", [True, False])
+def test_forward_varlen_rounds_bitwise(causal, d):
+    """knob 11 (items per workgroup of the assembly forward on varlen calls, snake-paired rounds over
+    the decoded order): the same per-item arithmetic in any work order, so out and LSE are bitwise
+    those of one workgroup per item -- empty sequences and blocks past a sequence's end included"""
+    import flash_attn_2_cuda as m
+    from knobs import FWD_VARLEN_ROUNDS
+
+    torch.manual_seed(3)
+    lens = [700, 0, 130, 2100, 64, 1025, 9, 3000, 1]
+    h = 8
+    cu = torch.tensor([0] + lens, dtype=torch.int64).cumsum(0).to(torch.int32).to(DEV)
+    total = sum(lens)
+    q, k, v = (torch.randn(total, h, d, device=DEV, dtype=torch.bfloat16) for _ in range(3))
+    res = {}
+    for rounds in (1, 2, 3):
+        with knob(FWD_VARLEN_ROUNDS, rounds):
+            r = m.varlen_fwd(q, k, v, None, cu, cu, max(lens), max(lens), 0.0, d ** -0.5, False, causal, False, None)
+        res[rounds] = (r[0].clone(), r[5].clone())
+    for rounds, (o, lse) in res.items():
+        assert torch.equal(o, res[1][0]), rounds
+        for i, n in enumerate(lens):     # (LSE rows past a sequence's length are not written)
+            assert torch.equal(lse[i, :, :n], res[1][1][i, :, :n]), (rounds, i)

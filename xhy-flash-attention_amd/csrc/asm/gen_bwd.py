@@ -59,7 +59,7 @@ SUB = 32                # query rows per subtile
 BKN = 128               # keys per workgroup
 QT = SUB * D * 2        # bytes of a Q (or dO) subtile = 8 KiB
 SLOT = 2 * QT           # Q | dO
-NS = 9                  # Q / dO ring slots
+NS = int(os.environ.get("FA_GBW_NS", "9"))   # Q / dO ring slots (a power of two wraps with one s_and)
 RING = NS * SLOT        # 147456
 LBASE = RING            # -LSE/scale | -D ring (16 x 256 B)
 NLS = 16
@@ -358,6 +358,9 @@ class K:
     def slot_advance(self, reg, key=0):
         t = S_TMP + 2
         I = Inst
+        if RING & (RING - 1) == 0:     # (the ring starts at LDS 0)
+            return [I(f"s_add_u32 s{reg}, s{reg}, {SLOT}", SALU, rd=sr(reg), wr=sr(reg) + [("scc", 0)], key=key),
+                    I(f"s_and_b32 s{reg}, s{reg}, {RING - 1}", SALU, rd=sr(reg), wr=sr(reg) + [("scc", 0)], key=key)]
         return [I(f"s_add_u32 s{reg}, s{reg}, {SLOT}", SALU, rd=sr(reg), wr=sr(reg) + [("scc", 0)], key=key),
                 I(f"s_sub_u32 s{t}, s{reg}, {RING}", SALU, rd=sr(reg), wr=sr(t) + [("scc", 0)], key=key),
                 I(f"s_cmp_ge_u32 s{reg}, {RING}", SALU, rd=sr(reg), wr=[("scc", 0)], key=key),

@@ -235,6 +235,12 @@ bool launch_fwd_asm(const FwdParams& p, bool is_bf16, hipStream_t stream) {
                             : nullptr;
   long long grid = nwg;
   if (persist && cus > 0 && nwg > cus && (dev_list || s.cu_seqlens_q == nullptr)) grid = cus;
+  // varlen launches that stay one workgroup per item (the XCD-grouped order has no device list):
+  // R items per workgroup instead (knob 11) in snake-paired rounds over the decoded order, the
+  // dispatcher still balancing the workgroups; G a multiple of 8 keeps each on its XCD's items
+  const int rounds = knob(kKnobFwdVarlenRounds);
+  if (s.cu_seqlens_q != nullptr && grid == nwg && rounds > 1 && nwg > 8ll * rounds)
+    grid = ((nwg + rounds - 1) / rounds + 7) / 8 * 8;
   FwdAsmArgs a;
   std::memset(&a, 0, sizeof(a));
   a.q = p.q; a.k = p.k; a.v = p.v; a.o = p.o; a.lse = p.lse;

@@ -223,7 +223,11 @@ enum Knob { kKnobNoSplitKv = 0 /* FLASH_ATTN_MI355X_NO_SPLITKV: 1 = never split 
             kKnobBwd2W = 10 /* FLASH_ATTN_MI355X_BWD_2W: 1 = the assembly dK/dV kernel with two waves per SIMD
                                (gen_bwd2.py, 8 waves by role; bitwise the same results, 7-8 % slower at C3,
                                DESIGN.md round 6); 0 (default) = one wave per SIMD (gen_bwd.py) */,
-            kNumKnobs = 11 };
+            kKnobFwdVarlenRounds = 11 /* FLASH_ATTN_MI355X_FWD_VARLEN_ROUNDS: items per workgroup of the
+                                         assembly forward on varlen calls that do not run persistent
+                                         (snake-paired rounds: the next item's Q / K / V are issued
+                                         under the current one's last steps); 1 = one per item */,
+            kNumKnobs = 12 };
 int knob(int id);
 void set_knob(int id, int value);
 

@@ -106,9 +106,11 @@ constexpr KnobDef kKnobs[kNumKnobs] = {{"FLASH_ATTN_MI355X_NO_SPLITKV", 0},
                                        {"FLASH_ATTN_MI355X_ASM_XCD_GROUP_MIN_MIB", 0},
                                        {"FLASH_ATTN_MI355X_FUSE_PRE", 1},
                                        {"FLASH_ATTN_MI355X_VARLEN_ROUNDS", 2},
-                                       {"FLASH_ATTN_MI355X_BWD_2W", 0}};
+                                       {"FLASH_ATTN_MI355X_BWD_2W", 0},
+                                       {"FLASH_ATTN_MI355X_FWD_VARLEN_ROUNDS", 1}};
 std::atomic<int> g_knob[kNumKnobs] = {{INT_MIN}, {INT_MIN}, {INT_MIN}, {INT_MIN}, {INT_MIN},
-                                      {INT_MIN}, {INT_MIN}, {INT_MIN}, {INT_MIN}, {INT_MIN}, {INT_MIN}};
+                                      {INT_MIN}, {INT_MIN}, {INT_MIN}, {INT_MIN}, {INT_MIN}, {INT_MIN},
+                                      {INT_MIN}};
 }  // namespace
 
 int knob(int id) {
