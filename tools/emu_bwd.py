@@ -27,7 +27,8 @@ BKN = 128
 KINDS = {1: (GEN, "fa_bwd_dkdv_asm", 4), 2: (GEN2, "fa_bwd2_dkdv_asm", 8), 64: (GEN64, "fa_bwd_dkdv_asm", 4)}
 DIMS = {1: (128, 128), 2: (128, 128), 64: (64, 256)}     # (head dim, keys per workgroup)
 # the -LSE / -D ring, which every wave DMAs with the same bytes (benign for the race checker)
-LRING = {1: (147456, 147456 + 4096), 2: (114688, 114688 + 4096), 64: (73728, 73728 + 4096)}
+_NS = int(os.environ.get("FA_GBW_NS", "9"))      # (gen_bwd.py's Q / dO ring slots)
+LRING = {1: (_NS * 16384, _NS * 16384 + 4096), 2: (114688, 114688 + 4096), 64: (_NS * 8192, _NS * 8192 + 4096)}
 RACES = []          # cross-wave LDS races the last run found (race checker on)
 
 
