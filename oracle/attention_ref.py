@@ -115,6 +115,23 @@ def attention_lse_pt(q, k, causal=False, key_padding_mask=None):
     return torch.where(torch.isneginf(lse), torch.full_like(lse, float("inf")), lse)
 
 
+def fold_lse_bound(q, k, causal=False, softmax_scale=None):
+    """Per row (b, h, sq): the a-priori LSE error of scoring from Q' = round(scale log2 e Q) in Q's
+    dtype (the assembly kernels' fold, DESIGN.md deviation 8) -- u max_j sum_d |scale q_d k_jd| over
+    the row's visible keys, u the dtype's unit roundoff (bf16 2^-8, fp16 2^-11): the LSE is a smooth
+    max of the scores, each off by at most that -- and the row's visible key count."""
+    u = 2.0 ** -8 if q.dtype == torch.bfloat16 else 2.0 ** -11
+    qd, kd = q.double(), _repeat_kv(k.double(), q.shape[2] // k.shape[2])
+    scale = q.shape[-1] ** -0.5 if softmax_scale is None else softmax_scale
+    s_abs = torch.einsum("bthd,bshd->bhts", qd.abs(), kd.abs()) * scale
+    sq, sk = q.shape[1], k.shape[1]
+    vis = torch.ones(sq, sk, dtype=torch.bool, device=q.device)
+    if causal:
+        vis = ~torch.triu(vis, 1)
+    s_abs = s_abs.masked_fill(~vis, 0.0)
+    return u * s_abs.amax(dim=-1), vis.sum(dim=-1).expand(q.shape[0], q.shape[2], sq)
+
+
 def check_lse_within_bound(lse, ref, pt, atol=1e-3, rtol=1e-4, factor=2.0):
     """softmax_lse acceptance: rows without a key must read +inf; elsewhere
     |lse - ref| <= max(factor * max|pt - ref|, atol + rtol |ref|) -- the 2x rule of the outputs

@@ -28,7 +28,7 @@ OURS = ("fwd_kernel", "bwd_pre_kernel", "bwd_dkdv_kernel", "bwd_dq_kernel", "spl
 
 
 def short(name):
-    if name.startswith("fa_fwd_asm_"):   # the assembly forward (csrc/asm/gen_fwd.py) is the fwd_kernel slot
+    if name.startswith(("fa_fwd_asm_", "fa_fwdnf_asm_")):   # the assembly forward (gen_fwd.py / gen_fwdnf.py) is the fwd_kernel slot
         return "fwd_kernel"
     if name.startswith(("fa_bwd_dkdv_asm_", "fa_bwd2_dkdv_asm_")):   # the assembly dK/dV kernels (gen_bwd*.py)
         return "bwd_dkdv_kernel"

@@ -4,6 +4,7 @@ bf16 / fp16, fixed length and varlen.  Head dims 64 and 128 run the hand-schedul
 (forward, dK/dV, dQ), whose schedules are generated -- a random sweep of shapes is the cheap way to
 catch a latent schedule bug (a register live across an out-of-line branch, a ring slot reused early)
 that the fixed parametrizations miss; head dim 96 runs the HIP kernels."""
+import os
 import random
 
 import pytest
@@ -11,7 +12,7 @@ import torch
 
 from lse_record import lse_ratio, record
 from oracle.attention_ref import (attention_lse_pt, attention_lse_ref, attention_ref,
-                                  check_lse_within_bound, check_within_bound)
+                                  check_lse_within_bound, check_within_bound, fold_lse_bound)
 
 pytestmark = pytest.mark.gpu
 DEV = "cuda"
@@ -60,18 +61,19 @@ def _ref_grads(q, k, v, g, causal):
     return out
 
 
-# Ceiling on err / (plain 2x bound) for the LSE of a folded call (d 64 / 128, DESIGN.md deviation 8),
-# and on the share of its rows above the plain bound.  The unfolded calls (d 96 here) have no slack.
-LSE_FOLD_CEIL = 2.0   # (round 6: worst 1.57, one single-key row of 92 cases; the rest <= 0.55)
+# A folded call's LSE (d 64 / 128, DESIGN.md deviation 8): rows with at most LSE_SHORT_KEYS visible keys
+# may take the fold's a-priori bound (oracle fold_lse_bound) instead of the plain 2x rule -- such a row
+# sees the rounding of Q' whole; on the longer rows, where it averages out, err / (plain bound) may
+# reach LSE_FOLD_CEIL on at most LSE_FOLD_MAX_ROW_SHARE of them.  Unfolded calls (d 96) have no slack.
+LSE_SHORT_KEYS = 4
+LSE_FOLD_CEIL = 2.0   # (round 6, 800 seeds: long rows <= 0.56; the single-key rows up to 3.5 x the plain bound)
 LSE_FOLD_MAX_ROW_SHARE = 0.05
 
 
 def _check_lse(lse, q, k, c, seed):
-    """softmax_lse under the plain 2x rule of check_lse_within_bound.  A folded call (Q' =
-    round(scale log2e Q), DESIGN.md deviation 8) may exceed it by the rounding of Q', which averages
-    out over many keys and is seen whole by a row with one key: every case's worst ratio
-    err / bound and its rows above the bound are recorded (tests/lse_record.py), and a folded call
-    fails above LSE_FOLD_CEIL or when more than LSE_FOLD_MAX_ROW_SHARE of its rows exceed the bound."""
+    """softmax_lse under the plain 2x rule of check_lse_within_bound, with the fold's slack above for
+    folded calls; every case's worst ratio err / bound and its rows above the bound are recorded
+    (tests/lse_record.py)."""
     causal = c["causal"]
     ref, pt = attention_lse_ref(q, k, causal), attention_lse_pt(q, k, causal)
     ok, err, pt_err = check_lse_within_bound(lse, ref, pt)
@@ -80,11 +82,23 @@ def _check_lse(lse, q, k, c, seed):
     if ok or c["d"] not in (64, 128):
         assert ok, f"{c}: lse err {err:.3e} (pt {pt_err:.3e})"
         return
-    assert ratio <= LSE_FOLD_CEIL and over <= max(1, LSE_FOLD_MAX_ROW_SHARE * rows), \
-        f"{c}: lse err {err:.3e} = {ratio:.2f} x the 2x bound (pt {pt_err:.3e}) on {over} of {rows} rows"
+    fb, nk = (x.cpu().double() for x in fold_lse_bound(q.detach(), k.detach(), causal))
+    lse_d, ref_d = lse.detach().cpu().double(), ref.detach().cpu().double()
+    live = ~torch.isinf(ref_d)
+    e = (lse_d - ref_d).abs()
+    plain = torch.clamp(1e-3 + 1e-4 * ref_d.abs(), min=2.0 * pt_err)
+    short = live & (nk.double() <= LSE_SHORT_KEYS)
+    bad_short = short & (e > torch.maximum(plain, fb))
+    assert not bad_short.any(), f"{c}: a short row's lse err {float(e[bad_short].max()):.3e} > the fold bound"
+    long_ = live & ~short
+    r = (e / plain)[long_]
+    n_over = int((r > 1).sum())
+    assert (r.numel() == 0 or float(r.max()) <= LSE_FOLD_CEIL) and n_over <= max(1, LSE_FOLD_MAX_ROW_SHARE * r.numel()), \
+        f"{c}: lse err {err:.3e} = {float(r.max()):.2f} x the 2x bound (pt {pt_err:.3e}) on {n_over} of {r.numel()} rows"
 
 
-@pytest.mark.parametrize("seed", range(160))
+# FA_FUZZ_SEEDS widens the sweep for a one-off run (the suite runs 160)
+@pytest.mark.parametrize("seed", range(int(os.environ.get("FA_FUZZ_SEEDS", "160"))))
 def test_random_shape(seed):
     from flash_attn import flash_attn_func, flash_attn_varlen_func
 
@@ -124,3 +138,28 @@ def test_random_shape(seed):
                 dst[name][a:e] = t[0].float()
     for name, got in (("out", out), ("dq", dq), ("dk", dk), ("dv", dv)):
         _bound(name, got, refs[name], pts[name], c)
+
+
+
+@pytest.mark.parametrize("dtype", [torch.float16, torch.bfloat16])
+@pytest.mark.parametrize("causal", [False, True])
+@pytest.mark.parametrize("d", [64, 128])
+@pytest.mark.parametrize("seqlen", [1, 2, 5, 17, 128, 300])
+@pytest.mark.parametrize("hk", [5, 1])
+def test_large_scores(seqlen, d, causal, dtype, hk):
+    """the reference's overflow test (tests/test_flash_attn.py:835-878: fp16, Q x 5, K / V x 3, b 2,
+    5 heads, seqlens 1 / 2 / 5 / 17 / 128, its 5x + 1e-3 rule) on the assembly kernels' head dims 64
+    and 128, in bf16 too, MQA too, and one longer length: |LSE| and P dS large (round 6 found keys
+    past seqlen_k overflowing the fp16 dS pack this way)"""
+    from flash_attn import flash_attn_func
+
+    torch.manual_seed(0)
+    q = (torch.randn(2, seqlen, 5, d, dtype=dtype, device=DEV) * 5).requires_grad_()
+    k, v = ((torch.randn(2, seqlen, hk, d, dtype=dtype, device=DEV) * 3).requires_grad_() for _ in range(2))
+    out = flash_attn_func(q, k, v, causal=causal)
+    g = torch.randn_like(out)
+    dq, dk, dv = torch.autograd.grad(out, (q, k, v), g)
+    rg = _ref_grads(q, k, v, g, causal)
+    for name, got, r_, p_ in zip(("out", "dq", "dk", "dv"), (out, dq, dk, dv), rg["ref"], rg["pt"]):
+        ok, err, bound = check_within_bound(got.float(), r_.float(), p_.float(), factor=5.0, floor=1e-3)
+        assert ok, f"{name} max|err| {err:.3e} > bound {bound:.3e}"

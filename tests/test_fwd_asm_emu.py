@@ -147,3 +147,27 @@ def test_generated_kernels_are_hazard_free():
         if x.startswith("v_readfirstlane_b32"):
             assert lines[i - 1].startswith("s_nop"), (i, lines[i - 1])
     assert isa.XDL_RAW == 12 and isa.VALU_RFL == 1
+
+
+# ------------------------------------------------------------------------------------------------
+# the unfolded forward (csrc/asm/gen_fwdnf.py: fp32 scores from the exact Q, one v_fma per score), for
+# FLASH_ATTN_MI355X_NO_QFOLD=1 and fp16 calls with |scale log2 e| > 1
+# ------------------------------------------------------------------------------------------------
+@pytest.fixture(scope="module")
+def nf_text():
+    return subprocess.run([sys.executable, os.path.join(ROOT, "xhy-flash-attention_amd", "csrc", "asm", "gen_fwdnf.py")],
+                          check=True, capture_output=True, text=True).stdout
+
+
+@pytest.mark.timeout(600)
+@pytest.mark.parametrize("b,sq,sk,h,hk,causal,bf16,big,d", [
+    (1, 600, 600, 2, 1, True, True, None, 128),
+    (1, 300, 700, 2, 1, True, False, None, 64),
+    (2, 130, 77, 1, 1, False, True, None, 64),
+    (1, 520, 520, 1, 1, True, True, 400, 128),    # forced refits
+])
+def test_unfolded_forward_in_emulator(nf_text, b, sq, sk, h, hk, causal, bf16, big, d):
+    eo, el, *_ = emu_fwd.run(b, sq, sk, h, hk, causal, bf16, seed=0, big=big, text=nf_text, verbose=False, d=d,
+                             fold=False, prefix="fa_fwdnf_asm")
+    assert eo <= (1.6e-2 if bf16 else 2e-3), eo
+    assert el <= 1e-5, el

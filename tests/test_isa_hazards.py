@@ -183,7 +183,7 @@ def test_hazard_checker_catches_planted_hazards(tmp_path):
 
 
 def test_shipped_assembly_kernels_hazard_free():
-    """every kernel of the six embedded code objects, every control-flow path"""
+    """every kernel of the seven embedded code objects, every control-flow path"""
     import sys
     sys.path.insert(0, sys_path_tools)
     import hazard_check as hc
@@ -193,6 +193,7 @@ def test_shipped_assembly_kernels_hazard_free():
     res = hc.check_library(LIB)
     names = sorted(res)
     assert len([n for n in names if n.startswith("fa_fwd_asm_")]) == 8, names
+    assert len([n for n in names if n.startswith("fa_fwdnf_asm_")]) == 8, names      # without the Q fold
     assert len([n for n in names if n.startswith("fa_bwd_dkdv_asm_d128")]) == 8, names   # (+ the c = 1 kernels)
     assert len([n for n in names if n.startswith("fa_bwd_dkdv_asm_d64")]) == 8, names    # head dim 64
     assert len([n for n in names if n.startswith("fa_bwd_dq_asm_d128")]) == 4, names

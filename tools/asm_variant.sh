@@ -11,7 +11,7 @@ W=/tmp/fa_asmv/$NAME
 rm -rf "$W"; mkdir -p "$W" "$ROOT/variants"
 # (the in-tree build must not see the dev switches)
 env $(env | grep -o '^FA_G[A-Z_]*' | sed 's/^/-u /') make -s -C "$CS" >/dev/null
-for k in fwd bwd dq bwd2 bwd64 dq64; do
+for k in fwd bwd dq bwd2 bwd64 dq64 fwdnf; do
   python3 "$CS/asm/gen_$k.py" > "$W/fa_${k}_asm.s"
   /opt/rocm/lib/llvm/bin/clang -x assembler -target amdgcn-amd-amdhsa -mcpu=gfx950 -c "$W/fa_${k}_asm.s" -o "$W/fa_${k}_asm.o"
   /opt/rocm/lib/llvm/bin/ld.lld -shared "$W/fa_${k}_asm.o" -o "$W/fa_${k}_asm.co"
@@ -25,9 +25,9 @@ for f in $CXX_FILES; do
 done
 for o in $CS/build/*.o; do
   b=$(basename $o .o)
-  case $b in fa_fwd_asm|fa_fwd_asm_blob.cpp|fa_bwd_asm|fa_bwd_asm_blob.cpp|fa_dq_asm|fa_dq_asm_blob.cpp|fa_bwd2_asm|fa_bwd2_asm_blob.cpp|fa_bwd64_asm|fa_bwd64_asm_blob.cpp|fa_dq64_asm|fa_dq64_asm_blob.cpp) continue;; esac
+  case $b in fa_fwd_asm|fa_fwd_asm_blob.cpp|fa_bwd_asm|fa_bwd_asm_blob.cpp|fa_dq_asm|fa_dq_asm_blob.cpp|fa_bwd2_asm|fa_bwd2_asm_blob.cpp|fa_bwd64_asm|fa_bwd64_asm_blob.cpp|fa_dq64_asm|fa_dq64_asm_blob.cpp|fa_fwdnf_asm|fa_fwdnf_asm_blob.cpp) continue;; esac
   case " $CXX_FILES " in *" $b "*) continue;; esac
   OBJS="$OBJS $o"
 done
-/opt/rocm/bin/hipcc -shared --offload-arch=gfx950 -o "$ROOT/variants/libfa_$NAME.so" $OBJS "$W/blob_fwd.o" "$W/blob_bwd.o" "$W/blob_dq.o" "$W/blob_bwd2.o" "$W/blob_bwd64.o" "$W/blob_dq64.o"
+/opt/rocm/bin/hipcc -shared --offload-arch=gfx950 -o "$ROOT/variants/libfa_$NAME.so" $OBJS "$W/blob_fwd.o" "$W/blob_bwd.o" "$W/blob_dq.o" "$W/blob_bwd2.o" "$W/blob_bwd64.o" "$W/blob_dq64.o" "$W/blob_fwdnf.o"
 echo "$ROOT/variants/libfa_$NAME.so"

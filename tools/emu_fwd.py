@@ -62,10 +62,11 @@ def reference(q, k, v, causal, scale, seqs_q=None, seqs_k=None):
 
 
 def run(b=1, sq=300, sk=300, h=2, hk=1, causal=True, bf16=True, seed=0, big=None, text=None, verbose=True,
-        grid=None, d=128, hp=0, fold=None):
+        grid=None, d=128, hp=0, fold=None, prefix="fa_fwd_asm"):
     """grid: workgroups of the persistent item loop (default: one per item); d: head dim (128, 64);
     hp: heads per XCD group of the work order (0: head-fastest); fold: compare with the folded-scale
-    arithmetic (gen_fwd.py FA_GEN_FOLD, default as the generator's environment)"""
+    arithmetic (gen_fwd.py FA_GEN_FOLD, default as the generator's environment); prefix: the kernel
+    name prefix ("fa_fwdnf_asm": gen_fwdnf.py's unfolded kernels, with fold=False)"""
     if fold is None:
         fold = os.environ.get("FA_GEN_FOLD", "1") == "1"
     D = d
@@ -94,7 +95,7 @@ def run(b=1, sq=300, sk=300, h=2, hk=1, causal=True, bf16=True, seed=0, big=None
               n_items=n_items, grid=grid or n_items, dec=fwd_item_decode(b * h, h, h // hk, nmb, hp))
     akarg = heap.put(np.frombuffer(pack_args(**kw), dtype=np.uint8))
     text = text or asm_text()
-    name = f"fa_fwd_asm_d{D}_{'bf16' if bf16 else 'f16'}_{'causal' if causal else 'full'}"
+    name = f"{prefix}_d{D}_{'bf16' if bf16 else 'f16'}_{'causal' if causal else 'full'}"
     emu = Emu(text, name, heap)
     for L in range(grid or n_items):
         emu.run_wg(L, akarg)

@@ -253,7 +253,7 @@ def check_kernel(name, ins):
     return bad
 
 
-ASM_PREFIXES = (b"fa_fwd_asm_", b"fa_bwd_dkdv_asm_", b"fa_bwd_dq_asm_", b"fa_bwd2_dkdv_asm_")
+ASM_PREFIXES = (b"fa_fwd_asm_", b"fa_fwdnf_asm_", b"fa_bwd_dkdv_asm_", b"fa_bwd_dq_asm_", b"fa_bwd2_dkdv_asm_")
 
 
 def check_library(path=LIB):

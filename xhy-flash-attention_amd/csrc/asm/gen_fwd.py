@@ -128,6 +128,7 @@ NVGPR = 228
 # P = v_exp_f32(acc) -- one VALU op per score instead of two.  Scores wholly above the causal
 # diagonal are written as -inf (no chain), so the all -inf tile V_NT gives its registers to V_M.
 OPT_FOLD = os.environ.get("FA_GEN_FOLD", "1") == "1"
+NAME = "fa_fwd_asm"     # kernel name prefix (gen_fwdnf.py: the unfolded kernels, "fa_fwdnf_asm")
 V_M = (212, 228)      # 212..227, 228..243
 if OPT_FOLD:
     NVGPR = 244
@@ -253,7 +254,7 @@ class K:
         self.bf16 = bf16
         self.causal = causal
         self.ty = "bf16" if bf16 else "f16"
-        self.name = f"fa_fwd_asm_d{D}_{self.ty}_{'causal' if causal else 'full'}"
+        self.name = f"{NAME}_d{D}_{self.ty}_{'causal' if causal else 'full'}"
         self.lines = []
         self.uid = 0
         self.refit_regs = {}

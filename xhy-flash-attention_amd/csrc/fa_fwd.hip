@@ -736,11 +736,19 @@ static void plan_split(FwdParams& p) {
 // a mask that hides nothing gives the unmasked call's result (the mask term enters the log2-domain
 // scores as mask * unscale * c); fp16 only with |c| <= 1, where c Q cannot overflow the 16-bit Q'.
 // Dropout calls (HIP kernels only) keep the exact Q: a fold would cost them a Q' pass for nothing.
+// FLASH_ATTN_MI355X_NO_QFOLD=1 (read once per process, so a forward and its backward always agree)
+// scores every call from the exact Q: the reference's precision class, at +5 % forward / +2 % dK/dV
+// time at C3 (profiles/r06/ab_c3_nofold_r06n.txt).  The fold's extra rounding of c Q matters only
+// where |c q.k| is large and a row has few keys (DESIGN.md deviation 8).
 bool attn_folds_q(const AttnShape& s, bool is_bf16) {
 #ifdef FA_NO_QFOLD   // (A/B variants whose assembly forward is generated with FA_GEN_FOLD=0)
   return false;
 #endif
-  return (s.d == 128 || s.d == 64) && !s.dropout && (is_bf16 || std::fabs(s.scale_log2) <= 1.0f);
+  static const bool no_fold = [] {
+    const char* e = std::getenv("FLASH_ATTN_MI355X_NO_QFOLD");
+    return e != nullptr && e[0] == '1';
+  }();
+  return !no_fold && (s.d == 128 || s.d == 64) && !s.dropout && (is_bf16 || std::fabs(s.scale_log2) <= 1.0f);
 }
 
 void launch_fwd(const FwdParams& p_in, bool is_bf16, hipStream_t stream) {

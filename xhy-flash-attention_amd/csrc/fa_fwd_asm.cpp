@@ -30,6 +30,8 @@
 
 extern "C" const unsigned char fa_fwd_asm_co[];
 extern "C" const unsigned long fa_fwd_asm_co_size;
+extern "C" const unsigned char fa_fwdnf_asm_co[];
+extern "C" const unsigned long fa_fwdnf_asm_co_size;
 
 namespace fa {
 namespace {
@@ -54,8 +56,9 @@ static_assert(sizeof(FwdAsmArgs) == 224 && offsetof(FwdAsmArgs, dec) == 184, "Fw
 
 constexpr int kMaxDev = 64;
 struct DevModule {
-  hipModule_t mod = nullptr;
+  hipModule_t mod = nullptr, mod_nf = nullptr;
   hipFunction_t fn[8] = {};   // d 128 then d 64: [bf16 causal, bf16 full, f16 causal, f16 full]
+  hipFunction_t fn_nf[8] = {};   // the same without the Q fold (gen_fwdnf.py)
   int cus = 0;
 };
 std::mutex g_mu;
@@ -67,6 +70,10 @@ const char* kNames[8] = {"fa_fwd_asm_d128_bf16_causal", "fa_fwd_asm_d128_bf16_fu
                          "fa_fwd_asm_d128_f16_causal", "fa_fwd_asm_d128_f16_full",
                          "fa_fwd_asm_d64_bf16_causal", "fa_fwd_asm_d64_bf16_full",
                          "fa_fwd_asm_d64_f16_causal", "fa_fwd_asm_d64_f16_full"};
+const char* kNamesNf[8] = {"fa_fwdnf_asm_d128_bf16_causal", "fa_fwdnf_asm_d128_bf16_full",
+                           "fa_fwdnf_asm_d128_f16_causal", "fa_fwdnf_asm_d128_f16_full",
+                           "fa_fwdnf_asm_d64_bf16_causal", "fa_fwdnf_asm_d64_bf16_full",
+                           "fa_fwdnf_asm_d64_f16_causal", "fa_fwdnf_asm_d64_f16_full"};
 
 void check(hipError_t e, const char* what) {
   if (e != hipSuccess) throw std::runtime_error(std::string("flash_attn_fwd (asm path): ") + what + ": " + hipGetErrorString(e));
@@ -78,6 +85,8 @@ DevModule& module_for(int dev) {
   if (m.mod == nullptr) {
     check(hipModuleLoadData(&m.mod, fa_fwd_asm_co), "hipModuleLoadData");
     for (int i = 0; i < 8; ++i) check(hipModuleGetFunction(&m.fn[i], m.mod, kNames[i]), kNames[i]);
+    check(hipModuleLoadData(&m.mod_nf, fa_fwdnf_asm_co), "hipModuleLoadData (no Q fold)");
+    for (int i = 0; i < 8; ++i) check(hipModuleGetFunction(&m.fn_nf[i], m.mod_nf, kNamesNf[i]), kNamesNf[i]);
     check(hipDeviceGetAttribute(&m.cus, hipDeviceAttributeMultiprocessorCount, dev), "hipDeviceGetAttribute");
   }
   return m;
@@ -186,9 +195,9 @@ bool fwd_asm_applicable(const FwdParams& p, bool is_bf16) {
       p.n_split != 0 || p.pack_g != 1)
     return false;
   if (p.k_row != p.v_row) return false;   // the K and V DMA share per-lane offsets
-  // The kernel holds Q as f16/bf16(c Q), c = scale * log2(e) (gen_fwd.py FA_GEN_FOLD): with fp16 and
-  // c > 1 a finite Q could overflow there, so such calls take the HIP kernel (fp32 scores).
-  if (!is_bf16 && !(std::fabs(s.scale_log2) <= 1.0f)) return false;
+  // (the folding kernels hold Q as f16/bf16(c Q), c = scale * log2(e), gen_fwd.py FA_GEN_FOLD; a call
+  // attn_folds_q does not fold -- fp16 with |c| > 1, where c Q could overflow, or
+  // FLASH_ATTN_MI355X_NO_QFOLD=1 -- takes the unfolded kernels, gen_fwdnf.py: fp32 scores from Q)
   if (s.b > 65535 || s.h > 65535 || p.num_m_blocks > 65535 || s.h % s.hk != 0) return false;
   const int64_t q_row = 2 * p.q_row, kv_row = 2 * p.k_row, o_row = 2 * p.o_row;
   const int64_t q_head = 2 * p.q_head, k_head = 2 * p.k_head, v_head = 2 * p.v_head, o_head = 2 * p.o_head;
@@ -226,7 +235,7 @@ bool launch_fwd_asm(const FwdParams& p, bool is_bf16, hipStream_t stream) {
   {
     std::lock_guard<std::mutex> lk(g_mu);
     DevModule& m = module_for(dev);
-    fn = m.fn[(s.d == 64 ? 4 : 0) + (is_bf16 ? 0 : 2) + (s.causal ? 0 : 1)];
+    fn = (attn_folds_q(s, is_bf16) ? m.fn : m.fn_nf)[(s.d == 64 ? 4 : 0) + (is_bf16 ? 0 : 2) + (s.causal ? 0 : 1)];
     cus = m.cus;
   }
   StreamScratch vbuf;          // device-built varlen work list (stream-ordered allocation)
