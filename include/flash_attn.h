@@ -441,7 +441,9 @@ void flash_attn_timing_read(int kernel_id, double * total_ms, long * count);
  * read from its environment variable once, at first use. */
 void flash_attn_set_knob(int id, int value);
 int flash_attn_get_knob(int id);
-/* 0 routes every forward to the HIP kernel, 1 (default) lets head dim 128 and 64 take the assembly
+/* (FLASH_ATTN_MI355X_NO_QFOLD=1 in the environment, read once per process, makes attn_folds_q false for
+ * every call: scores from the exact Q, the unfolded assembly forward fa_fwdnf_asm_*.)
+ * 0 routes every forward to the HIP kernel, 1 (default) lets head dim 128 and 64 take the assembly
  * kernel (FLASH_ATTN_MI355X_FWD_ASM=0 sets 0).  Neither this nor any knob changes a call's
  * numerics contract: whether a call scores from Q' = bf16/f16(scale log2(e) Q) (head dim 64 / 128,
  * no dropout; fp16 only with |scale log2(e)| <= 1) is decided by the call alone, the HIP forward
