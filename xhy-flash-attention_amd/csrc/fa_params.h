@@ -171,7 +171,9 @@ void launch_q_fold(const QFoldArgs& a, bool is_bf16, hipStream_t stream);
 // masks -- and never of a runtime knob, a stride or the kernel launch_fwd happens to pick: a forward
 // that folds but cannot take the assembly kernel (knobs, split-KV, return_softmax, 32-bit record
 // limits) runs the HIP kernels on a materialised Q' (launch_q_fold), so forward and backward agree
-// whatever switches are flipped between them.
+// whatever switches are flipped between them.  The one process-wide input is
+// FLASH_ATTN_MI355X_NO_QFOLD=1, read once at the first call: no call folds, the forward runs the
+// unfolded assembly kernels (gen_fwdnf.py) and the backward its c != 1 kernels.
 bool attn_folds_q(const AttnShape& s, bool is_bf16);                 // fa_fwd.hip
 
 // Host launchers (fa_fwd.hip / fa_bwd.hip).  Throw std::runtime_error on invalid configuration.
