@@ -1,6 +1,7 @@
 #!/usr/bin/env python3
 """Generates fa_bwd_asm.s: the gfx950 FlashAttention-2 dK / dV kernel for head dim 128, written as a
-hand-scheduled assembly kernel (one wave per SIMD).
+hand-scheduled assembly kernel (one wave per SIMD); gen_bwd64.py (head dim 64) and gen_bwd2.py (two
+waves per SIMD) build on it.
 
     python3 gen_bwd.py > fa_bwd_asm.s
 

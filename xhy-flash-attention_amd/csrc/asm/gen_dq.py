@@ -1,6 +1,6 @@
 #!/usr/bin/env python3
 """Generates fa_dq_asm.s: the gfx950 FlashAttention-2 dQ kernel for head dim 128, written as a
-hand-scheduled assembly kernel (one wave per SIMD).
+hand-scheduled assembly kernel (one wave per SIMD); gen_dq64.py instantiates it at head dim 64.
 
     python3 gen_dq.py > fa_dq_asm.s
 
