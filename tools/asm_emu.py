@@ -137,7 +137,7 @@ class Wave:
         self.done = False
         self.at_barrier = False
         self.wid = wid
-        self.vm = []        # outstanding VMEM ops in issue order: LDS-DMA writes (dst, bytes) or None
+        self.vm = []        # outstanding VMEM ops in issue order: LDS-DMA writes (dst, bytes), ("reg", index, data) or None
 
 
 class Emu:
@@ -348,18 +348,13 @@ class Emu:
                 if t.startswith("vmcnt("):
                     n = int(t[6:-1])
                     while len(w.vm) > n:
-                        e = w.vm.pop(0)
-                        if e is not None:
-                            lds[e[0]:e[0] + len(e[1])] = e[1]
-                            self._dma_land(w, e[0], len(e[1]))
+                        self._land(w, lds, w.vm.pop(0))
             return
         if op == "s_nop" or op == "s_setprio":
             return
         if op == "s_endpgm":
             for e in w.vm:
-                if e is not None:
-                    lds[e[0]:e[0] + len(e[1])] = e[1]
-                    self._dma_land(w, e[0], len(e[1]))
+                self._land(w, lds, e)
             w.vm = []
             w.done = True
             return
@@ -624,6 +619,16 @@ class Emu:
             _, _, lo, _ = self.reg_index(dst)
             s[lo] = r
 
+    def _land(self, w, lds, e):
+        """a VMEM load completes: LDS-DMA bytes or (POISON) deferred register data"""
+        if e is None:
+            return
+        if e[0] == "reg":
+            w.r[e[1]:e[1] + e[2].shape[0]] = e[2]
+            return
+        lds[e[0]:e[0] + len(e[1])] = e[1]
+        self._dma_land(w, e[0], len(e[1]))
+
     def buffer(self, w, lds, op, a, mods):
         n = {"buffer_load_dword": 1, "buffer_load_dwordx4": 4, "buffer_store_dword": 1, "buffer_store_dwordx2": 2,
              "buffer_store_dwordx4": 4}[op]
@@ -647,6 +652,9 @@ class Emu:
                 return
             else:
                 ri, _ = self.regs(w, a[0])
+                if POISON:   # lands at the wait that forces it, as the LDS-DMA data (a missing wait reads poison)
+                    w.vm.append(("reg", ri, np.ascontiguousarray(data.T)))
+                    return
                 w.r[ri:ri + n] = data.T
         else:
             ri, _ = self.regs(w, a[0])

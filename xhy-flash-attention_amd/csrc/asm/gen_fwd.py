@@ -203,6 +203,10 @@ OPT_DEFER = os.environ.get("FA_GEN_DEFER") == "1"
 OPT_T0ZERO = os.environ.get("FA_GEN_T0ZERO") == "1"
 # cache-policy modifiers of the epilogue's O stores (dev A/B), e.g. "nt"
 OPT_OPOL = (" " + os.environ["FA_GEN_OPOL"]) if os.environ.get("FA_GEN_OPOL") else ""
+# cold item start: the Q fragment loads are waited for by tile 0's vmcnt wait (they are older than
+# the K / V DMA it waits for) instead of before the DMA issue -- one memory round trip less per cold
+# item (round 6; FA_GEN_QWAIT=1 restores the wait, which an item with no tiles still takes)
+OPT_QWAIT = os.environ.get("FA_GEN_QWAIT") == "1"
 # O staged through LDS (the K/V slot of the item's last tile, free after the last step): each store
 # then writes whole rows (4 rows of 256 B at d = 128) instead of 32 rows x 32 B (round 4 default:
 # C3 -0.3 %, C4 -0.4 %, C2 ±0, bitwise identical; FA_GEN_OSTAGE=0 restores the direct stores)
@@ -1297,12 +1301,14 @@ class K:
                 I(f"s_lshl_b32 s{S_DOFF}, s{S_WAVE}, 10", SALU)]
         ins += self.item_zero(o=False)
         # no tiles at all: epilogue (O = 0, LSE = +inf)
-        ins += [I(f"s_cmp_eq_u32 s{S_NBLK}, 0", SALU, rd=sr(S_NBLK), wr=[("scc", 0)]),
-                I("s_waitcnt vmcnt(0)", WAIT),
-                I(f"s_cbranch_scc1 {self.l_empty if OPT_T0ZERO else l_epi}", BRANCH)]
+        l_nt = self.lab("notiles")
+        ins += [I(f"s_cmp_eq_u32 s{S_NBLK}, 0", SALU, rd=sr(S_NBLK), wr=[("scc", 0)])]
+        ins += [I("s_waitcnt vmcnt(0)", WAIT)] if OPT_QWAIT else []
+        ins += [I(f"s_cbranch_scc1 {l_nt}", BRANCH)]
         for tile in range(4):
             ins += self.dma_tile_ops(f"c{tile}")
         ins += [I(f"s_branch {l_tile0}", BRANCH)]
+        ins += [label(l_nt), I("s_waitcnt vmcnt(0)", WAIT), I(f"s_branch {self.l_empty if OPT_T0ZERO else l_epi}", BRANCH)]
         ins += [label(l_skip), I(f"s_add_u32 s{S_ROUND}, s{S_ROUND}, 1", SALU), I(f"s_branch {l_cold}", BRANCH)]
         if OPT_T0ZERO:   # an item with no tiles: O = 0 for its epilogue (no tile 0 zeroes it)
             ins += [label(self.l_empty)] + self.o_zero_ops() + [I(f"s_branch {l_epi}", BRANCH)]
