@@ -4,6 +4,7 @@
 #   tools/gpu_final.sh TAG a   the GPU suite, smoke(), the bench lines (C3, C4, C2, C5, d64, C3 dropout)
 #   tools/gpu_final.sh TAG b   the PMC passes of the C3 / C2 / C4 bench commands (profiles/pmc_run.sh)
 #                              and the rocprofv3 kernel statistics of the C3 bench
+#   tools/gpu_final.sh TAG pmc2  the PMC passes of the d64 and C5 bench commands
 # Each GPU step has its own time limit; a timeout, abort or crash ends the script there.
 export TMPDIR=/tmp
 TAG=${1:-final}
@@ -21,11 +22,14 @@ if [ "$PART" = a ]; then
     timeout -k 10 300 python3 bench.py --workload $w > "$OUT/bench_$w.log" 2>&1; rc=$?; stop $rc bench_$w
   done
   timeout -k 10 300 python3 bench.py --dropout 0.1 > "$OUT/bench_c3_drop.log" 2>&1; rc=$?; stop $rc bench_drop
+elif [ "$PART" = pmc2 ]; then
+  bash profiles/pmc_run.sh "$OUT/pmc_d64" d64; rc=$?; stop $rc pmc_d64
+  bash profiles/pmc_run.sh "$OUT/pmc_c5" c5; rc=$?; stop $rc pmc_c5
 else
   bash profiles/pmc_run.sh "$OUT/pmc_c3" c3; rc=$?; stop $rc pmc_c3
   bash profiles/pmc_run.sh "$OUT/pmc_c2" c2; rc=$?; stop $rc pmc_c2
   bash profiles/pmc_run.sh "$OUT/pmc_c4" c4; rc=$?; stop $rc pmc_c4
-  timeout -k 10 400 rocprofv3 --kernel-trace --stats -d "$OUT/prof_c3" -o run -- python3 bench.py --no-cpu-baseline > "$OUT/bench_c3_prof.log" 2>&1
+  timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof_c3" -o run -- python3 bench.py --no-cpu-baseline > "$OUT/bench_c3_prof.log" 2>&1
   rc=$?; stop $rc rocprof
 fi
 echo "part $PART done"
