@@ -1,0 +1,80 @@
+"""Varlen calls with sequences that have query rows but no keys, or keys but no query rows
+(cu_seqlens_q != cu_seqlens_k with zero-length entries).  The reference's forward gives such rows
+O = 0 and LSE = +inf (n_block_max = 0, flash_fwd_kernel.h:509-518; block_info.h:14-31), and its
+backward adds nothing for them; every other sequence is held to the 2x rule
+(tests/test_flash_attn.py:774-783).  At head dims 64 / 128 the rows without keys take the assembly
+forward's item start for an item with no K/V tiles (gen_fwd.py item_start): through the persistent
+device-built list and, with FLASH_ATTN_MI355X_FWD_PERSIST=0, one workgroup per item."""
+import math
+
+import pytest
+import torch
+
+from knobs import FWD_PERSIST, knob
+from oracle.attention_ref import attention_ref, check_within_bound
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda"
+
+
+@pytest.fixture(scope="module", autouse=True)
+def _need_gpu():
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    import flash_attn_2_cuda  # noqa: F401
+
+
+def _ref(q, k, v, g, causal):
+    out = {}
+    for upcast, key in ((True, "ref"), (False, "pt")):
+        qr, kr, vr = (x.detach().clone().requires_grad_() for x in (q, k, v))
+        o, _ = attention_ref(qr, kr, vr, causal=causal, upcast=upcast, reorder_ops=not upcast)
+        out[key] = (o,) + tuple(torch.autograd.grad(o, (qr, kr, vr), g))
+    return out
+
+
+@pytest.mark.parametrize("persist", [1, 0])
+@pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float16])
+@pytest.mark.parametrize("causal", [False, True])
+@pytest.mark.parametrize("d", [64, 128])
+def test_varlen_sequences_without_keys(d, causal, dtype, persist):
+    from flash_attn import flash_attn_varlen_func
+
+    lens_q = [300, 5, 0, 257, 64, 700]
+    lens_k = [0, 130, 90, 0, 64, 333]
+    h, hk = 4, 2
+    torch.manual_seed(7)
+    cu_q = torch.tensor([0] + lens_q, dtype=torch.int64).cumsum(0).to(torch.int32).to(DEV)
+    cu_k = torch.tensor([0] + lens_k, dtype=torch.int64).cumsum(0).to(torch.int32).to(DEV)
+    q = torch.randn(sum(lens_q), h, d, device=DEV, dtype=dtype, requires_grad=True)
+    k, v = (torch.randn(sum(lens_k), hk, d, device=DEV, dtype=dtype, requires_grad=True) for _ in range(2))
+    with knob(FWD_PERSIST, persist):
+        out, lse, _ = flash_attn_varlen_func(q, k, v, cu_q, cu_k, max(lens_q), max(lens_k), causal=causal,
+                                             return_attn_probs=True)
+        g = torch.randn_like(out)
+        dq, dk, dv = torch.autograd.grad(out, (q, k, v), g)
+    torch.cuda.synchronize()
+    for name, t in (("out", out), ("lse", lse), ("dq", dq), ("dk", dk), ("dv", dv)):
+        assert not torch.isnan(t).any(), f"{name} has NaN"
+    for i, (lq, lk) in enumerate(zip(lens_q, lens_k)):
+        qa, qe, ka, ke = int(cu_q[i]), int(cu_q[i + 1]), int(cu_k[i]), int(cu_k[i + 1])
+        if lq and not lk:
+            # no keys: O = 0, LSE = +inf, no gradient
+            assert (out[qa:qe] == 0).all() and (dq[qa:qe] == 0).all(), f"sequence {i}: rows without keys"
+            assert torch.isinf(lse[i, :, :lq]).all() and (lse[i, :, :lq] > 0).all(), f"sequence {i}: lse"
+            continue
+        if lk and not lq:
+            assert (dk[ka:ke] == 0).all() and (dv[ka:ke] == 0).all(), f"sequence {i}: keys without rows"
+            continue
+        if not lq:
+            continue
+        sl = lambda t, a, e: t.detach()[a:e].unsqueeze(0)  # noqa: E731
+        r = _ref(sl(q, qa, qe), sl(k, ka, ke), sl(v, ka, ke), sl(g, qa, qe), causal)
+        for j, (name, got) in enumerate((("out", out[qa:qe]), ("dq", dq[qa:qe]), ("dk", dk[ka:ke]),
+                                         ("dv", dv[ka:ke]))):
+            ok, err, bound = check_within_bound(got.float(), r["ref"][j][0].float(), r["pt"][j][0].float(),
+                                                floor=1e-4)
+            assert ok, f"sequence {i} ({lq} rows, {lk} keys): {name} max|err| {err:.3e} > bound {bound:.3e}"
+        live = lse[i, :, :lq]
+        assert torch.isfinite(live).all() or causal, f"sequence {i}: lse not finite"
+        assert not math.isnan(float(live.float().sum()))
