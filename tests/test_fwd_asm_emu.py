@@ -57,6 +57,21 @@ def test_asm_forward_varlen_in_emulator(asm_text, seqs, h, hk, causal, bf16, d):
 
 
 @pytest.mark.timeout(600)
+@pytest.mark.parametrize("causal", [False, True])
+@pytest.mark.parametrize("bf16", [True, False])
+@pytest.mark.parametrize("d", [128, 64])
+def test_asm_forward_rows_without_keys_in_emulator(asm_text, d, bf16, causal):
+    """varlen sequences with query rows and no keys: items with no K/V tile reach the staged epilogue
+    without a tile 0 having set the ring position (round 6 fix: the staging region is pinned to slot
+    0; before it, the region came from a stale ring offset and its LDS writes fell outside the
+    allocation -- garbage rows on the GPU).  O = 0 and LSE = +inf there (checked in run_varlen)."""
+    eo, el = emu_fwd.run_varlen([300, 5, 257], [0, 130, 0], h=1, hk=1, causal=causal, bf16=bf16, text=asm_text,
+                                verbose=False, d=d)
+    assert eo <= (1.6e-2 if bf16 else 2e-3), eo
+    assert el <= 1e-5, el
+
+
+@pytest.mark.timeout(600)
 @pytest.mark.parametrize("b,sq,sk,h,hk,causal,bf16,grid", [
     (1, 600, 600, 2, 1, True, True, 1),      # one workgroup walks all 6 items: warm starts (>= 4 tiles)
     (1, 600, 600, 2, 1, True, True, 4),      # snake rounds: items 0-3, then 7, 6 / 5, 4 reversed

@@ -5,7 +5,7 @@ backward adds nothing for them; every other sequence is held to the 2x rule
 (tests/test_flash_attn.py:774-783).  At head dims 64 / 128 the rows without keys take the assembly
 forward's item start for an item with no K/V tiles (gen_fwd.py item_start): through the persistent
 device-built list and, with FLASH_ATTN_MI355X_FWD_PERSIST=0, one workgroup per item."""
-import math
+import random
 
 import pytest
 import torch
@@ -36,14 +36,32 @@ def _ref(q, k, v, g, causal):
 @pytest.mark.parametrize("persist", [1, 0])
 @pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float16])
 @pytest.mark.parametrize("causal", [False, True])
-@pytest.mark.parametrize("d", [64, 128])
+@pytest.mark.parametrize("d", [64, 128, 96])
 def test_varlen_sequences_without_keys(d, causal, dtype, persist):
+    _check([300, 5, 0, 257, 64, 700], [0, 130, 90, 0, 64, 333], 4, 2, d, causal, dtype, persist, 7)
+
+
+# seeded random cu_seqlens_q != cu_seqlens_k (zero-length entries on either side), GQA, head dims of
+# the assembly (64, 128) and HIP (96) paths
+@pytest.mark.parametrize("seed", range(48))
+def test_varlen_random_q_k_lengths(seed):
+    r = random.Random(5000 + seed)
+    n = r.randint(1, 5)
+    pick = lambda: r.choice([0, 1, r.randint(2, 130), r.randint(131, 700)])  # noqa: E731
+    lens_q, lens_k = [pick() for _ in range(n)], [pick() for _ in range(n)]
+    if sum(lens_q) == 0:
+        lens_q[0] = 33
+    if sum(lens_k) == 0:
+        lens_k[-1] = 41
+    hk = r.choice([1, 2])
+    _check(lens_q, lens_k, hk * r.choice([1, 2, 3]), hk, r.choice([64, 128, 128, 96]), r.random() < 0.5,
+           r.choice([torch.bfloat16, torch.float16]), 1, seed)
+
+
+def _check(lens_q, lens_k, h, hk, d, causal, dtype, persist, seed):
     from flash_attn import flash_attn_varlen_func
 
-    lens_q = [300, 5, 0, 257, 64, 700]
-    lens_k = [0, 130, 90, 0, 64, 333]
-    h, hk = 4, 2
-    torch.manual_seed(7)
+    torch.manual_seed(seed)
     cu_q = torch.tensor([0] + lens_q, dtype=torch.int64).cumsum(0).to(torch.int32).to(DEV)
     cu_k = torch.tensor([0] + lens_k, dtype=torch.int64).cumsum(0).to(torch.int32).to(DEV)
     q = torch.randn(sum(lens_q), h, d, device=DEV, dtype=dtype, requires_grad=True)
@@ -75,6 +93,5 @@ def test_varlen_sequences_without_keys(d, causal, dtype, persist):
             ok, err, bound = check_within_bound(got.float(), r["ref"][j][0].float(), r["pt"][j][0].float(),
                                                 floor=1e-4)
             assert ok, f"sequence {i} ({lq} rows, {lk} keys): {name} max|err| {err:.3e} > bound {bound:.3e}"
-        live = lse[i, :, :lq]
-        assert torch.isfinite(live).all() or causal, f"sequence {i}: lse not finite"
-        assert not math.isnan(float(live.float().sum()))
+        live = lse[i, :, :lq].detach()
+        assert torch.isfinite(live).all(), f"sequence {i}: lse not finite"

@@ -159,6 +159,10 @@ def run_varlen(seqs_q, seqs_k=None, h=2, hk=1, causal=True, bf16=True, seed=0, t
     eo = el = 0.0
     for i in range(b):
         lq, lk = seqs_q[i], seqs_k[i]
+        if lq and not lk:   # rows without keys: O = 0, LSE = +inf (flash_fwd_kernel.h:509-518)
+            eo = max(eo, float(np.nan_to_num(np.abs(o[cuq[i]:cuq[i + 1]]), nan=np.inf).max()))
+            el = max(el, 0.0 if np.all(lse[i, :, :lq] == np.inf) else np.inf)
+            continue
         if lq == 0 or lk == 0:
             continue
         o_ref, lse_ref = reference(qc[None, cuq[i]:cuq[i + 1]], kf[None, cuk[i]:cuk[i + 1]],

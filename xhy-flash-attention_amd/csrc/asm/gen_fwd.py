@@ -1308,7 +1308,10 @@ class K:
         for tile in range(4):
             ins += self.dma_tile_ops(f"c{tile}")
         ins += [I(f"s_branch {l_tile0}", BRANCH)]
-        ins += [label(l_nt), I("s_waitcnt vmcnt(0)", WAIT), I(f"s_branch {self.l_empty if OPT_T0ZERO else l_epi}", BRANCH)]
+        # an item with rows but no keys (a varlen sequence of length 0 in cu_seqlens_k): no tile 0 sets
+        # the ring position, so the staged epilogue's region (the last tile's slot) is pinned to slot 0
+        ins += [label(l_nt), I("s_waitcnt vmcnt(0)", WAIT), I(f"s_mov_b32 s{S_VOFF}, {VBASE + TILE}", SALU, wr=sr(S_VOFF)),
+                I(f"s_branch {self.l_empty if OPT_T0ZERO else l_epi}", BRANCH)]
         ins += [label(l_skip), I(f"s_add_u32 s{S_ROUND}, s{S_ROUND}, 1", SALU), I(f"s_branch {l_cold}", BRANCH)]
         if OPT_T0ZERO:   # an item with no tiles: O = 0 for its epilogue (no tile 0 zeroes it)
             ins += [label(self.l_empty)] + self.o_zero_ops() + [I(f"s_branch {l_epi}", BRANCH)]
