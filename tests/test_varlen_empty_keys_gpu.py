@@ -54,11 +54,13 @@ def test_varlen_random_q_k_lengths(seed):
     if sum(lens_k) == 0:
         lens_k[-1] = 41
     hk = r.choice([1, 2])
+    # max_seqlen_q / _k above the longest sequence, as a caller may pass (the grid covers more blocks)
+    slack = (r.choice([0, 0, 37, 300]), r.choice([0, 0, 64, 129]))
     _check(lens_q, lens_k, hk * r.choice([1, 2, 3]), hk, r.choice([64, 128, 128, 96]), r.random() < 0.5,
-           r.choice([torch.bfloat16, torch.float16]), 1, seed)
+           r.choice([torch.bfloat16, torch.float16]), 1, seed, slack)
 
 
-def _check(lens_q, lens_k, h, hk, d, causal, dtype, persist, seed):
+def _check(lens_q, lens_k, h, hk, d, causal, dtype, persist, seed, slack=(0, 0)):
     from flash_attn import flash_attn_varlen_func
 
     torch.manual_seed(seed)
@@ -67,7 +69,8 @@ def _check(lens_q, lens_k, h, hk, d, causal, dtype, persist, seed):
     q = torch.randn(sum(lens_q), h, d, device=DEV, dtype=dtype, requires_grad=True)
     k, v = (torch.randn(sum(lens_k), hk, d, device=DEV, dtype=dtype, requires_grad=True) for _ in range(2))
     with knob(FWD_PERSIST, persist):
-        out, lse, _ = flash_attn_varlen_func(q, k, v, cu_q, cu_k, max(lens_q), max(lens_k), causal=causal,
+        out, lse, _ = flash_attn_varlen_func(q, k, v, cu_q, cu_k, max(lens_q) + slack[0], max(lens_k) + slack[1],
+                                             causal=causal,
                                              return_attn_probs=True)
         g = torch.randn_like(out)
         dq, dk, dv = torch.autograd.grad(out, (q, k, v), g)
