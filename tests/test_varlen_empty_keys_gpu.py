@@ -1,7 +1,9 @@
 """Varlen calls with sequences that have query rows but no keys, or keys but no query rows
-(cu_seqlens_q != cu_seqlens_k with zero-length entries).  The reference's forward gives such rows
-O = 0 and LSE = +inf (n_block_max = 0, flash_fwd_kernel.h:509-518; block_info.h:14-31), and its
-backward adds nothing for them; every other sequence is held to the 2x rule
+(cu_seqlens_q != cu_seqlens_k with zero-length entries).  Rows without keys get O = 0 and
+LSE = +inf, the reference epilogue's values for an empty softmax (row sum 0,
+flash_fwd_kernel.h:509-518), and their backward adds nothing.  (The reference itself starts such a
+sequence's key loop at block -1, flash_fwd_kernel.h:300-303, and reads the rows before it: its
+result there is undefined.)  Every other sequence is held to the 2x rule
 (tests/test_flash_attn.py:774-783).  At head dims 64 / 128 the rows without keys take the assembly
 forward's item start for an item with no K/V tiles (gen_fwd.py item_start): through the persistent
 device-built list and, with FLASH_ATTN_MI355X_FWD_PERSIST=0, one workgroup per item."""
@@ -98,3 +100,20 @@ def _check(lens_q, lens_k, h, hk, d, causal, dtype, persist, seed, slack=(0, 0))
             assert ok, f"sequence {i} ({lq} rows, {lk} keys): {name} max|err| {err:.3e} > bound {bound:.3e}"
         live = lse[i, :, :lq].detach()
         assert torch.isfinite(live).all(), f"sequence {i}: lse not finite"
+
+
+# fixed-length calls with no keys (k / v of seqlen 0) or no query rows: refused with a RuntimeError.
+# The reference does not define them either: seqlen_q = 0 launches an empty grid (grid.x = 0,
+# flash_fwd_launch_template.h:21-61, a launch error) and seqlen_k = 0 starts its key loop at block -1
+# (flash_fwd_kernel.h:300-303), reading before K.  Empty tensors reach the C ABI as null pointers,
+# which it rejects (fa_capi.cpp fwd_impl).
+@pytest.mark.parametrize("sq,sk", [(37, 0), (0, 50), (0, 0)])
+@pytest.mark.parametrize("d", [64, 128, 96])
+def test_fixed_length_without_keys_or_rows_is_refused(sq, sk, d):
+    from flash_attn import flash_attn_func
+
+    q = torch.randn(2, sq, 4, d, device=DEV, dtype=torch.bfloat16)
+    k, v = (torch.randn(2, sk, 2, d, device=DEV, dtype=torch.bfloat16) for _ in range(2))
+    with pytest.raises(RuntimeError):
+        flash_attn_func(q, k, v, causal=True)
+    torch.cuda.synchronize()
