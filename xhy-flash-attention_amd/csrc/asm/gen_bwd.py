@@ -599,6 +599,10 @@ class K:
                 I("s_load_dwordx4 s[20:23], s[0:1], 0xb8", SMEM, rd=sr(0, 2), wr=sr(20, 4)),
                 I(f"s_load_dwordx2 s[{S_C}:{S_SCALE}], s[0:1], 0xc8", SMEM, rd=sr(0, 2), wr=sr(S_C, 2)),
                 I("s_load_dword s3, s[0:1], 0xd0", SMEM, rd=sr(0, 2), wr=sr(3)),
+                # the work order (fa_params.h ItemDecode) into s[36:45] (free until the geometry), in the
+                # same scalar-memory round trip as the kernargs: (bidb, hx, kvh, key block) of this item
+                I(f"s_load_dwordx8 s[36:43], s[0:1], {DEC_OFF}", SMEM),
+                I(f"s_load_dwordx2 s[44:45], s[0:1], {DEC_OFF + 32}", SMEM),
                 I("s_waitcnt lgkmcnt(0)", WAIT)]
         if OPT_STAMP:
             ins += [I(f"s_memtime s[{S_TMP + 1}:{S_TMP + 2}]", SMEM, wr=sr(S_TMP + 1, 2)),
@@ -616,11 +620,6 @@ class K:
         H, NG, NHS, GRP = 20, 21, 22, 23
         FLG = 3
         T0, T1, T2, T3, T4, T5, T6 = (S_TMP + i for i in range(7))
-        # the work order (fa_params.h ItemDecode) into s[36:45] (free until the geometry):
-        # (bidb, hx, kvh, key block) of this workgroup
-        ins += [I(f"s_load_dwordx8 s[36:43], s[0:1], {DEC_OFF}", SMEM),
-                I(f"s_load_dwordx2 s[44:45], s[0:1], {DEC_OFF + 32}", SMEM),
-                I("s_waitcnt lgkmcnt(0)", WAIT)]
         ins += substamp(V_SS + 11)
         BIDB, HX, KVH, KB = 24, 25, 26, 27      # S_N .. S_Q0V, set at the end
         # varlen with a device-built work list (flags bit 2, fa_fwd_asm.cpp varlen_items_kernel: the
