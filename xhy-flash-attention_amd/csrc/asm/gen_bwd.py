@@ -149,6 +149,7 @@ OPT_WIN = int(os.environ.get("FA_GBW_WIN", "16"))     # an A fragment may be rea
 # still reads: the scheduler orders fillers among themselves, the MFMA sequence only by earliest)
 assert 2 <= OPT_WIN <= 16, "FA_GBW_WIN must be within the 16-slot fragment ring"
 OPT_LEAD = int(os.environ.get("FA_GBW_LEAD", "2"))    # ... and at least LEAD MFMAs ahead
+OPT_DECBURST = os.environ.get("FA_GBW_DECBURST") == "1"
 # dev timeline: every workgroup stores {start, end} s_memtime, HW_ID, XCC_ID, id at the `stamps`
 # kernarg address + 32 id (tools/bwd_stamps.py)
 OPT_STAMP = os.environ.get("FA_GBW_STAMP") == "1"
@@ -599,11 +600,14 @@ class K:
                 I("s_load_dwordx4 s[20:23], s[0:1], 0xb8", SMEM, rd=sr(0, 2), wr=sr(20, 4)),
                 I(f"s_load_dwordx2 s[{S_C}:{S_SCALE}], s[0:1], 0xc8", SMEM, rd=sr(0, 2), wr=sr(S_C, 2)),
                 I("s_load_dword s3, s[0:1], 0xd0", SMEM, rd=sr(0, 2), wr=sr(3)),
-                # the work order (fa_params.h ItemDecode) into s[36:45] (free until the geometry), in the
-                # same scalar-memory round trip as the kernargs: (bidb, hx, kvh, key block) of this item
-                I(f"s_load_dwordx8 s[36:43], s[0:1], {DEC_OFF}", SMEM),
-                I(f"s_load_dwordx2 s[44:45], s[0:1], {DEC_OFF + 32}", SMEM),
                 I("s_waitcnt lgkmcnt(0)", WAIT)]
+        # the work order (fa_params.h ItemDecode) into s[36:45] (free until the geometry): (bidb, hx,
+        # kvh, key block) of this item; FA_GBW_DECBURST=1 (dev switch, off in the shipped build): in the
+        # kernargs' scalar round trip, one less per item
+        dec = [I(f"s_load_dwordx8 s[36:43], s[0:1], {DEC_OFF}", SMEM),
+               I(f"s_load_dwordx2 s[44:45], s[0:1], {DEC_OFF + 32}", SMEM)]
+        if OPT_DECBURST:
+            ins[-1:-1] = dec
         if OPT_STAMP:
             ins += [I(f"s_memtime s[{S_TMP + 1}:{S_TMP + 2}]", SMEM, wr=sr(S_TMP + 1, 2)),
                     I(f"s_getreg_b32 s{S_TMP + 3}, hwreg(HW_REG_HW_ID)", SALU, wr=sr(S_TMP + 3)),
@@ -620,6 +624,8 @@ class K:
         H, NG, NHS, GRP = 20, 21, 22, 23
         FLG = 3
         T0, T1, T2, T3, T4, T5, T6 = (S_TMP + i for i in range(7))
+        if not OPT_DECBURST:
+            ins += dec + [I("s_waitcnt lgkmcnt(0)", WAIT)]
         ins += substamp(V_SS + 11)
         BIDB, HX, KVH, KB = 24, 25, 26, 27      # S_N .. S_Q0V, set at the end
         # varlen with a device-built work list (flags bit 2, fa_fwd_asm.cpp varlen_items_kernel: the

@@ -64,6 +64,7 @@ OPT_WIN = int(os.environ.get("FA_GDQ_WIN", "16"))
 assert 2 <= OPT_WIN <= 16, "FA_GDQ_WIN must be within the 16-slot fragment ring"
 OPT_LEAD = int(os.environ.get("FA_GDQ_LEAD", "2"))
 OPT_OWAIT = int(os.environ.get("FA_GDQ_OWAIT", "23"))
+OPT_DECBURST = os.environ.get("FA_GDQ_DECBURST") == "1"
 
 # ---- AGPRs ----
 def DQ(j, dt):
@@ -368,12 +369,15 @@ class K:
                 I(f"s_load_dwordx16 s[{ka + 16}:{ka + 31}], s[0:1], 0x40", SMEM, rd=sr(0, 2), wr=sr(ka + 16, 16)),
                 I(f"s_load_dwordx8 s[{ka + 32}:{ka + 39}], s[0:1], 0x80", SMEM, rd=sr(0, 2), wr=sr(ka + 32, 8)),
                 I(f"s_load_dwordx4 s[{ka + 40}:{ka + 43}], s[0:1], 0xa0", SMEM, rd=sr(0, 2), wr=sr(ka + 40, 4)),
-                I(f"s_load_dwordx2 s[{S_C}:{S_SCALE}], s[0:1], 0xb0", SMEM, rd=sr(0, 2), wr=sr(S_C, 2)),
-                # the work order (fa_params.h ItemDecode) into s[40:49] (free until the geometry), in the
-                # same scalar-memory round trip as the kernargs
-                I(f"s_load_dwordx8 s[40:47], s[0:1], {DEC_OFF}", SMEM),
-                I(f"s_load_dwordx2 s[48:49], s[0:1], {DEC_OFF + 32}", SMEM),
                 I("s_waitcnt lgkmcnt(0)", WAIT)]
+        # the c / scale kernargs and the work order (fa_params.h ItemDecode) into s[40:49] (free until
+        # the geometry); FA_GDQ_DECBURST=1 (dev switch, off in the shipped build): with the kernargs,
+        # one scalar round trip less
+        late = [I(f"s_load_dwordx2 s[{S_C}:{S_SCALE}], s[0:1], 0xb0", SMEM, rd=sr(0, 2), wr=sr(S_C, 2)),
+                I(f"s_load_dwordx8 s[40:47], s[0:1], {DEC_OFF}", SMEM),
+                I(f"s_load_dwordx2 s[48:49], s[0:1], {DEC_OFF + 32}", SMEM)]
+        if OPT_DECBURST:
+            ins[-1:-1] = late
         P = lambda i: ka + i   # noqa: E731
         # dwords: 0 q, 2 k, 4 v, 6 dout, 8 dq, 10 lse, 12 dsum, 14 sched, 16 cu_q, 18 cu_k,
         # 20 q_batch, 22 kv_batch, 24 do_batch, 26 dq_batch (i64 bytes),
@@ -385,6 +389,8 @@ class K:
         SQ, SK, LP, DPt, NH, NHK, FLG = (P(37 + i) for i in range(7))
         T = [S_TMP + i for i in range(9)]
         ins += [I(f"v_mov_b32_e32 v1, s{S_WAVE}", VALU, rd=sr(S_WAVE), wr=vr(1))]     # (v0, v1: S^T tiles in the loop)
+        if not OPT_DECBURST:
+            ins = ins[:-1] + [late[0], ins[-1]] + late[1:] + [I("s_waitcnt lgkmcnt(0)", WAIT)]
         BIDB, HEAD, KVH, MB = S_N, S_NLAST, S_MASK0, S_KV32     # temporaries until the loop state
         ins += item_decode_ops(L=S_ITEM, M=40, pa=T[1], pb=T[3], t=T[5], u=T[6], o_blk=MB, reverse=True)
         ins += [I(f"s_mov_b32 s{BIDB}, s{T[3]}", SALU), I(f"s_mov_b32 s{HEAD}, s{T[6]}", SALU),

@@ -153,7 +153,11 @@ S_KA = 40         # kernarg block 40..84 (84: grid)
 S_C = S_KA + 41   # scale * log2(e) (kernarg)
 S_NITEMS = S_KA + 43
 S_GRID = S_KA + 44
-S_RNGD = S_KD     # rng_state store descriptor (4..7), written once in entry(), before the geometry
+# FA_GEN_DECBURST=1 (dev switch, off in the shipped build): the first item's ItemDecode comes with the
+# kernargs (one scalar round trip less per workgroup; profiles/r06/ab_*_decburst_r06s3.txt), so the
+# rng_state store descriptor moves off s[92:95]
+OPT_DECBURST = os.environ.get("FA_GEN_DECBURST") == "1"
+S_RNGD = S_KD if OPT_DECBURST else 92   # rng_state store descriptor, written once in entry(), before the geometry
 # persistent item loop: the NEXT item's descriptors (its K/V tiles are DMA'd into the ring while the
 # current item finishes, its Q is loaded in the current item's last step)
 S_QD2 = 56        # over the rng / seed / offset kernargs (dead after the rng store)
@@ -951,13 +955,14 @@ class K:
                 I(f"s_load_dwordx8 s[{ka + 16}:{ka + 23}], s[0:1], 0x40", SMEM, rd=sr(0, 2), wr=sr(ka + 16, 8)),
                 I(f"s_load_dwordx16 s[{ka + 24}:{ka + 39}], s[0:1], 0x60", SMEM, rd=sr(0, 2), wr=sr(ka + 24, 16)),
                 I(f"s_load_dwordx4 s[{ka + 40}:{ka + 43}], s[0:1], 0xa0", SMEM, rd=sr(0, 2), wr=sr(ka + 40, 4)),
-                I(f"s_load_dword s{S_GRID}, s[0:1], 0xb0", SMEM, rd=sr(0, 2), wr=sr(S_GRID)),
-                # the first item's work order (fa_params.h ItemDecode) in the same scalar-memory round
-                # trip: s[88:97] hold it until that item's geometry (item_geom skips its reload in
-                # round 0; later items reload it, the geometry reuses the registers)
-                I(f"s_load_dwordx8 s[88:95], s[0:1], {DEC_OFF}", SMEM, rd=sr(0, 2), wr=sr(88, 8)),
-                I(f"s_load_dwordx2 s[96:97], s[0:1], {DEC_OFF + 32}", SMEM, rd=sr(0, 2), wr=sr(96, 2)),
-                I("s_waitcnt lgkmcnt(0)", WAIT)]
+                I(f"s_load_dword s{S_GRID}, s[0:1], 0xb0", SMEM, rd=sr(0, 2), wr=sr(S_GRID))]
+        if OPT_DECBURST:
+            # the first item's work order (fa_params.h ItemDecode) in the same scalar-memory round
+            # trip: s[88:97] hold it until that item's geometry (item_geom skips its reload in
+            # round 0; later items reload it, the geometry reuses the registers)
+            ins += [I(f"s_load_dwordx8 s[88:95], s[0:1], {DEC_OFF}", SMEM, rd=sr(0, 2), wr=sr(88, 8)),
+                    I(f"s_load_dwordx2 s[96:97], s[0:1], {DEC_OFF + 32}", SMEM, rd=sr(0, 2), wr=sr(96, 2))]
+        ins += [I("s_waitcnt lgkmcnt(0)", WAIT)]
         T0 = S_TMP
         # varlen work list built on the device (flags bit 1): the item count is its first dword and
         # the entries start 8 bytes in
@@ -1123,14 +1128,14 @@ class K:
         # entry (bidb | head << 16, kvh | m_block << 16)
         l_tab, l_dec = self.lab("tab"), self.lab("dec")
         ins += [I(f"s_bitcmp1_b32 s{A['FL']}, 1", SALU), I(f"s_cbranch_scc1 {l_tab}", BRANCH)]
-        if kind == "cold":
+        if kind == "cold" and OPT_DECBURST:
             # round 0 (the workgroup's first item, entered from entry()): s[88:97] already hold it
             l_have = self.lab("decin")
             ins += [I(f"s_cmp_eq_u32 s{S_ROUND}, 0", SALU), I(f"s_cbranch_scc1 {l_have}", BRANCH)]
         ins += [I(f"s_load_dwordx8 s[88:95], s[0:1], {DEC_OFF}", SMEM),
                 I(f"s_load_dwordx2 s[96:97], s[0:1], {DEC_OFF + 32}", SMEM),
                 I("s_waitcnt lgkmcnt(0)", WAIT)]
-        if kind == "cold":
+        if kind == "cold" and OPT_DECBURST:
             ins += [label(l_have)]
         ins += item_decode_ops(L=S_SWT, M=88, pa=T0, pb=T2, t=S_N, u=S_M0R, o_blk=MB, reverse=True)
         ins += [I(f"s_mov_b32 s{HEAD}, s{S_M0R}", SALU), I(f"s_mov_b32 s{KVH}, s{T0}", SALU),
